@@ -1,0 +1,1051 @@
+/* ckoracle.c -- CPU ORACLE (test infrastructure only; see ckoracle.h).
+ *
+ * Chemistry: standard Chemkin-II gas kinetics (the closed libKINetics.so is not in the
+ * reference; its call sites are chemkin_wrapper.py:375-498 and mixture.py:1442,1551).
+ * Integrator: CVODE-style variable-order (1..5) variable-step BDF in Nordsieck form with a
+ * modified Newton corrector and dense partial-pivot LU, i.e. the DASPK/DASSL-class method
+ * family the reference's KINAll0D_Calculate uses.  Ignition
+ * definitions follow ChemkinKeywordTips.yaml:184-199 (TIFP, DTIGN, TLIM, KLIM) and the
+ * defaults of batchreactor.py:91-92,296.
+ */
+#include "ckoracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define BOLTZMANN 1.3806504e-16
+#define AVOGADRO 6.02214179e23
+#define RU (BOLTZMANN * AVOGADRO)
+#define PATM 1.01325e6
+#define NMAX 512
+
+/* ------------------------------------------------------------------ thermo */
+void cko_thermo(const cko_mech* m, double T, double* cp_R, double* h_RT, double* s_R) {
+  const double lnT = log(T), T2 = T * T, T3 = T2 * T, T4 = T3 * T;
+  for (int k = 0; k < m->KK; ++k) {
+    const double* th = m->thermo + 17 * k;
+    const double* a = (T > th[1]) ? th + 10 : th + 3;
+    if (cp_R) cp_R[k] = a[0] + a[1] * T + a[2] * T2 + a[3] * T3 + a[4] * T4;
+    if (h_RT) h_RT[k] = a[0] + a[1] * T / 2 + a[2] * T2 / 3 + a[3] * T3 / 4 + a[4] * T4 / 5 + a[5] / T;
+    if (s_R) s_R[k] = a[0] * lnT + a[1] * T + a[2] * T2 / 2 + a[3] * T3 / 3 + a[4] * T4 / 4 + a[6];
+  }
+}
+
+static double powi_nu(double c, double nu) {
+  if (nu == 1.0) return c;
+  if (nu == 2.0) return c * c;
+  if (nu == 3.0) return c * c * c;
+  return pow(c, nu);
+}
+
+/* Per-reaction kinetics at (T, C[]).  Returns kf_eff (incl. falloff), kr_eff, the
+ * third-body factor (1 if none), Pi_f, Pi_r, and d ln kf / dT, d ln kr / dT. */
+typedef struct {
+  double kf, kr, mfac, pf, pr, dlkf, dlkr;
+} rxn_eval;
+
+static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, const double* C,
+                          double Ctot, const double* g_RT, const double* h_RT, rxn_eval* e) {
+  const double* a = m->arr + 3 * i;
+  double kf = exp(a[0] + a[1] * lnT - a[2] * invT);
+  double dlkf = (a[1] + a[2] * invT) * invT;
+  double mfac = 1.0;
+  const int type = m->rtype[i];
+  if (type == 1 || type == 2) {
+    double M;
+    if (m->tbsp[i] >= 0) {
+      M = C[m->tbsp[i]];
+    } else {
+      M = Ctot;
+      for (int p = m->eff_ptr[i]; p < m->eff_ptr[i + 1]; ++p) M += (m->eff_val[p] - 1.0) * C[m->eff_sp[p]];
+    }
+    if (type == 1) {
+      mfac = M;
+    } else {
+      const double* l = m->low + 3 * i;
+      double k0 = exp(l[0] + l[1] * lnT - l[2] * invT);
+      double Pr = k0 * M / kf;
+      double F = 1.0;
+      const int ft = m->ftype[i];
+      const double* fp = m->fpar + 5 * i;
+      if (ft == 2 || ft == 3) {
+        double Fcent = (1.0 - fp[0]) * exp(-T / fp[1]) + fp[0] * exp(-T / fp[2]);
+        if (ft == 3) Fcent += exp(-fp[3] * invT);
+        double lFc = log10(Fcent > 1e-300 ? Fcent : 1e-300);
+        double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
+        double c = -0.4 - 0.67 * lFc, nn = 0.75 - 1.27 * lFc;
+        double f1 = (lPr + c) / (nn - 0.14 * (lPr + c));
+        F = pow(10.0, lFc / (1.0 + f1 * f1));
+      } else if (ft == 4) {
+        double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
+        double X = 1.0 / (1.0 + lPr * lPr);
+        F = fp[3] * pow(fp[0] * exp(-fp[1] * invT) + exp(-T / fp[2]), X) * pow(T, fp[4]);
+      }
+      kf = kf * (Pr / (1.0 + Pr)) * F;
+    }
+  }
+  double kr = 0.0, dlkr = 0.0;
+  if (m->rev[i]) {
+    if (m->has_rev[i]) {
+      const double* r = m->revp + 3 * i;
+      kr = exp(r[0] + r[1] * lnT - r[2] * invT);
+      if (type == 2) kr *= kf / exp(a[0] + a[1] * lnT - a[2] * invT);
+      dlkr = (r[1] + r[2] * invT) * invT;
+    } else {
+      double dG = 0.0, dH = 0.0, dnu = 0.0;
+      for (int s = 0; s < m->nr[i]; ++s) {
+        int k = m->rsp[CKO_SLOTS * i + s];
+        double nu = m->rnu[CKO_SLOTS * i + s];
+        dG -= nu * g_RT[k]; dH -= nu * h_RT[k]; dnu -= nu;
+      }
+      for (int s = 0; s < m->np[i]; ++s) {
+        int k = m->psp[CKO_SLOTS * i + s];
+        double nu = m->pnu[CKO_SLOTS * i + s];
+        dG += nu * g_RT[k]; dH += nu * h_RT[k]; dnu += nu;
+      }
+      /* Kc = exp(-dG) (PATM/RT)^dnu ; kr = kf / Kc */
+      kr = kf * exp(dG - dnu * log(PATM / (RU * T)));
+      dlkr = dlkf - (dH - dnu) * invT;
+    }
+  }
+  double pf = 1.0, pr = 1.0;
+  for (int s = 0; s < m->nr[i]; ++s) pf *= powi_nu(C[m->rsp[CKO_SLOTS * i + s]], m->rnu[CKO_SLOTS * i + s]);
+  for (int s = 0; s < m->np[i]; ++s) pr *= powi_nu(C[m->psp[CKO_SLOTS * i + s]], m->pnu[CKO_SLOTS * i + s]);
+  e->kf = kf; e->kr = kr; e->mfac = mfac; e->pf = pf; e->pr = pr; e->dlkf = dlkf; e->dlkr = dlkr;
+}
+
+static void conc_from_Y(const cko_mech* m, double rho, const double* Y, int nneg, double* C, double* Ctot) {
+  double s = 0.0;
+  for (int k = 0; k < m->KK; ++k) {
+    double y = Y[k];
+    if (nneg && y < 0.0) y = 0.0;
+    C[k] = rho * y / m->wt[k];
+    s += C[k];
+  }
+  *Ctot = s;
+}
+
+static double mean_wt(const cko_mech* m, const double* Y) {
+  double s = 0.0;
+  for (int k = 0; k < m->KK; ++k) s += Y[k] / m->wt[k];
+  return 1.0 / s;
+}
+
+void cko_rates(const cko_mech* m, double T, double P, const double* Y, double* qf, double* qr, double* wdot) {
+  const int KK = m->KK;
+  double C[NMAX], h_RT[NMAX], s_R[NMAX], g_RT[NMAX], Ctot;
+  double rho = P * mean_wt(m, Y) / (RU * T);
+  conc_from_Y(m, rho, Y, 0, C, &Ctot);
+  cko_thermo(m, T, NULL, h_RT, s_R);
+  for (int k = 0; k < KK; ++k) g_RT[k] = h_RT[k] - s_R[k];
+  if (wdot) memset(wdot, 0, sizeof(double) * KK);
+  const double lnT = log(T), invT = 1.0 / T;
+  for (int i = 0; i < m->II; ++i) {
+    rxn_eval e;
+    eval_reaction(m, i, T, lnT, invT, C, Ctot, g_RT, h_RT, &e);
+    double f = e.mfac * e.kf * e.pf, r = e.mfac * e.kr * e.pr;
+    if (qf) qf[i] = f;
+    if (qr) qr[i] = r;
+    if (wdot) {
+      double q = f - r;
+      for (int s = 0; s < m->nr[i]; ++s) wdot[m->rsp[CKO_SLOTS * i + s]] -= m->rnu[CKO_SLOTS * i + s] * q;
+      for (int s = 0; s < m->np[i]; ++s) wdot[m->psp[CKO_SLOTS * i + s]] += m->pnu[CKO_SLOTS * i + s] * q;
+    }
+  }
+}
+
+void cko_rop_batch(const cko_mech* m, int n, const double* T, const double* P, const double* Y, double* wdot,
+                   double* cp, double* h, int nthreads) {
+  const int KK = m->KK;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+  for (int s = 0; s < n; ++s) {
+    double Ys[NMAX], cp_R[NMAX], h_RT[NMAX];
+    for (int k = 0; k < KK; ++k) Ys[k] = Y[(size_t)k * n + s]; /* SoA input Y[KK][n] */
+    double w[NMAX];
+    cko_rates(m, T[s], P[s], Ys, NULL, NULL, w);
+    for (int k = 0; k < KK; ++k) wdot[(size_t)k * n + s] = w[k];
+    cko_thermo(m, T[s], cp_R, h_RT, NULL);
+    double c = 0.0, hh = 0.0;
+    for (int k = 0; k < KK; ++k) {
+      c += Ys[k] * cp_R[k] * RU / m->wt[k];
+      hh += Ys[k] * h_RT[k] * RU * T[s] / m->wt[k];
+    }
+    cp[s] = c;
+    h[s] = hh;
+  }
+}
+
+/* --------------------------------------------------------- reactor model */
+typedef struct {
+  const cko_mech* m;
+  const cko_cfg* cfg;
+  int problem;
+  double mass_density0; /* rho0 (CONV: density at V0) */
+  double V0, P0, T0;
+  int nfe, nje;
+} rctx;
+
+static void profile_eval(const cko_cfg* c, double t, double base, double* v, double* dvdt) {
+  if (c->nprof <= 0) { *v = base; *dvdt = 0.0; return; }
+  const double* x = c->prof_t;
+  const double* y = c->prof_v;
+  int n = c->nprof;
+  if (t <= x[0]) { *v = y[0]; *dvdt = 0.0; return; }
+  if (t >= x[n - 1]) { *v = y[n - 1]; *dvdt = 0.0; return; }
+  int j = 0;
+  while (j < n - 2 && t >= x[j + 1]) ++j;
+  double s = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
+  *v = y[j] + s * (t - x[j]);
+  *dvdt = s;
+}
+
+/* f = dy/dt for y = (T, Y_1..Y_KK); J (n x n row-major, optional) = approximate analytic Jacobian */
+static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J) {
+  const cko_mech* m = c->m;
+  const int KK = m->KK, n = KK + 1;
+  const double T = y[0];
+  const double* Y = y + 1;
+  double C[NMAX], cp_R[NMAX], h_RT[NMAX], s_R[NMAX], g_RT[NMAX], Ctot;
+  double rho, P, V, dVdt = 0.0, dPdt = 0.0;
+  const int conp = (c->problem == 1);
+  double Wbar = mean_wt(m, Y);
+  if (conp) {
+    profile_eval(c->cfg, t, c->P0, &P, &dPdt);
+    rho = P * Wbar / (RU * T);
+    V = c->mass_density0 * c->V0 / rho;
+  } else {
+    profile_eval(c->cfg, t, c->V0, &V, &dVdt);
+    rho = c->mass_density0 * c->V0 / V;
+    P = rho * RU * T / Wbar;
+  }
+  conc_from_Y(m, rho, Y, 0, C, &Ctot);
+  cko_thermo(m, T, cp_R, h_RT, s_R);
+  for (int k = 0; k < KK; ++k) g_RT[k] = h_RT[k] - s_R[k];
+  double wdot[NMAX];
+  memset(wdot, 0, sizeof(double) * KK);
+  double dwdT[NMAX];
+  if (J) {
+    memset(J, 0, sizeof(double) * n * n);
+    memset(dwdT, 0, sizeof(double) * KK);
+  }
+  const double lnT = log(T), invT = 1.0 / T;
+  for (int i = 0; i < m->II; ++i) {
+    rxn_eval e;
+    eval_reaction(m, i, T, lnT, invT, C, Ctot, g_RT, h_RT, &e);
+    const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
+    const int* rs = m->rsp + CKO_SLOTS * i;
+    const int* ps = m->psp + CKO_SLOTS * i;
+    const double* rn = m->rnu + CKO_SLOTS * i;
+    const double* pn = m->pnu + CKO_SLOTS * i;
+    for (int s = 0; s < m->nr[i]; ++s) wdot[rs[s]] -= rn[s] * q;
+    for (int s = 0; s < m->np[i]; ++s) wdot[ps[s]] += pn[s] * q;
+    if (!J) continue;
+    /* dq/dT at fixed C, then at fixed (Y, P) for CONP */
+    double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
+    if (conp) {
+      double ordf = 0.0, ordr = 0.0;
+      for (int s = 0; s < m->nr[i]; ++s) ordf += rn[s];
+      for (int s = 0; s < m->np[i]; ++s) ordr += pn[s];
+      dqdT -= e.mfac * (ordf * e.kf * e.pf - ordr * e.kr * e.pr) * invT;
+      if (m->rtype[i] == 1) dqdT -= q * invT;
+    }
+    for (int s = 0; s < m->nr[i]; ++s) dwdT[rs[s]] -= rn[s] * dqdT;
+    for (int s = 0; s < m->np[i]; ++s) dwdT[ps[s]] += pn[s] * dqdT;
+    /* dq/dC_j over reactant and product slots */
+    for (int side = 0; side < 2; ++side) {
+      const int nsl = side == 0 ? m->nr[i] : m->np[i];
+      const int* sp = side == 0 ? rs : ps;
+      const double* nu = side == 0 ? rn : pn;
+      const double kk = side == 0 ? e.mfac * e.kf : -e.mfac * e.kr;
+      if (kk == 0.0) continue;
+      for (int s = 0; s < nsl; ++s) {
+        double d = nu[s] * powi_nu(C[sp[s]], nu[s] - 1.0);
+        for (int u = 0; u < nsl; ++u)
+          if (u != s) d *= powi_nu(C[sp[u]], nu[u]);
+        const double dq = kk * d;
+        const int j = sp[s];
+        const double wj = 1.0 / m->wt[j];
+        for (int u = 0; u < m->nr[i]; ++u) J[(1 + rs[u]) * n + 1 + j] -= rn[u] * dq * m->wt[rs[u]] * wj;
+        for (int u = 0; u < m->np[i]; ++u) J[(1 + ps[u]) * n + 1 + j] += pn[u] * dq * m->wt[ps[u]] * wj;
+      }
+    }
+  }
+  /* species equations */
+  const double rinv = 1.0 / rho;
+  for (int k = 0; k < KK; ++k) f[1 + k] = wdot[k] * m->wt[k] * rinv;
+  /* energy equation */
+  if (c->cfg->energy == 1) {
+    double cpm = 0.0, sum = 0.0, e_k[NMAX], c_k[NMAX];
+    for (int k = 0; k < KK; ++k) {
+      const double cpk = cp_R[k] * RU / m->wt[k];              /* erg/g-K */
+      const double hk = h_RT[k] * RU * T / m->wt[k];            /* erg/g   */
+      c_k[k] = conp ? cpk : cpk - RU / m->wt[k];
+      e_k[k] = conp ? hk : hk - RU * T / m->wt[k];
+      cpm += Y[k] * c_k[k];
+      sum += e_k[k] * f[1 + k];
+    }
+    double fT = -sum / cpm;
+    if (conp) fT += dPdt / (rho * cpm);
+    else fT -= P * dVdt / (V * rho * cpm);
+    f[0] = fT;
+    if (J) {
+      for (int k = 0; k < KK; ++k) J[(1 + k) * n] = dwdT[k] * m->wt[k] * rinv + (conp ? f[1 + k] * invT : 0.0);
+      for (int j = 0; j < KK; ++j) {
+        double s = 0.0;
+        for (int k = 0; k < KK; ++k) s += e_k[k] * J[(1 + k) * n + 1 + j];
+        J[1 + j] = -s / cpm - fT * c_k[j] / cpm;
+      }
+      double s = 0.0;
+      for (int k = 0; k < KK; ++k) s += c_k[k] * f[1 + k] + e_k[k] * J[(1 + k) * n];
+      J[0] = -s / cpm;
+    }
+  } else {
+    f[0] = 0.0;
+    if (J) {
+      for (int k = 0; k < KK; ++k) J[(1 + k) * n] = dwdT[k] * m->wt[k] * rinv + (conp ? f[1 + k] * invT : 0.0);
+    }
+  }
+  c->nfe++;
+  if (J) c->nje++;
+}
+
+void cko_rhs_jac(const cko_mech* m, const cko_cfg* cfg, double t, const double* y, double mass_density0,
+                 double V0, double P0, double* f, double* J) {
+  rctx c = {m, cfg, cfg->problem, mass_density0, V0, P0, y[0], 0, 0};
+  reactor_rhs(&c, t, y, f, J);
+}
+
+/* ---------------------------------------------------------- dense LU */
+static int lu_factor(int n, double* A, int* piv) {
+  for (int k = 0; k < n; ++k) {
+    int p = k;
+    double amax = fabs(A[k * n + k]);
+    for (int i = k + 1; i < n; ++i)
+      if (fabs(A[i * n + k]) > amax) { amax = fabs(A[i * n + k]); p = i; }
+    piv[k] = p;
+    if (amax == 0.0) return k + 1;
+    if (p != k)
+      for (int j = 0; j < n; ++j) { double t = A[k * n + j]; A[k * n + j] = A[p * n + j]; A[p * n + j] = t; }
+    const double r = 1.0 / A[k * n + k];
+    for (int i = k + 1; i < n; ++i) {
+      const double l = A[i * n + k] * r;
+      A[i * n + k] = l;
+      if (l != 0.0)
+        for (int j = k + 1; j < n; ++j) A[i * n + j] -= l * A[k * n + j];
+    }
+  }
+  return 0;
+}
+
+static void lu_solve(int n, const double* A, const int* piv, double* b) {
+  /* whole rows (multipliers included) were swapped during the factorization, so the
+   * permutation is applied to b in full before the unit-lower forward sweep */
+  for (int k = 0; k < n; ++k) {
+    const int p = piv[k];
+    if (p != k) { double t = b[k]; b[k] = b[p]; b[p] = t; }
+  }
+  for (int k = 0; k < n; ++k)
+    for (int i = k + 1; i < n; ++i) b[i] -= A[i * n + k] * b[k];
+  for (int k = n - 1; k >= 0; --k) {
+    double s = b[k];
+    for (int j = k + 1; j < n; ++j) s -= A[k * n + j] * b[j];
+    b[k] = s / A[k * n + k];
+  }
+}
+
+/* ------------------------------------------------------ BDF integrator */
+#define QMAX 5
+#define L_MAX (QMAX + 1)
+#define ETAMX1 10000.0
+#define ETAMX2 10.0
+#define ETAMX3 10.0
+#define ETAMXF 0.2
+#define ETAMIN 0.1
+#define ETACF 0.25
+#define ADDON 1e-6
+#define BIAS1 6.0
+#define BIAS2 6.0
+#define BIAS3 10.0
+#define ONEPSM 1.000001
+#define SMALL_NST 10
+#define MXNCF 10
+#define MXNEF 7
+#define MXNEF1 3
+#define SMALL_NEF 2
+#define LONG_WAIT 10
+#define MAXCOR 3
+#define CRDOWN 0.3
+#define DGMAX 0.3
+#define RDIV 2.0
+#define MSBP 20
+#define MSBJ 50
+#define THRESH 1.5
+#define CORTES 0.1
+#define UROUND 2.220446049250313e-16
+#define NNEG_TOL 0.01
+
+
+typedef struct {
+  int n;
+  double zn[QMAX + 1][NMAX];
+  double ewt[NMAX], acor[NMAX], tempv[NMAX], ftemp[NMAX], y[NMAX];
+  double* J; /* saved Jacobian n*n */
+  double* M; /* LU of I - gamma J */
+  int piv[NMAX];
+  double tau[QMAX + 2], tq[6], l[QMAX + 1];
+  double h, hprime, hscale, eta, etamax, hmin, hmax_inv, tn, rl1, gamma, gammap, gamrat, crate, acnrm, hu;
+  double saved_tq5;
+  int q, qprime, qwait, L, nst, nstlp, nstlj, jcur, nscon, ncf_tot, nef_tot, nlu;
+  double rtol, atol;
+  int nneg;
+  rctx* ctx;
+} bdf;
+
+static double wrms(const bdf* b, const double* v) {
+  double s = 0.0;
+  for (int i = 0; i < b->n; ++i) { double x = v[i] * b->ewt[i]; s += x * x; }
+  return sqrt(s / b->n);
+}
+
+static void set_ewt(bdf* b, const double* y) {
+  for (int i = 0; i < b->n; ++i) b->ewt[i] = 1.0 / (b->rtol * fabs(y[i]) + b->atol);
+}
+
+static void rescale(bdf* b) {
+  double factor = b->eta;
+  for (int j = 1; j <= b->q; ++j) {
+    for (int i = 0; i < b->n; ++i) b->zn[j][i] *= factor;
+    factor *= b->eta;
+  }
+  b->h = b->hscale * b->eta;
+  b->hscale = b->h;
+  b->nscon = 0;
+}
+
+static void predict(bdf* b) {
+  b->tn += b->h;
+  for (int k = 1; k <= b->q; ++k)
+    for (int j = b->q; j >= k; --j)
+      for (int i = 0; i < b->n; ++i) b->zn[j - 1][i] += b->zn[j][i];
+}
+
+static void restore(bdf* b, double saved_t) {
+  b->tn = saved_t;
+  for (int k = 1; k <= b->q; ++k)
+    for (int j = b->q; j >= k; --j)
+      for (int i = 0; i < b->n; ++i) b->zn[j - 1][i] -= b->zn[j][i];
+}
+
+static void set_bdf(bdf* b) {
+  const int q = b->q;
+  double* l = b->l;
+  double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = b->h;
+  l[0] = l[1] = 1.0;
+  for (int i = 2; i <= QMAX; ++i) l[i] = 0.0;
+  if (q > 1) {
+    for (int j = 2; j < q; ++j) {
+      hsum += b->tau[j - 1];
+      xi_inv = b->h / hsum;
+      alpha0 -= 1.0 / j;
+      for (int i = j; i >= 1; --i) l[i] += l[i - 1] * xi_inv;
+    }
+    alpha0 -= 1.0 / q;
+    xistar_inv = -l[1] - alpha0;
+    hsum += b->tau[q - 1];
+    xi_inv = b->h / hsum;
+    alpha0_hat = -l[1] - xi_inv;
+    for (int i = q; i >= 1; --i) l[i] += l[i - 1] * xistar_inv;
+  }
+  const double A1 = 1.0 - alpha0_hat + alpha0;
+  const double A2 = 1.0 + q * A1;
+  b->tq[2] = fabs(A1 / (alpha0 * A2));
+  b->tq[5] = fabs(A2 * xistar_inv / (l[q] * xi_inv));
+  if (b->qwait == 1) {
+    if (q > 1) {
+      const double Cc = xistar_inv / l[q];
+      const double A3 = alpha0 + 1.0 / q;
+      const double A4 = alpha0_hat + xi_inv;
+      const double Cpinv = (1.0 - A4 + A3) / A3;
+      b->tq[1] = fabs(Cc * Cpinv);
+    } else {
+      b->tq[1] = 1.0;
+    }
+    hsum += b->tau[q];
+    xi_inv = b->h / hsum;
+    const double A5 = alpha0 - 1.0 / (q + 1);
+    const double A6 = alpha0_hat - xi_inv;
+    const double Cppinv = (1.0 - A6 + A5) / A2;
+    b->tq[3] = fabs(Cppinv / (xi_inv * (q + 2) * A5));
+  }
+  b->tq[4] = CORTES / b->tq[2];
+  b->rl1 = 1.0 / l[1];
+  b->gamma = b->h * b->rl1;
+  if (b->nst == 0) b->gammap = b->gamma;
+  b->gamrat = (b->nst > 0) ? b->gamma / b->gammap : 1.0;
+}
+
+static void adjust_order(bdf* b, int deltaq) {
+  const int q = b->q;
+  double* l = b->l;
+  for (int i = 0; i <= QMAX; ++i) l[i] = 0.0;
+  l[2] = 1.0;
+  if (deltaq == 1) {
+    double alpha1 = 1.0, prod = 1.0, xiold = 1.0, alpha0 = -1.0, hsum = b->hscale;
+    for (int j = 1; j < q; ++j) {
+      hsum += b->tau[j + 1];
+      const double xi = hsum / b->hscale;
+      prod *= xi;
+      alpha0 -= 1.0 / (j + 1);
+      alpha1 += 1.0 / xi;
+      for (int i = j + 2; i >= 2; --i) l[i] = l[i] * xiold + l[i - 1];
+      xiold = xi;
+    }
+    const double A1 = (-alpha0 - alpha1) / prod;
+    const int L = q + 1;
+    for (int i = 0; i < b->n; ++i) b->zn[L][i] = A1 * b->zn[QMAX][i];
+    for (int j = 2; j <= q; ++j)
+      for (int i = 0; i < b->n; ++i) b->zn[j][i] += l[j] * b->zn[L][i];
+  } else {
+    double hsum = 0.0;
+    for (int j = 1; j <= q - 2; ++j) {
+      hsum += b->tau[j];
+      const double xi = hsum / b->hscale;
+      for (int i = j + 2; i >= 2; --i) l[i] = l[i] * xi + l[i - 1];
+    }
+    for (int j = 2; j < q; ++j)
+      for (int i = 0; i < b->n; ++i) b->zn[j][i] -= l[j] * b->zn[q][i];
+  }
+}
+
+enum { NF_FIRST = 0, NF_CONV_FAIL = 1, NF_ERR_FAIL = 2 };
+enum { CF_NONE = 0, CF_BAD_J = 1, CF_OTHER = 2 };
+
+/* modified Newton corrector: 0 converged, 1 convergence failure */
+static int nls(bdf* b, int nflag) {
+  const int n = b->n;
+  int convfail = (nflag == NF_FIRST || nflag == NF_ERR_FAIL) ? CF_NONE : CF_OTHER;
+  int call_setup = (nflag != NF_FIRST) || b->nst == 0 || b->nst >= b->nstlp + MSBP || fabs(b->gamrat - 1.0) > DGMAX;
+  for (;;) {
+    for (int i = 0; i < n; ++i) b->y[i] = b->zn[0][i];
+    reactor_rhs(b->ctx, b->tn, b->y, b->ftemp, NULL);
+    if (call_setup) {
+      const double dgamma = fabs(b->gamma / b->gammap - 1.0);
+      const int jbad = b->nst == 0 || b->nst >= b->nstlj + MSBJ || (convfail == CF_BAD_J && dgamma < DGMAX) ||
+                       convfail == CF_OTHER;
+      if (jbad) {
+        double* fdum = b->tempv;
+        reactor_rhs(b->ctx, b->tn, b->y, fdum, b->J);
+        b->nstlj = b->nst;
+        b->jcur = 1;
+      } else {
+        b->jcur = 0;
+      }
+      for (int i = 0; i < n * n; ++i) b->M[i] = -b->gamma * b->J[i];
+      for (int i = 0; i < n; ++i) b->M[i * n + i] += 1.0;
+      const int sing = lu_factor(n, b->M, b->piv);
+      b->nlu++;
+      b->crate = 1.0;
+      b->gammap = b->gamma;
+      b->gamrat = 1.0;
+      b->nstlp = b->nst;
+      if (sing) return 1;
+    }
+    for (int i = 0; i < n; ++i) b->acor[i] = 0.0;
+    double delp = 0.0;
+    int mm = 0;
+    int failed = 0;
+    for (;;) {
+      for (int i = 0; i < n; ++i) b->tempv[i] = b->gamma * b->ftemp[i] - (b->rl1 * b->zn[1][i] + b->acor[i]);
+      lu_solve(n, b->M, b->piv, b->tempv);
+      if (b->gamrat != 1.0) {
+        const double s = 2.0 / (1.0 + b->gamrat);
+        for (int i = 0; i < n; ++i) b->tempv[i] *= s;
+      }
+      const double del = wrms(b, b->tempv);
+      for (int i = 0; i < n; ++i) {
+        b->acor[i] += b->tempv[i];
+        b->y[i] = b->zn[0][i] + b->acor[i];
+      }
+      if (mm > 0) b->crate = fmax(CRDOWN * b->crate, del / delp);
+      const double dcon = del * fmin(1.0, b->crate) / b->tq[4];
+      if (dcon <= 1.0) {
+        if (b->nneg) {
+          /* DASSL-style non-negativity: a large negative excursion is a failure, a small one is projected */
+          double s = 0.0;
+          int neg = 0;
+          for (int i = 1; i < n; ++i)
+            if (b->y[i] < 0.0) { const double x = b->y[i] * b->ewt[i]; s += x * x; neg = 1; }
+          if (neg) {
+            if (sqrt(s / n) > NNEG_TOL) { failed = 2; break; }
+            for (int i = 1; i < n; ++i)
+              if (b->y[i] < 0.0) { b->y[i] = 0.0; b->acor[i] = -b->zn[0][i]; }
+            b->acnrm = wrms(b, b->acor);
+            b->jcur = 0;
+            return 0;
+          }
+        }
+        b->acnrm = (mm == 0) ? del : wrms(b, b->acor);
+        b->jcur = 0;
+        return 0;
+      }
+      mm++;
+      if (mm == MAXCOR || (mm >= 2 && del > RDIV * delp)) { failed = 1; break; }
+      delp = del;
+      reactor_rhs(b->ctx, b->tn, b->y, b->ftemp, NULL);
+    }
+    if (failed == 1 && !b->jcur) {
+      convfail = CF_BAD_J;
+      call_setup = 1;
+      continue;
+    }
+    return 1;
+  }
+}
+
+static double dky0(const bdf* b, double t, int comp) {
+  const double s = (t - b->tn) / b->h;
+  double v = b->zn[b->q][comp];
+  for (int j = b->q - 1; j >= 0; --j) v = b->zn[j][comp] + s * v;
+  return v;
+}
+
+static void dky_vec(const bdf* b, double t, double* out) {
+  const double s = (t - b->tn) / b->h;
+  for (int i = 0; i < b->n; ++i) {
+    double v = b->zn[b->q][i];
+    for (int j = b->q - 1; j >= 0; --j) v = b->zn[j][i] + s * v;
+    out[i] = v;
+  }
+}
+
+/* initial step size, CVODE cvHin-style */
+static double initial_step(bdf* b, double tout) {
+  const int n = b->n;
+  const double t0 = b->tn;
+  const double tdist = fabs(tout - t0);
+  const double tround = UROUND * fmax(fabs(t0), fabs(tout));
+  const double hlb = 100.0 * tround;
+  double hub = 0.1 * tdist;
+  double hub_inv = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double num = fabs(b->zn[1][i]);
+    const double den = 0.1 * fabs(b->zn[0][i]) + b->atol;
+    const double r = num / (den > 0 ? den : 1e-300);
+    if (r > hub_inv) hub_inv = r;
+  }
+  if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
+  double hg = sqrt(hlb * hub);
+  if (hub < hlb) return hg;
+  double hnew = hg;
+  double y1[NMAX], f1[NMAX];
+  for (int count = 1; count <= 4; ++count) {
+    /* ydd norm */
+    for (int i = 0; i < n; ++i) y1[i] = b->zn[0][i] + hg * b->zn[1][i];
+    reactor_rhs(b->ctx, t0 + hg, y1, f1, NULL);
+    for (int i = 0; i < n; ++i) f1[i] = (f1[i] - b->zn[1][i]) / hg;
+    const double yddnrm = wrms(b, f1);
+    hnew = (yddnrm * hub * hub > 2.0) ? sqrt(2.0 / yddnrm) : sqrt(hg * hub);
+    if (count == 4) break;
+    const double hrat = hnew / hg;
+    if (hrat > 0.5 && hrat < 2.0) break;
+    if (count >= 2 && hrat > 2.0) { hnew = hg; break; }
+    hg = hnew;
+  }
+  double h0 = 0.5 * hnew;
+  if (h0 < hlb) h0 = hlb;
+  if (h0 > hub) h0 = hub;
+  return h0;
+}
+
+/* (re)start the Nordsieck history at (t, y) */
+static void bdf_start(bdf* b, double t, const double* y, double tout, double h0, double hmax) {
+  const int n = b->n;
+  b->tn = t;
+  for (int i = 0; i < n; ++i) b->zn[0][i] = y[i];
+  set_ewt(b, y);
+  reactor_rhs(b->ctx, t, y, b->zn[1], NULL);
+  double h = h0 > 0.0 ? h0 : initial_step(b, tout);
+  if (h > hmax) h = hmax;
+  if (h > tout - t) h = tout - t;
+  for (int i = 0; i < n; ++i) b->zn[1][i] *= h;
+  b->h = b->hscale = b->hprime = h;
+  b->q = b->qprime = 1;
+  b->L = 2;
+  b->qwait = b->L;
+  b->etamax = ETAMX1;
+  b->nst = 0;
+  b->nstlp = 0;
+  b->nstlj = 0;
+  b->jcur = 0;
+  b->nscon = 0;
+  b->crate = 1.0;
+  b->gammap = b->gamma = b->h;
+  b->gamrat = 1.0;
+  b->saved_tq5 = 0.0;
+  for (int i = 0; i <= QMAX + 1; ++i) b->tau[i] = 0.0;
+  for (int i = 0; i < 6; ++i) b->tq[i] = 0.0;
+  b->hu = 0.0;
+}
+
+/* one BDF step: 0 ok, 2 error test failures, 3 convergence failures */
+static int bdf_step(bdf* b, int* nst_global) {
+  const double saved_t = b->tn;
+  int ncf = 0, nef = 0, nflag = NF_FIRST;
+  double dsm;
+  if (b->nst > 0 && b->hprime != b->h) {
+    if (b->qprime != b->q) {
+      adjust_order(b, b->qprime - b->q);
+      b->q = b->qprime;
+      b->L = b->q + 1;
+      b->qwait = b->L;
+    }
+    rescale(b);
+  }
+  for (;;) {
+    predict(b);
+    set_bdf(b);
+    const int r = nls(b, nflag);
+    if (r != 0) {
+      ncf++;
+      b->ncf_tot++;
+      b->etamax = 1.0;
+      restore(b, saved_t);
+      if (fabs(b->h) <= b->hmin * ONEPSM || ncf == MXNCF) return 3;
+      b->eta = fmax(ETACF, b->hmin / fabs(b->h));
+      nflag = NF_CONV_FAIL;
+      rescale(b);
+      continue;
+    }
+    dsm = b->acnrm * b->tq[2];
+    if (dsm <= 1.0) break;
+    nef++;
+    b->nef_tot++;
+    nflag = NF_ERR_FAIL;
+    restore(b, saved_t);
+    if (fabs(b->h) <= b->hmin * ONEPSM || nef == MXNEF) return 2;
+    b->etamax = 1.0;
+    if (nef <= MXNEF1) {
+      b->eta = 1.0 / (pow(BIAS2 * dsm, 1.0 / b->L) + ADDON);
+      b->eta = fmax(ETAMIN, fmax(b->eta, b->hmin / fabs(b->h)));
+      if (nef >= SMALL_NEF) b->eta = fmin(b->eta, ETAMXF);
+      rescale(b);
+      continue;
+    }
+    if (b->q > 1) {
+      b->eta = fmax(ETAMIN, b->hmin / fabs(b->h));
+      adjust_order(b, -1);
+      b->L = b->q;
+      b->q--;
+      b->qwait = b->L;
+      rescale(b);
+      continue;
+    }
+    b->eta = fmax(ETAMIN, b->hmin / fabs(b->h));
+    b->h *= b->eta;
+    b->hscale = b->h;
+    b->qwait = LONG_WAIT;
+    b->nscon = 0;
+    reactor_rhs(b->ctx, b->tn, b->zn[0], b->tempv, NULL);
+    for (int i = 0; i < b->n; ++i) b->zn[1][i] = b->h * b->tempv[i];
+  }
+  /* complete step */
+  b->nst++;
+  (*nst_global)++;
+  b->nscon++;
+  b->hu = b->h;
+  for (int i = b->q; i >= 2; --i) b->tau[i] = b->tau[i - 1];
+  if (b->q == 1 && b->nst > 1) b->tau[2] = b->tau[1];
+  b->tau[1] = b->h;
+  for (int j = 0; j <= b->q; ++j)
+    for (int i = 0; i < b->n; ++i) b->zn[j][i] += b->l[j] * b->acor[i];
+  b->qwait--;
+  if (b->qwait == 1 && b->q != QMAX) {
+    for (int i = 0; i < b->n; ++i) b->zn[QMAX][i] = b->acor[i];
+    b->saved_tq5 = b->tq[5];
+  }
+  /* prepare next step */
+  if (b->etamax == 1.0) {
+    if (b->qwait < 2) b->qwait = 2;
+    b->qprime = b->q;
+    b->hprime = b->h;
+    b->eta = 1.0;
+  } else {
+    const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / b->L) + ADDON);
+    if (b->qwait != 0) {
+      b->eta = etaq;
+      b->qprime = b->q;
+    } else {
+      b->qwait = 2;
+      double etaqm1 = 0.0, etaqp1 = 0.0;
+      if (b->q > 1) {
+        const double ddn = wrms(b, b->zn[b->q]) * b->tq[1];
+        etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / b->q) + ADDON);
+      }
+      if (b->q != QMAX && b->saved_tq5 != 0.0) {
+        const double cquot = (b->tq[5] / b->saved_tq5) * pow(b->h / b->tau[2], (double)b->L);
+        for (int i = 0; i < b->n; ++i) b->tempv[i] = b->acor[i] - cquot * b->zn[QMAX][i];
+        const double dup = wrms(b, b->tempv) * b->tq[3];
+        etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (b->L + 1)) + ADDON);
+      }
+      const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
+      if (etam < THRESH) {
+        b->eta = 1.0;
+        b->qprime = b->q;
+      } else if (etam == etaq) {
+        b->eta = etaq;
+        b->qprime = b->q;
+      } else if (etam == etaqm1) {
+        b->eta = etaqm1;
+        b->qprime = b->q - 1;
+      } else {
+        b->eta = etaqp1;
+        b->qprime = b->q + 1;
+        for (int i = 0; i < b->n; ++i) b->zn[QMAX][i] = b->acor[i];
+      }
+    }
+    /* set eta */
+    if (b->eta < THRESH) {
+      b->eta = 1.0;
+      b->hprime = b->h;
+    } else {
+      b->eta = fmin(b->eta, b->etamax);
+      b->eta /= fmax(1.0, fabs(b->h) * b->hmax_inv * b->eta);
+      b->hprime = b->h * b->eta;
+    }
+  }
+  b->etamax = (b->nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+  return 0;
+}
+
+/* ------------------------------------------------------ ignition monitor */
+typedef struct {
+  int mode, comp;
+  double thresh;
+  double best, tbest, tprev, vprev, tnext, vnext, tlast, vlast;
+  int have_prev, have_next, found, started;
+  double tau;
+} ignmon;
+
+static void ign_init(ignmon* g, const cko_cfg* cfg, double T0) {
+  memset(g, 0, sizeof(*g));
+  g->mode = cfg->ign_mode;
+  g->tau = -1.0;
+  g->best = -1e300;
+  if (g->mode == 2) g->thresh = T0 + cfg->ign_val;
+  if (g->mode == 3) g->thresh = cfg->ign_val;
+  g->comp = (g->mode == 4) ? 1 + cfg->ign_species : 0;
+}
+
+/* called after every accepted step; v = monitored value at tn (dT/dt for TIFP, Y_k for KLIM) */
+static void ign_peak_update(ignmon* g, double t, double v) {
+  if (g->started && g->found == 0 && v > g->best) {
+    g->tprev = g->tlast; g->vprev = g->vlast; g->have_prev = 1;
+    g->best = v; g->tbest = t; g->have_next = 0;
+  } else if (g->started && !g->have_next && g->tbest != 0.0 && t > g->tbest) {
+    g->tnext = t; g->vnext = v; g->have_next = 1;
+  } else if (!g->started) {
+    g->best = v; g->tbest = t; g->have_prev = 0;
+  }
+  g->started = 1;
+  g->tlast = t; g->vlast = v;
+}
+
+static double ign_peak_time(const ignmon* g) {
+  if (g->tbest <= 0.0) return -1.0;
+  if (!(g->have_prev && g->have_next)) return g->tbest;
+  /* vertex of the parabola through the three samples around the maximum */
+  const double x0 = g->tprev, x1 = g->tbest, x2 = g->tnext;
+  const double y0 = g->vprev, y1 = g->best, y2 = g->vnext;
+  const double d01 = (y1 - y0) / (x1 - x0), d12 = (y2 - y1) / (x2 - x1);
+  const double a = (d12 - d01) / (x2 - x0);
+  if (!(a < 0.0)) return x1;
+  const double bcoef = d01 - a * (x0 + x1);
+  const double tv = -bcoef / (2.0 * a);
+  if (tv < x0 || tv > x2) return x1;
+  return tv;
+}
+
+/* ---------------------------------------------------------- driver */
+int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, double V0, const double* Y0,
+                double* Yend, cko_result* res, int nsave, const double* t_save, double* y_save, double* p_save,
+                double* v_save) {
+  const int KK = m->KK, n = KK + 1;
+  bdf* b = (bdf*)calloc(1, sizeof(bdf));
+  b->J = (double*)calloc((size_t)n * n, sizeof(double));
+  b->M = (double*)calloc((size_t)n * n, sizeof(double));
+  b->n = n;
+  b->rtol = cfg->rtol;
+  b->atol = cfg->atol;
+  b->nneg = cfg->nneg;
+  const double Wbar0 = mean_wt(m, Y0);
+  const double rho0 = P0 * Wbar0 / (RU * T0);
+  double Vstart = V0;
+  if (cfg->problem == 2 && cfg->nprof > 0) Vstart = cfg->prof_v[0];
+  rctx ctx = {m, cfg, cfg->problem, rho0, Vstart, P0, T0, 0, 0};
+  if (cfg->problem == 1 && cfg->nprof > 0) ctx.P0 = cfg->prof_v[0];
+  b->ctx = &ctx;
+  const double tend = cfg->t_end;
+  const double hmax = cfg->hmax > 0.0 ? cfg->hmax : tend / 100.0;
+  b->hmax_inv = 1.0 / hmax;
+  b->hmin = 0.0;
+  double y[NMAX];
+  y[0] = T0;
+  for (int k = 0; k < KK; ++k) y[1 + k] = Y0[k];
+  /* profile breakpoints are integration stop points (derivative discontinuities) */
+  double tcrit[64];
+  int ncrit = 0;
+  for (int i = 0; i < cfg->nprof && ncrit < 63; ++i)
+    if (cfg->prof_t[i] > 0.0 && cfg->prof_t[i] < tend) tcrit[ncrit++] = cfg->prof_t[i];
+  tcrit[ncrit++] = tend;
+  int icrit = 0;
+  bdf_start(b, 0.0, y, tcrit[0], cfg->h0, hmax);
+  ignmon g;
+  ign_init(&g, cfg, T0);
+  int isave = 0;
+  /* save points at t = 0 */
+  while (isave < nsave && t_save[isave] <= 0.0) {
+    for (int i = 0; i < n; ++i) y_save[(size_t)isave * n + i] = y[i];
+    if (p_save) p_save[isave] = P0;
+    if (v_save) v_save[isave] = Vstart;
+    isave++;
+  }
+  if (g.mode == 1 || g.mode == 4) {
+    double f0[NMAX];
+    reactor_rhs(&ctx, 0.0, y, f0, NULL);
+    ign_peak_update(&g, 0.0, g.mode == 1 ? f0[0] : y[g.comp]);
+  }
+  int status = 0, nst = 0, stopped = 0;
+  const int max_steps = cfg->max_steps > 0 ? cfg->max_steps : 200000;
+  double tstop_final = tend;
+  while (b->tn < tend * (1.0 - 1e-15)) {
+    /* clamp the next step to the next critical time */
+    const double tc = tcrit[icrit];
+    if (b->tn + b->hprime > tc) {
+      const double hp = tc - b->tn;
+      b->eta = hp / b->h;
+      if (b->nst > 0) {
+        b->hprime = hp;
+      } else {
+        rescale(b);
+        b->hprime = b->h;
+      }
+    }
+    set_ewt(b, b->zn[0]);
+    const double told = b->tn;
+    int r = bdf_step(b, &nst);
+    if (r != 0) { status = r; break; }
+    const double tn = b->tn;
+    /* solution saving by interpolation */
+    while (isave < nsave && t_save[isave] <= tn) {
+      double ys[NMAX];
+      dky_vec(b, t_save[isave], ys);
+      for (int i = 0; i < n; ++i) y_save[(size_t)isave * n + i] = ys[i];
+      double Wb = mean_wt(m, ys + 1), rho, P, V, d;
+      if (cfg->problem == 1) {
+        profile_eval(cfg, t_save[isave], ctx.P0, &P, &d);
+        rho = P * Wb / (RU * ys[0]);
+        V = rho0 * Vstart / rho;
+      } else {
+        profile_eval(cfg, t_save[isave], Vstart, &V, &d);
+        rho = rho0 * Vstart / V;
+        P = rho * RU * ys[0] / Wb;
+      }
+      if (p_save) p_save[isave] = P;
+      if (v_save) v_save[isave] = V;
+      isave++;
+    }
+    /* ignition detection */
+    if (g.mode == 1) {
+      ign_peak_update(&g, tn, b->zn[1][0] / b->h);
+    } else if (g.mode == 4) {
+      ign_peak_update(&g, tn, b->zn[0][g.comp]);
+    } else if ((g.mode == 2 || g.mode == 3) && !g.found && b->zn[0][0] >= g.thresh) {
+      double lo = told, hi = tn;
+      for (int it = 0; it < 60; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (dky0(b, mid, 0) >= g.thresh) hi = mid; else lo = mid;
+      }
+      g.found = 1;
+      g.tau = hi;
+    }
+    if (cfg->ign_stop) {
+      if ((g.mode == 2 || g.mode == 3) && g.found) { stopped = 1; tstop_final = tn; break; }
+      if (g.mode == 1 && g.have_next && g.vlast < 0.1 * g.best && b->zn[0][0] > T0 + 200.0) {
+        stopped = 1; tstop_final = tn; break;
+      }
+    }
+    if (nst >= max_steps) { status = 1; break; }
+    if (tn >= tc * (1.0 - 1e-15) && icrit < ncrit - 1) {
+      /* restart at the breakpoint */
+      double yc[NMAX];
+      for (int i = 0; i < n; ++i) yc[i] = b->zn[0][i];
+      icrit++;
+      const int nlu = b->nlu, ncf = b->ncf_tot, nef = b->nef_tot;
+      bdf_start(b, tn, yc, tcrit[icrit], 0.0, hmax);
+      b->nlu = nlu; b->ncf_tot = ncf; b->nef_tot = nef;
+    }
+  }
+  /* final state */
+  double yf[NMAX];
+  double tf = tend;
+  if (stopped || status) {
+    tf = b->tn;
+    for (int i = 0; i < n; ++i) yf[i] = b->zn[0][i];
+  } else {
+    dky_vec(b, tend, yf);
+  }
+  (void)tstop_final;
+  if (g.mode == 1 || g.mode == 4) g.tau = ign_peak_time(&g);
+  if (res) {
+    res->tau = g.tau;
+    res->t_end = tf;
+    res->T = yf[0];
+    double Wb = mean_wt(m, yf + 1), d;
+    if (cfg->problem == 1) {
+      profile_eval(cfg, tf, ctx.P0, &res->P, &d);
+      res->V = rho0 * Vstart / (res->P * Wb / (RU * yf[0]));
+    } else {
+      profile_eval(cfg, tf, Vstart, &res->V, &d);
+      res->P = (rho0 * Vstart / res->V) * RU * yf[0] / Wb;
+    }
+    res->status = status;
+    res->nst = nst;
+    res->nfe = ctx.nfe;
+    res->nje = ctx.nje;
+    res->nlu = b->nlu;
+    res->ncf = b->ncf_tot;
+    res->nef = b->nef_tot;
+  }
+  if (Yend)
+    for (int k = 0; k < KK; ++k) Yend[k] = yf[1 + k];
+  free(b->J);
+  free(b->M);
+  free(b);
+  return status;
+}
+
+int cko_reactor_batch(const cko_mech* m, const cko_cfg* cfg, int n, const int* problem, const double* T0,
+                      const double* P0, const double* V0, const double* Y0, double* Yend, cko_result* res,
+                      int nthreads) {
+  const int KK = m->KK;
+  int nfail = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nfail)
+#endif
+  for (int i = 0; i < n; ++i) {
+    cko_cfg c = *cfg;
+    if (problem) c.problem = problem[i];
+    int r = cko_reactor(m, &c, T0[i], P0[i], V0 ? V0[i] : 1.0, Y0 + (size_t)i * KK, Yend + (size_t)i * KK,
+                        res + i, 0, NULL, NULL, NULL, NULL);
+    if (r) nfail++;
+  }
+  return nfail;
+}
