@@ -1,0 +1,164 @@
+/* ckmi.h -- C ABI of libckmi.so, the MI355X (gfx950) batched batch-reactor engine.
+ *
+ * This is the drop-in boundary for PyChemkin's batch-reactor hot path.  The reference
+ * reaches the closed Chemkin library through ctypes (chemkin_wrapper.py:244,271-272) with
+ * Fortran-style by-pointer scalars, caller-allocated arrays and an int error return
+ * (0 = success).  libckmi keeps that convention and adds batched entry points that take
+ * device-resident struct-of-arrays buffers:
+ *
+ *   ckmi_mech_create        replaces KINPreProcess + KINGetChemistrySizes + table getters
+ *                           (chemkin_wrapper.py:303-316,333-397; chemistry.py:675-703).
+ *                           The Chemkin-format text is parsed on the host
+ *                           (pychemkin_amd/mechanism.py) and handed over as flat tables.
+ *   ckmi_rop_thermo         batched KINGetGasROP + KINGetGasMixtureSpecificHeat /
+ *                           KINGetGasMixtureEnthalpy (chemkin_wrapper.py:427-440,482-489;
+ *                           mixture.py:1236,1341,1442).
+ *   ckmi_reaction_rates     batched KINGetGasReactionRates (chemkin_wrapper.py:490-498;
+ *                           mixture.py:1551).
+ *   ckmi_species_thermo     batched KINGetGasSpecificHeat / SpeciesEnthalpy /
+ *                           SpeciesInternalEnergy (chemkin_wrapper.py:375-392).
+ *   ckmi_reactor_run        batched KINAll0D_SetupBatchInputs + KINAll0D_SetUserKeyword +
+ *                           KINAll0D_Calculate + KINAll0D_GetIgnitionDelay +
+ *                           KINAll0D_GetGasSolnResponse (chemkin_wrapper.py:606-618,
+ *                           688-689,698-699,751-763; batchreactor.py:1036-1159,582,1396).
+ *   ckmi_set_afactor /      KINSetAFactorForAReaction / KINGetReactionRateParameters
+ *   ckmi_get_arrhenius      (chemkin_wrapper.py:499-511; chemistry.py:1627,1665).
+ *
+ * All buffers passed to ckmi_rop_thermo / ckmi_reaction_rates / ckmi_species_thermo /
+ * ckmi_reactor_run are device pointers on the handle's device; `stream` is a hipStream_t
+ * (NULL = default stream).  The calls are asynchronous on that stream.
+ */
+#ifndef CKMI_H
+#define CKMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CKMI_SLOTS 4 /* distinct species per reaction side in the flat tables */
+
+/* reaction types */
+#define CKMI_RXN_ELEMENTARY 0
+#define CKMI_RXN_THIRDBODY 1
+#define CKMI_RXN_FALLOFF 2
+/* falloff forms */
+#define CKMI_FALL_NONE 0
+#define CKMI_FALL_LINDEMANN 1
+#define CKMI_FALL_TROE3 2
+#define CKMI_FALL_TROE4 3
+#define CKMI_FALL_SRI 4
+
+/* error codes (0 = success, as the KIN* functions) */
+#define CKMI_OK 0
+#define CKMI_ERR_ARG 1
+#define CKMI_ERR_HIP 2
+#define CKMI_ERR_SIZE 3
+#define CKMI_ERR_UNSUPPORTED 4
+
+/* Flat mechanism tables (host pointers), layout produced by Mechanism.to_tables(). */
+typedef struct {
+  int32_t KK, II;
+  const double* wt;       /* [KK] molecular weights, g/mol */
+  const double* thermo;   /* [KK][17]: tlow, tmid, thigh, low a1..a7, high a1..a7 */
+  const int32_t* rtype;   /* [II] CKMI_RXN_* */
+  const int32_t* rev;     /* [II] 1 reversible */
+  const int32_t* nr;      /* [II] reactant slots used */
+  const int32_t* np;      /* [II] product slots used */
+  const int32_t* rsp;     /* [II][4] reactant species */
+  const int32_t* psp;     /* [II][4] product species */
+  const double* rnu;      /* [II][4] reactant stoichiometric coefficients */
+  const double* pnu;      /* [II][4] product stoichiometric coefficients */
+  const double* arr;      /* [II][3] ln A (cgs), b, E/R (K) */
+  const double* low;      /* [II][3] falloff low-pressure limit */
+  const double* revp;     /* [II][3] explicit reverse parameters (REV) */
+  const int32_t* has_rev; /* [II] */
+  const int32_t* ftype;   /* [II] CKMI_FALL_* */
+  const double* fpar;     /* [II][5] TROE a,T***,T*,T** or SRI a,b,c,d,e */
+  const int32_t* tbsp;    /* [II] -1 mixture M, else collider species index */
+  const int32_t* eff_ptr; /* [II+1] CSR into eff_sp / eff_val */
+  const int32_t* eff_sp;
+  const double* eff_val;  /* third-body efficiencies (absolute) */
+} ckmi_mech_desc;
+
+typedef struct ckmi_mech ckmi_mech; /* opaque: tables resident in HBM of one device */
+
+/* Reactor-run configuration (one per batch; the reference passes these as keyword text,
+ * reactormodel.py:966-996, batchreactor.py:1106-1114). */
+typedef struct {
+  int32_t energy;      /* 1 ENERGY equation, 2 given (constant) temperature */
+  double t_end;        /* TIME [s] */
+  double atol, rtol;   /* ATOL / RTOL */
+  double h0;           /* HO initial step [s], 0 = estimate */
+  double hmax;         /* STPT max step [s], 0 = t_end/100 */
+  int32_t nneg;        /* NNEG */
+  int32_t ign_mode;    /* 0 none, 1 TIFP, 2 DTIGN, 3 TLIM, 4 KLIM */
+  double ign_val;      /* DTIGN rise [K] or TLIM temperature [K] */
+  int32_t ign_species; /* KLIM species index */
+  int32_t ign_stop;    /* IGN_STOP */
+  int32_t max_steps;   /* 0 = 200000 */
+  int32_t nprof;       /* VPRO (CONV) / PPRO (CONP) profile points, 0 = none (<= 64) */
+  double prof_t[64];
+  double prof_v[64];
+} ckmi_reactor_cfg;
+
+/* per-reactor statistics written by ckmi_reactor_run (int32 [n][8]) */
+#define CKMI_STAT_NST 0
+#define CKMI_STAT_NFE 1
+#define CKMI_STAT_NJE 2
+#define CKMI_STAT_NLU 3
+#define CKMI_STAT_NCF 4
+#define CKMI_STAT_NEF 5
+#define CKMI_STAT_STATUS 6
+#define CKMI_NSTAT 8
+
+/* reactor status (CKMI_STAT_STATUS) */
+#define CKMI_RUN_OK 0
+#define CKMI_RUN_MAXSTEPS 1
+#define CKMI_RUN_ERRTEST 2
+#define CKMI_RUN_CONVFAIL 3
+
+const char* ckmi_last_error(void);
+int ckmi_version(void);
+
+/* Build device tables on the current HIP device. */
+int ckmi_mech_create(const ckmi_mech_desc* desc, ckmi_mech** out);
+int ckmi_mech_destroy(ckmi_mech* mech);
+int ckmi_mech_sizes(const ckmi_mech* mech, int32_t* KK, int32_t* II);
+
+/* A-factor get/set (original reaction order, 0-based); set takes effect for later calls. */
+int ckmi_get_arrhenius(const ckmi_mech* mech, double* A, double* b, double* E_R);
+int ckmi_set_afactor(ckmi_mech* mech, int32_t irxn, double A);
+
+/* Species thermo per state: cp/R, h/RT, s/R  (device, [KK][n] each; any may be NULL). */
+int ckmi_species_thermo(const ckmi_mech* mech, int32_t n, const double* T, double* cp_R, double* h_RT,
+                        double* s_R, void* stream);
+
+/* Batched ROP + mixture thermo at (T, P, Y):  T[n], P[n] dyn/cm2, Y[KK][n] mass fractions
+ * -> wdot[KK][n] mol/cm3-s, cp[n] erg/g-K, h[n] erg/g (cp and h may be NULL). */
+int ckmi_rop_thermo(const ckmi_mech* mech, int32_t n, const double* T, const double* P, const double* Y,
+                    double* wdot, double* cp, double* h, void* stream);
+
+/* Batched forward/reverse rates of progress: qf[II][n], qr[II][n] mol/cm3-s. */
+int ckmi_reaction_rates(const ckmi_mech* mech, int32_t n, const double* T, const double* P, const double* Y,
+                        double* qf, double* qr, void* stream);
+
+/* Batched closed homogeneous reactors.
+ *   problem[n]   1 CONP (given pressure), 2 CONV (given volume)
+ *   T0, P0, V0   [n] initial temperature [K], pressure [dyn/cm2], volume [cm3]
+ *   Y0           [n][KK] initial mass fractions (reactor-major)
+ *   tau          [n] ignition delay [s] (-1 if not detected)
+ *   Tend, Pend, Vend [n], Yend [n][KK] final state (at t_end, or at the stop time)
+ *   stats        [n][CKMI_NSTAT] int32
+ *   nsave, t_save[nsave] (device) and y_save [n][nsave][KK+1] (T, Y) optional (nsave = 0)
+ */
+int ckmi_reactor_run(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int32_t n, const int32_t* problem,
+                     const double* T0, const double* P0, const double* V0, const double* Y0, double* tau,
+                     double* Tend, double* Pend, double* Vend, double* Yend, int32_t* stats, int32_t nsave,
+                     const double* t_save, double* y_save, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,248 @@
+"""ctypes binding of libckmi.so (include/ckmi.h) -- the product's native path.
+
+Mirrors the reference's FFI layer (``chemkin_wrapper.py:244,271-272,300-867``): one
+``ctypes.CDLL`` loaded at import, prototypes declared once, ``int`` status returns.  Device
+buffers are torch tensors on the ROCm device; torch is imported first so that libckmi binds
+to the same HIP runtime instance (both carry SONAME ``libamdhip64.so.7``).
+
+There is no CPU fallback: if the library is missing or no GPU is present, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+from typing import Dict, Optional
+
+import numpy as np
+import torch  # noqa: F401  (must be loaded before libckmi.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libckmi.so")
+
+SLOTS = 4
+NSTAT = 8
+STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "reserved")
+RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures"}
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+_P = ct.c_void_p
+
+
+class MechDesc(ct.Structure):
+    _fields_ = [("KK", ct.c_int32), ("II", ct.c_int32)] + [
+        (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
+                          "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val")
+    ]
+
+
+class ReactorCfg(ct.Structure):
+    _fields_ = [
+        ("energy", ct.c_int32), ("t_end", ct.c_double), ("atol", ct.c_double), ("rtol", ct.c_double),
+        ("h0", ct.c_double), ("hmax", ct.c_double), ("nneg", ct.c_int32), ("ign_mode", ct.c_int32),
+        ("ign_val", ct.c_double), ("ign_species", ct.c_int32), ("ign_stop", ct.c_int32), ("max_steps", ct.c_int32),
+        ("nprof", ct.c_int32), ("prof_t", ct.c_double * 64), ("prof_v", ct.c_double * 64),
+    ]
+
+
+_lib: Optional[ct.CDLL] = None
+
+# every symbol include/ckmi.h declares, with its prototype
+PROTOTYPES = {
+    "ckmi_last_error": (ct.c_char_p, []),
+    "ckmi_version": (ct.c_int, []),
+    "ckmi_mech_create": (ct.c_int, [ct.POINTER(MechDesc), ct.POINTER(_P)]),
+    "ckmi_mech_destroy": (ct.c_int, [_P]),
+    "ckmi_mech_sizes": (ct.c_int, [_P, ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),
+    "ckmi_get_arrhenius": (ct.c_int, [_P, _P, _P, _P]),
+    "ckmi_set_afactor": (ct.c_int, [_P, ct.c_int32, ct.c_double]),
+    "ckmi_species_thermo": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P, _P]),
+    "ckmi_rop_thermo": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P, _P, _P, _P]),
+    "ckmi_reaction_rates": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P, _P, _P]),
+    "ckmi_reactor_run": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                     _P, ct.c_int32, _P, _P, _P]),
+}
+
+
+def lib() -> ct.CDLL:
+    """Load libckmi.so once (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"libckmi.so not found at {LIB_PATH}; run __graft_entry__.build()")
+        L = ct.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ckmi_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (code {rc}): {msg}")
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def _stream_ptr(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+IGN_MODES = {None: 0, "none": 0, "T_inflection": 1, "TIFP": 1, "T_rise": 2, "DTIGN": 2, "T_ignition": 3,
+             "TLIM": 3, "Species_peak": 4, "KLIM": 4}
+
+
+def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: float = 1e-6, h0: float = 0.0,
+             hmax: float = 0.0, nneg: bool = False, ign_mode=None, ign_val: float = 0.0, ign_species: int = 0,
+             ign_stop: bool = False, max_steps: int = 0, profile=None) -> ReactorCfg:
+    c = ReactorCfg()
+    c.energy, c.t_end, c.atol, c.rtol = int(energy), float(t_end), float(atol), float(rtol)
+    c.h0, c.hmax, c.nneg = float(h0), float(hmax), int(bool(nneg))
+    c.ign_mode = IGN_MODES[ign_mode] if not isinstance(ign_mode, int) else int(ign_mode)
+    c.ign_val, c.ign_species, c.ign_stop, c.max_steps = float(ign_val), int(ign_species), int(bool(ign_stop)), int(max_steps)
+    c.nprof = 0
+    if profile is not None:
+        x, v = np.asarray(profile[0], np.float64), np.asarray(profile[1], np.float64)
+        if len(x) != len(v) or len(x) > 64:
+            raise ValueError("profile must have matching lengths <= 64")
+        c.nprof = len(x)
+        for i in range(len(x)):
+            c.prof_t[i] = x[i]
+            c.prof_v[i] = v[i]
+    return c
+
+
+class DeviceMechanism:
+    """Mechanism tables resident in HBM of one GPU (wraps a ckmi_mech handle)."""
+
+    def __init__(self, tables: Dict[str, np.ndarray], device=None):
+        if not torch.cuda.is_available():
+            raise NativeError("no ROCm GPU visible: the ckmi device path requires an MI355X")
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else torch.device(device).index or 0)
+        self.KK = int(tables["KK"])
+        self.II = int(tables["II"])
+        keep = {k: np.ascontiguousarray(v) for k, v in tables.items() if isinstance(v, np.ndarray) and v.ndim > 0}
+        d = MechDesc()
+        d.KK, d.II = self.KK, self.II
+        for name, _ in MechDesc._fields_[2:]:
+            setattr(d, name, keep[name].ctypes.data)
+        h = _P()
+        with torch.cuda.device(self.device):
+            _check(lib().ckmi_mech_create(ct.byref(d), ct.byref(h)), "ckmi_mech_create")
+        self._h = h
+        del keep
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().ckmi_mech_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -------------------------------------------------------------- parameters
+    def arrhenius(self):
+        A, b, E = (np.zeros(self.II) for _ in range(3))
+        _check(lib().ckmi_get_arrhenius(self._h, A.ctypes.data, b.ctypes.data, E.ctypes.data), "ckmi_get_arrhenius")
+        return A, b, E
+
+    def set_afactor(self, irxn: int, A: float) -> None:
+        with torch.cuda.device(self.device):
+            _check(lib().ckmi_set_afactor(self._h, int(irxn), float(A)), "ckmi_set_afactor")
+
+    # -------------------------------------------------------------- helpers
+    def _dev(self, x, dtype=torch.float64):
+        if isinstance(x, torch.Tensor):
+            return x.to(device=self.device, dtype=dtype).contiguous()
+        return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=self.device)
+
+    # -------------------------------------------------------------- kernels
+    def species_thermo(self, T):
+        T = self._dev(T).reshape(-1)
+        n = T.numel()
+        cp, h, s = (torch.empty((self.KK, n), dtype=torch.float64, device=self.device) for _ in range(3))
+        _check(lib().ckmi_species_thermo(self._h, n, _ptr(T), _ptr(cp), _ptr(h), _ptr(s), _stream_ptr(self.device)),
+               "ckmi_species_thermo")
+        return cp, h, s
+
+    def rop_thermo(self, T, P, Y_soa, wdot=None, cp=None, h=None):
+        """T[n], P[n], Y[KK][n] -> wdot[KK][n], cp[n], h[n] (all device tensors)."""
+        T = self._dev(T).reshape(-1)
+        P = self._dev(P).reshape(-1)
+        Y = self._dev(Y_soa)
+        n = T.numel()
+        if Y.shape != (self.KK, n):
+            raise ValueError(f"Y must be [KK={self.KK}][n={n}], got {tuple(Y.shape)}")
+        if wdot is None:
+            wdot = torch.empty((self.KK, n), dtype=torch.float64, device=self.device)
+        if cp is None:
+            cp = torch.empty(n, dtype=torch.float64, device=self.device)
+        if h is None:
+            h = torch.empty(n, dtype=torch.float64, device=self.device)
+        _check(lib().ckmi_rop_thermo(self._h, n, _ptr(T), _ptr(P), _ptr(Y), _ptr(wdot), _ptr(cp), _ptr(h),
+                                     _stream_ptr(self.device)), "ckmi_rop_thermo")
+        return wdot, cp, h
+
+    def reaction_rates(self, T, P, Y_soa):
+        T = self._dev(T).reshape(-1)
+        P = self._dev(P).reshape(-1)
+        Y = self._dev(Y_soa)
+        n = T.numel()
+        qf = torch.empty((self.II, n), dtype=torch.float64, device=self.device)
+        qr = torch.empty((self.II, n), dtype=torch.float64, device=self.device)
+        _check(lib().ckmi_reaction_rates(self._h, n, _ptr(T), _ptr(P), _ptr(Y), _ptr(qf), _ptr(qr),
+                                         _stream_ptr(self.device)), "ckmi_reaction_rates")
+        return qf, qr
+
+    def reactor_run(self, cfg: ReactorCfg, problem, T0, P0, V0, Y0, t_save=None, out=None):
+        """Integrate n independent reactors. Y0 is [n][KK]. Returns a dict of device tensors."""
+        T0 = self._dev(T0).reshape(-1)
+        n = T0.numel()
+        P0 = self._dev(P0).reshape(-1)
+        V0 = self._dev(V0).reshape(-1)
+        Y0 = self._dev(Y0).reshape(n, self.KK)
+        prob = self._dev(problem, torch.int32).reshape(-1)
+        if not (P0.numel() == V0.numel() == prob.numel() == n):
+            raise ValueError("T0, P0, V0, problem must all have n entries")
+        o = out or {}
+        dev = self.device
+        f64 = dict(dtype=torch.float64, device=dev)
+        tau = o.get("tau", torch.empty(n, **f64))
+        Tend = o.get("T", torch.empty(n, **f64))
+        Pend = o.get("P", torch.empty(n, **f64))
+        Vend = o.get("V", torch.empty(n, **f64))
+        Yend = o.get("Y", torch.empty((n, self.KK), **f64))
+        stats = o.get("stats", torch.empty((n, NSTAT), dtype=torch.int32, device=dev))
+        nsave = 0
+        ts = ys = None
+        if t_save is not None:
+            ts = self._dev(t_save).reshape(-1)
+            nsave = ts.numel()
+            ys = torch.empty((n, nsave, self.KK + 1), **f64)
+        _check(lib().ckmi_reactor_run(self._h, ct.byref(cfg), n, _ptr(prob), _ptr(T0), _ptr(P0), _ptr(V0), _ptr(Y0),
+                                      _ptr(tau), _ptr(Tend), _ptr(Pend), _ptr(Vend), _ptr(Yend), _ptr(stats), nsave,
+                                      _ptr(ts), _ptr(ys), _stream_ptr(dev)), "ckmi_reactor_run")
+        res = dict(tau=tau, T=Tend, P=Pend, V=Vend, Y=Yend, stats=stats)
+        if ys is not None:
+            res["t_save"] = ts
+            res["y_save"] = ys
+        return res

@@ -1,0 +1,39 @@
+"""Build libckmi.so for gfx950 with hipcc (in-tree, so the .so travels with the repo)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "csrc", "ckmi.hip")
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp")] + [
+    os.path.join(HERE, "..", "include", "ckmi.h")]
+OUT = os.path.join(HERE, "_lib", "libckmi.so")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics", "-mcode-object-version=5",
+         f"--offload-arch={ARCH}"]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in [SRC] + DEPS)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not needs_build():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))
