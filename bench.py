@@ -1,0 +1,239 @@
+#!/usr/bin/env python3
+"""Benchmark: GRI-Mech 3.0 constant-pressure ignition sweep on MI355X (BASELINE.json metric).
+
+One "step" = one ckmi_reactor_run over this rank's shard of the ignition-delay sweep
+(configs[2]: 64 T0 x 32 phi x 32 P = 65,536 CONP adiabatic CH4/air reactors per GPU,
+t_end = 1 s, TIFP ignition, ATOL/RTOL = 1e-10/1e-8).  For N GPUs the sweep has 64*N
+temperatures and rank r takes every N-th one (weak scaling, no collectives on the data path).
+Inputs are resident in HBM before the timed region.  value = reactors integrated by all
+ranks / max-over-ranks wall time.
+
+Also reported: the ROP+thermo evaluation rate (configs[1], random (T, P, Y) states), a
+roofline object for the reactor kernel (algorithmic FLOPs from solver statistics, see
+pychemkin_amd/perf.py) and the CPU baseline (oracle/ C restatement, OpenMP, timed on a
+strided sample of the same sweep on this host).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from pychemkin_amd import _native  # noqa: E402
+from pychemkin_amd.mechanism import Mechanism  # noqa: E402
+from pychemkin_amd.perf import count_ops, reactor_flops  # noqa: E402
+
+P_ATM = 1.01325e6
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak, MI355X_MICROARCH.md / SURVEY 8d
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak
+
+
+def mechanism():
+    return Mechanism.from_files(os.path.join(ROOT, "data", "grimech30_chem.inp"),
+                                os.path.join(ROOT, "data", "grimech30_thermo.dat"))
+
+
+def ch4_air_Y(mech, phi):
+    """CH4/air at equivalence ratio phi (X_by_Equivalence_Ratio, mixture.py:2383-2539), mass fractions."""
+    KK = mech.KK
+    iCH4, iO2, iN2 = mech.species.index("CH4"), mech.species.index("O2"), mech.species.index("N2")
+    alpha = 2.0 / 0.21
+    X = np.zeros((len(phi), KK))
+    X[:, iCH4] = phi
+    X[:, iO2] = 0.21 * alpha
+    X[:, iN2] = 0.79 * alpha
+    X /= X.sum(axis=1, keepdims=True)
+    Y = X * mech.wt
+    return Y / Y.sum(axis=1, keepdims=True)
+
+
+def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
+    """Rank's shard of the (64*world) x 32 x 32 ignition sweep (configs[2] at world = 1)."""
+    T_all = 1100.0 + 600.0 * np.arange(nT * world) / (nT * world - 1)
+    T_sel = T_all[rank::world]
+    phi = 0.5 + 1.5 * np.arange(nphi) / (nphi - 1)
+    P = P_ATM * 10.0 ** (2.0 * np.arange(nP) / (nP - 1))
+    TT, FF, PP = np.meshgrid(T_sel, phi, P, indexing="ij")
+    TT, FF, PP = TT.ravel(), FF.ravel(), PP.ravel()
+    return TT, PP, ch4_air_Y(mech, FF)
+
+
+RUN = dict(energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reactors", type=int, default=0, help="override reactors per GPU (0 = full 65,536 shard)")
+    ap.add_argument("--rop-states", type=int, default=10_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=384, help="reactors in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    mech = mechanism()
+    tables = mech.to_tables()
+    ops = count_ops(tables)
+    dm = _native.DeviceMechanism(tables, device=dev)
+
+    T0, P0, Y0 = sweep(mech, world, rank)
+    if args.reactors:
+        T0, P0, Y0 = T0[: args.reactors], P0[: args.reactors], Y0[: args.reactors]
+    n = len(T0)
+    T0_d = torch.as_tensor(T0, device=dev)
+    P0_d = torch.as_tensor(P0, device=dev)
+    V0_d = torch.ones(n, dtype=torch.float64, device=dev)
+    Y0_d = torch.as_tensor(Y0, device=dev).contiguous()
+    prob_d = torch.ones(n, dtype=torch.int32, device=dev)
+    cfg = _native.make_cfg(**RUN)
+    out = dict(tau=torch.empty(n, dtype=torch.float64, device=dev), T=torch.empty(n, dtype=torch.float64, device=dev),
+               P=torch.empty(n, dtype=torch.float64, device=dev), V=torch.empty(n, dtype=torch.float64, device=dev),
+               Y=torch.empty((n, mech.KK), dtype=torch.float64, device=dev),
+               stats=torch.empty((n, _native.NSTAT), dtype=torch.int32, device=dev))
+
+    def step():
+        return dm.reactor_run(cfg, prob_d, T0_d, P0_d, V0_d, Y0_d, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record()
+        res = step()
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    tmax = tmax.item()
+
+    stats = res["stats"].cpu().numpy()
+    tau = res["tau"].cpu().numpy()
+    nbad = int((stats[:, 6] != 0).sum())
+    nnoign = int((tau <= 0).sum())
+    flops = reactor_flops(ops, stats)
+    kern_s = float(np.mean(kern_ms)) / 1e3
+    achieved_tf = flops / kern_s / 1e12
+
+    total_reactors = n * world * args.steps
+    value = total_reactors / tmax
+
+    # ---- ROP + thermo (configs[1]) : secondary metric
+    rop = None
+    if args.rop_states > 0:
+        rng = np.random.default_rng(0)
+        ns = args.rop_states
+        Ts = torch.as_tensor(rng.uniform(300.0, 3000.0, ns), device=dev)
+        Ps = torch.as_tensor(P_ATM * 10.0 ** rng.uniform(-1.0, 2.0, ns), device=dev)
+        Ys = torch.as_tensor(rng.dirichlet(0.5 * np.ones(mech.KK), ns).T.copy(), device=dev)
+        wdot = torch.empty((mech.KK, ns), dtype=torch.float64, device=dev)
+        cp = torch.empty(ns, dtype=torch.float64, device=dev)
+        hh = torch.empty(ns, dtype=torch.float64, device=dev)
+        dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
+        torch.cuda.synchronize()
+        reps = 3
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
+        e1.record()
+        torch.cuda.synchronize()
+        sec = e0.elapsed_time(e1) / 1e3 / reps
+        rop = {
+            "value": ns / sec, "unit": "states/s", "states": ns, "ms_per_launch": sec * 1e3,
+            "roofline": {
+                "bound": "mfma", "pipe": "fp64-valu", "achieved": ops["F_rop"] * ns / sec / 1e12,
+                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": ops["F_rop"] * ns / sec / 1e12 / FP64_PEAK_TFLOPS,
+                "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "hbm_frac": ops["bytes_rop"] * ns / sec / 1e9 / HBM_PEAK_GBS,
+                "traffic": None,
+            },
+        }
+        del Ts, Ps, Ys, wdot, cp, hh
+
+    # ---- CPU baseline (rank 0, N = 1): oracle C restatement on a strided sample
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
+        orc = Oracle(mech)
+        stride = max(1, n // args.cpu_sample)
+        idx = np.arange(0, n, stride)[: args.cpu_sample]
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        tc = time.perf_counter()
+        nfail, cres, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=np.ones(len(idx), np.int32),
+                                           V0=np.ones(len(idx)), nthreads=threads, **RUN)
+        tcpu = time.perf_counter() - tc
+        ctau = np.array([r.tau for r in cres])
+        gtau = tau[idx]
+        cpu = {"value": len(idx) / tcpu, "unit": "reactors/s", "cores": threads, "kind": "port",
+               "sample": f"{len(idx)} reactors, every {stride}th of the GPU sweep, OpenMP over reactors",
+               "seconds": tcpu, "tau_max_rel_diff_vs_gpu": float(np.max(np.abs(gtau / ctau - 1)))}
+
+    if rank == 0:
+        line = {
+            "metric": "reactor integrations/sec (GRI-3.0 const-P ignition)",
+            "value": value,
+            "unit": "reactors/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": tmax / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": "configs[2]: GRI-3.0 CONP CH4/air ignition sweep 64 T0 x 32 phi x 32 P per GPU",
+                       "reactors_per_gpu": n, "t_end_s": 1.0, "atol": 1e-10, "rtol": 1e-8, "ignition": "TIFP",
+                       "parallelism": f"shard-by-condition x{world}"},
+            "reactors_per_min": value * 60.0,
+            "failed_reactors": nbad,
+            "not_ignited": nnoign,
+            "solver": {"mean_steps": float(stats[:, 0].mean()), "mean_rhs": float(stats[:, 1].mean()),
+                       "mean_jac": float(stats[:, 2].mean()), "mean_lu": float(stats[:, 3].mean()),
+                       "mean_newton": float(stats[:, 7].mean())},
+            "roofline": {"bound": "mfma", "pipe": "fp64-valu", "kernel": "reactor_kernel<54>",
+                         "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                         "flops_per_launch": flops, "kernel_ms": kern_s * 1e3},
+            "cpu_baseline": cpu,
+            "rop": rop,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

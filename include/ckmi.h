@@ -111,6 +111,7 @@ typedef struct {
 #define CKMI_STAT_NCF 4
 #define CKMI_STAT_NEF 5
 #define CKMI_STAT_STATUS 6
+#define CKMI_STAT_NNI 7 /* Newton iterations = linear solves */
 #define CKMI_NSTAT 8
 
 /* reactor status (CKMI_STAT_STATUS) */

@@ -48,7 +48,7 @@ typedef struct {
   double kf, kr, mfac, pf, pr, dlkf, dlkr;
 } rxn_eval;
 
-static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, const double* C,
+static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, double lnPRT, const double* C,
                           double Ctot, const double* g_RT, const double* h_RT, rxn_eval* e) {
   const double* a = m->arr + 3 * i;
   double kf = exp(a[0] + a[1] * lnT - a[2] * invT);
@@ -108,7 +108,7 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
         dG += nu * g_RT[k]; dH += nu * h_RT[k]; dnu += nu;
       }
       /* Kc = exp(-dG) (PATM/RT)^dnu ; kr = kf / Kc */
-      kr = kf * exp(dG - dnu * log(PATM / (RU * T)));
+      kr = kf * exp(dG - dnu * lnPRT);
       dlkr = dlkf - (dH - dnu) * invT;
     }
   }
@@ -143,10 +143,10 @@ void cko_rates(const cko_mech* m, double T, double P, const double* Y, double* q
   cko_thermo(m, T, NULL, h_RT, s_R);
   for (int k = 0; k < KK; ++k) g_RT[k] = h_RT[k] - s_R[k];
   if (wdot) memset(wdot, 0, sizeof(double) * KK);
-  const double lnT = log(T), invT = 1.0 / T;
+  const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   for (int i = 0; i < m->II; ++i) {
     rxn_eval e;
-    eval_reaction(m, i, T, lnT, invT, C, Ctot, g_RT, h_RT, &e);
+    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, &e);
     double f = e.mfac * e.kf * e.pf, r = e.mfac * e.kr * e.pr;
     if (qf) qf[i] = f;
     if (qr) qr[i] = r;
@@ -235,10 +235,10 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
     memset(J, 0, sizeof(double) * n * n);
     memset(dwdT, 0, sizeof(double) * KK);
   }
-  const double lnT = log(T), invT = 1.0 / T;
+  const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   for (int i = 0; i < m->II; ++i) {
     rxn_eval e;
-    eval_reaction(m, i, T, lnT, invT, C, Ctot, g_RT, h_RT, &e);
+    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, &e);
     const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
     const int* rs = m->rsp + CKO_SLOTS * i;
     const int* ps = m->psp + CKO_SLOTS * i;

@@ -1,0 +1,97 @@
+"""Second, independent CPU restatement of thermo + ROP in numpy (test infrastructure only).
+
+Written in matrix form (dense stoichiometric matrices nu' and nu'' [II, KK], Kc from the
+stoichiometric change of g/RT) rather than the slot loops of ckoracle.c, so the two CPU
+restatements share no code path.  Used by tests to pin the C oracle's kinetics, and with
+scipy's Radau to pin the C oracle's integrator.  Standard Chemkin-II gas kinetics (the closed
+library's call sites: chemkin_wrapper.py:375-498, mixture.py:1442,1551).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+BOLTZMANN = 1.3806504e-16
+AVOGADRO = 6.02214179e23
+RU = BOLTZMANN * AVOGADRO
+PATM = 1.01325e6
+
+
+class NumpyKinetics:
+    def __init__(self, tables):
+        t = tables
+        self.KK = KK = int(t["KK"])
+        self.II = II = int(t["II"])
+        self.wt = t["wt"]
+        self.th = t["thermo"]
+        self.nuf = np.zeros((II, KK))
+        self.nur = np.zeros((II, KK))
+        for i in range(II):
+            for s in range(int(t["nr"][i])):
+                self.nuf[i, t["rsp"][i, s]] += t["rnu"][i, s]
+            for s in range(int(t["np"][i])):
+                self.nur[i, t["psp"][i, s]] += t["pnu"][i, s]
+        self.dnu_mat = self.nur - self.nuf
+        self.arr = t["arr"]
+        self.low = t["low"]
+        self.revp = t["revp"]
+        self.has_rev = t["has_rev"].astype(bool)
+        self.rev = t["rev"].astype(bool)
+        self.rtype = t["rtype"]
+        self.ftype = t["ftype"]
+        self.fpar = t["fpar"]
+        self.tbsp = t["tbsp"]
+        self.eff = np.ones((II, KK))
+        for i in range(II):
+            for p in range(t["eff_ptr"][i], t["eff_ptr"][i + 1]):
+                self.eff[i, t["eff_sp"][p]] = t["eff_val"][p]
+
+    def thermo(self, T):
+        th = self.th
+        hi = T > th[:, 1]
+        a = np.where(hi[:, None], th[:, 10:17], th[:, 3:10])
+        cp = a[:, 0] + T * (a[:, 1] + T * (a[:, 2] + T * (a[:, 3] + T * a[:, 4])))
+        h = a[:, 0] + T * (a[:, 1] / 2 + T * (a[:, 2] / 3 + T * (a[:, 3] / 4 + T * a[:, 4] / 5))) + a[:, 5] / T
+        s = a[:, 0] * np.log(T) + T * (a[:, 1] + T * (a[:, 2] / 2 + T * (a[:, 3] / 3 + T * a[:, 4] / 4))) + a[:, 6]
+        return cp, h, s
+
+    def rates(self, T, P, Y):
+        Y = np.asarray(Y, dtype=np.float64)
+        rho = P / (RU * T) / np.sum(Y / self.wt)
+        C = rho * Y / self.wt
+        cp, h, s = self.thermo(T)
+        g = h - s
+        kf = np.exp(self.arr[:, 0] + self.arr[:, 1] * np.log(T) - self.arr[:, 2] / T)
+        M = self.eff @ C
+        tbc = self.tbsp >= 0
+        M = np.where(tbc, C[np.maximum(self.tbsp, 0)], M)
+        mfac = np.where(self.rtype == 1, M, 1.0)
+        fo = self.rtype == 2
+        k0 = np.exp(self.low[:, 0] + self.low[:, 1] * np.log(T) - self.low[:, 2] / T)
+        with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+            Pr = np.where(fo, k0 * M / kf, 0.0)
+            a, T3, T1, T2 = self.fpar[:, 0], self.fpar[:, 1], self.fpar[:, 2], self.fpar[:, 3]
+            Fc = (1 - a) * np.exp(-T / np.where(T3 != 0, T3, 1.0)) + a * np.exp(-T / np.where(T1 != 0, T1, 1.0))
+            Fc = Fc + np.where(self.ftype == 3, np.exp(-T2 / T), 0.0)
+            lFc = np.log10(np.maximum(Fc, 1e-300))
+            lPr = np.log10(np.maximum(Pr, 1e-300))
+            c = -0.4 - 0.67 * lFc
+            nn = 0.75 - 1.27 * lFc
+            f1 = (lPr + c) / (nn - 0.14 * (lPr + c))
+            Ftroe = 10.0 ** (lFc / (1 + f1 ** 2))
+            X = 1.0 / (1.0 + lPr ** 2)
+            Fsri = self.fpar[:, 3] * (self.fpar[:, 0] * np.exp(-self.fpar[:, 1] / T) + np.exp(-T / np.where(self.fpar[:, 2] != 0, self.fpar[:, 2], 1.0))) ** X * T ** self.fpar[:, 4]
+        F = np.where((self.ftype == 2) | (self.ftype == 3), Ftroe, np.where(self.ftype == 4, Fsri, 1.0))
+        kinf = kf.copy()
+        kf = np.where(fo, kf * Pr / (1 + Pr) * F, kf)
+        dG = self.dnu_mat @ g
+        dn = self.dnu_mat.sum(axis=1)
+        Kc = np.exp(-dG) * (PATM / (RU * T)) ** dn
+        kr_rev = np.exp(self.revp[:, 0] + self.revp[:, 1] * np.log(T) - self.revp[:, 2] / T)
+        kr_rev = np.where(fo, kr_rev * kf / kinf, kr_rev)
+        kr = np.where(self.rev, np.where(self.has_rev, kr_rev, kf / Kc), 0.0)
+        pf = np.prod(C[None, :] ** self.nuf, axis=1)
+        pr = np.prod(C[None, :] ** self.nur, axis=1)
+        qf = mfac * kf * pf
+        qr = mfac * kr * pr
+        wdot = self.dnu_mat.T @ (qf - qr)
+        return qf, qr, wdot

@@ -21,7 +21,7 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libckmi.so")
 
 SLOTS = 4
 NSTAT = 8
-STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "reserved")
+STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "nni")
 RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures"}
 
 
@@ -215,6 +215,10 @@ class DeviceMechanism:
 
     def reactor_run(self, cfg: ReactorCfg, problem, T0, P0, V0, Y0, t_save=None, out=None):
         """Integrate n independent reactors. Y0 is [n][KK]. Returns a dict of device tensors."""
+        if not isinstance(problem, torch.Tensor):
+            pv = np.asarray(problem)
+            if pv.size and not np.all((pv == 1) | (pv == 2)):
+                raise NativeError("problem must be 1 (CONP) or 2 (CONV) for every reactor")
         T0 = self._dev(T0).reshape(-1)
         n = T0.numel()
         P0 = self._dev(P0).reshape(-1)

@@ -10,7 +10,7 @@ SRC = os.path.join(HERE, "csrc", "ckmi.hip")
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp")] + [
     os.path.join(HERE, "..", "include", "ckmi.h")]
 OUT = os.path.join(HERE, "_lib", "libckmi.so")
-ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X only
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics", "-mcode-object-version=5",

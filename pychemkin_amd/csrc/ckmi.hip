@@ -99,6 +99,7 @@ __device__ __forceinline__ int bdf_nls(Bdf& b, BdfS& S, Wave<N>& w, int nflag) {
     for (;;) {
       const double rhs = act ? S.gamma * b.ftemp - (S.rl1 * b.zn[1] + b.acor) : 0.0;
       double x = w.solve(rhs);
+      S.nni++;
       if (S.gamrat != 1.0) x *= 2.0 / (1.0 + S.gamrat);
       if (!act) x = 0.0;
       const double del = wrms_lane(x, b.ewt, n);
@@ -486,7 +487,7 @@ __global__ __launch_bounds__(WAVE) void reactor_kernel(MechDev M, const ckmi_rea
   S.rtol = cfg->rtol;
   S.atol = cfg->atol;
   S.nneg = cfg->nneg;
-  S.ncf_tot = S.nef_tot = S.nlu = S.nfe = S.nje = 0;
+  S.ncf_tot = S.nef_tot = S.nlu = S.nfe = S.nje = S.nni = 0;
   const double tend = cfg->t_end;
   const double hmax = cfg->hmax > 0.0 ? cfg->hmax : tend / 100.0;
   S.hmax_inv = 1.0 / hmax;
@@ -604,7 +605,7 @@ __global__ __launch_bounds__(WAVE) void reactor_kernel(MechDev M, const ckmi_rea
     st[CKMI_STAT_NCF] = S.ncf_tot;
     st[CKMI_STAT_NEF] = S.nef_tot;
     st[CKMI_STAT_STATUS] = status;
-    st[7] = 0;
+    st[CKMI_STAT_NNI] = S.nni;
   }
   if (isp) Y_o[(size_t)r * KK + lane - 1] = yf;
 }
@@ -641,7 +642,7 @@ __global__ __launch_bounds__(WAVE) void rop_kernel(MechDev M, int nstate, const 
   }
   const double Wbar = 1.0 / wave_sum(s);
   const double rho = P * Wbar / (RU * T);
-  const double lnT = log(T), invT = 1.0 / T;
+  const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   double cpm = 0.0, hm = 0.0, ctot = 0.0;
   for (int k = lane; k < KK; k += WAVE) {
     const int c = k / WAVE;
@@ -668,7 +669,7 @@ __global__ __launch_bounds__(WAVE) void rop_kernel(MechDev M, int nstate, const 
     const int nrp = M.nrp[i];
     const int nr = nrp & 0xff, np = nrp >> 8;
     if (nr + np == 0) continue;
-    const RxnEval e = eval_rxn(M, i, T, lnT, invT, C, gRT, nullptr, Mg, false);
+    const RxnEval e = eval_rxn(M, i, T, lnT, invT, lnPRT, C, gRT, nullptr, Mg, false);
     const double qf = e.mfac * e.kf * e.pf, qr = e.mfac * e.kr * e.pr;
     if (MODE == 1) {
       const int oi = M.orig[i];

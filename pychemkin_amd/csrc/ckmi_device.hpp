@@ -120,7 +120,7 @@ struct RxnEval {
 // Rate coefficients and concentration products of device reaction slot i at (T, C).
 // C, gRT, hRT, Mg live in LDS.  Mirrors oracle/ckoracle.c eval_reaction().
 __device__ __forceinline__ RxnEval eval_rxn(const MechDev& M, int i, double T, double lnT, double invT,
-                                            const double* C, const double* gRT, const double* hRT,
+                                            double lnPRT, const double* C, const double* gRT, const double* hRT,
                                             const double* Mg, bool need_h) {
   const int fl = M.flags[i];
   const int type = fl & 3;
@@ -187,7 +187,7 @@ __device__ __forceinline__ RxnEval eval_rxn(const MechDev& M, int i, double T, d
         }
       }
       const double dnu = M.dnu[i];
-      kr = kf * exp(dG - dnu * log(PATM / (RU * T)));
+      kr = kf * exp(dG - dnu * lnPRT);
       dlkr = dlkf - (dH - dnu) * invT;
     }
   }

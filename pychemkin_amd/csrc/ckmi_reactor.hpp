@@ -98,7 +98,7 @@ __device__ __forceinline__ double reactor_rhs(const MechDev& M, const RunCtx& R,
     rho = R.rho0 * R.V0 / V;
     P = rho * RU * T / Wbar;
   }
-  const double lnT = log(T), invT = 1.0 / T;
+  const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   const double Ck = rho * Yk * rw;
   SpThermo th;
   th.cpR = th.hRT = th.sR = 0.0;
@@ -129,7 +129,7 @@ __device__ __forceinline__ double reactor_rhs(const MechDev& M, const RunCtx& R,
     const int nrp = M.nrp[i];
     const int nr = nrp & 0xff, np = nrp >> 8;
     if (nr + np == 0) continue;
-    const RxnEval e = eval_rxn(M, i, T, lnT, invT, L.C, L.gRT, L.hRT, L.Mg, WITH_J);
+    const RxnEval e = eval_rxn(M, i, T, lnT, invT, lnPRT, L.C, L.gRT, L.hRT, L.Mg, WITH_J);
     const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
     const int4 rs = M.rsp[i], ps = M.psp[i];
     double rn[SLOTS], pn[SLOTS];
@@ -283,7 +283,7 @@ __device__ __forceinline__ double pick(const double (&v)[S], int i) {
 struct BdfS {
   double h, hscale, hprime, eta, etamax, hmax_inv, hmin, tn, rl1, gamma, gammap, gamrat, crate, acnrm, saved_tq5, hu;
   double l[QMAX + 1], tq[6], tau[QMAX + 2];
-  int q, qprime, qwait, L, nst, nstlp, nstlj, jcur, ncf_tot, nef_tot, nlu, nfe, nje;
+  int q, qprime, qwait, L, nst, nstlp, nstlj, jcur, ncf_tot, nef_tot, nlu, nfe, nje, nni;
   double rtol, atol;
   int nneg;
 };

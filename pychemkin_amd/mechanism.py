@@ -198,6 +198,7 @@ class Mechanism:
         if missing:
             raise MechanismError(f"no thermo data for species {missing}")
         self.thermo = {s: data[s.upper()] for s in self.species}
+        self._A_override: Dict[int, float] = {}
         self._finish()
 
     @classmethod
@@ -258,6 +259,13 @@ class Mechanism:
                 section = None
                 current = None
                 continue
+            end_here = False
+            if section in ("ELEMENTS", "SPECIES"):
+                toks = s.split()
+                if any(t.upper() == "END" for t in toks):
+                    cut = [t.upper() for t in toks].index("END")
+                    s = " ".join(toks[:cut])
+                    end_here = True
             if section == "ELEMENTS":
                 for tok in re.findall(r"([A-Za-z][A-Za-z0-9]*)\s*(?:/\s*(" + _NUM + r")\s*/)?", s):
                     el = tok[0].upper()
@@ -274,6 +282,10 @@ class Mechanism:
                 for tok in s.split():
                     if tok.upper() not in (x.upper() for x in self.species):
                         self.species.append(tok)
+            if end_here:
+                section = None
+                current = None
+                continue
             elif section == "THERMO":
                 thermo_lines.append(raw_lines[ln_no])
             elif section == "REACTIONS":
@@ -437,9 +449,21 @@ class Mechanism:
     def MM(self) -> int:
         return len(self.elements)
 
+    def set_A_cgs(self, i: int, A: float) -> None:
+        """Override the forward pre-exponential factor of reaction i (0-based) in cgs units."""
+        if not (0 <= i < self.II) or not (A > 0.0):
+            raise MechanismError("bad reaction index or A-factor")
+        self._A_override[i] = float(A)
+
+    def A_cgs(self, i: int) -> float:
+        rx = self.reactions[i]
+        if i in self._A_override:
+            return self._A_override[i]
+        return self._A_cgs(rx, rx.A, rx.reactants, True, 1 if rx.kind == RXN_THIRDBODY else 0)
+
     def arrhenius(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """A [cgs], b, E/R [K] as KINGetReactionRateParameters returns them."""
-        A = np.array([self._A_cgs(rx, rx.A, rx.reactants, forward=True) for rx in self.reactions])
+        A = np.array([self.A_cgs(i) for i in range(self.II)])
         b = np.array([rx.b for rx in self.reactions])
         E = np.array([rx.E * rx.E_scale for rx in self.reactions])
         return A, b, E
@@ -501,7 +525,7 @@ class Mechanism:
                 psp[i, j] = idx[sp]
                 pnu[i, j] = nu
             extra = 1 if rx.kind == RXN_THIRDBODY else 0
-            A = self._A_cgs(rx, rx.A, rx.reactants, True, extra)
+            A = self.A_cgs(i)
             arr[i] = (math.log(A) if A > 0 else -1e300, rx.b, rx.E * rx.E_scale)
             if rx.kind == RXN_FALLOFF:
                 if rx.low is None:

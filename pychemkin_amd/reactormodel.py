@@ -1,0 +1,206 @@
+"""Reactor framework: keywords, profiles and the reactor-model base (reference reactormodel.py).
+
+The reference serialises every solver/output option as Chemkin keyword text and sends it
+line by line to the closed library (reactormodel.py:50-372,861-996; batchreactor.py:1106).
+Here the same keyword objects are kept (same names, protected-keyword rule of
+reactormodel.py:60-93) but they are translated once into a typed ckmi_reactor_cfg struct
+(pychemkin_amd._native.make_cfg) for the whole batch -- no per-reactor text parsing.
+"""
+from __future__ import annotations
+
+import copy
+from typing import List, Union
+
+import numpy as np
+
+from .logger import logger
+from .mixture import Mixture
+
+
+class ReactorError(RuntimeError):
+    pass
+
+
+class Keyword:
+    """A Chemkin keyword and its value (reference reactormodel.py:50-372)."""
+
+    _protectedkeywords = ["CONP", "CONV", "TRAN", "STST", "TGIV", "ENRG", "PRES", "TEMP", "TAU", "TIME", "XEND",
+                          "FLRT", "VDOT", "SCCM", "DIAM", "AREA", "REAC", "GAS", "INIT", "XEST", "SURF", "ACT",
+                          "TINL", "FUEL", "OXID", "PROD", "ASEN", "ATLS", "RTLS", "EPST", "EPSS"]
+    profilekeywords = ["TPRO", "PPRO", "VPRO", "QPRO", "AINT", "AEXT", "DPRO", "FPRO", "SCCMPRO", "VDOTPRO", "VELPRO",
+                       "TINPRO", "AFLO"]
+    noFullKeyword = True
+
+    def __init__(self, phrase: str, value: Union[int, float, bool, str], data_type: str = ""):
+        self.keyphrase = phrase.upper()
+        self.value = value
+        self.data_type = data_type or type(value).__name__
+
+    def resetvalue(self, value) -> None:
+        self.value = value
+
+    def getvalue_as_string(self):
+        if isinstance(self.value, bool):
+            line = self.keyphrase
+        else:
+            line = f"{self.keyphrase}    {self.value}"
+        return len(line), line
+
+
+class Profile:
+    """A piecewise-linear profile keyword such as VPRO (reference reactormodel.py:467-665)."""
+
+    def __init__(self, key: str, x, y):
+        x = np.asarray(x, dtype=np.float64)
+        y = np.asarray(y, dtype=np.float64)
+        if x.shape != y.shape or x.ndim != 1 or len(x) < 2:
+            raise ReactorError("profile position and value arrays must be 1-D with the same size >= 2")
+        if np.any(np.diff(x) <= 0.0):
+            raise ReactorError("profile positions must be strictly increasing")
+        self.profilekey = key.upper()
+        self.x = x
+        self.y = y
+
+    @property
+    def size(self) -> int:
+        return len(self.x)
+
+
+class ReactorModel:
+    """Base of the reactor models: initial mixture, keywords, run status, raw solution."""
+
+    def __init__(self, reactor_condition: Mixture, label: str):
+        if not isinstance(reactor_condition, Mixture):
+            raise ReactorError("the first argument must be a Mixture object")
+        if reactor_condition.validate() != 0:
+            raise ReactorError("the reactor mixture needs temperature, pressure and composition")
+        self.reactormixture = copy.deepcopy(reactor_condition)
+        self._chem = reactor_condition.chemistry
+        self._specieslist = reactor_condition._specieslist
+        self.numbspecies = reactor_condition.KK
+        self.label = label
+        self._keyword_index: List[str] = []
+        self._keyword_list: List[Keyword] = []
+        self._profiles_index: List[str] = []
+        self._profiles_list: List[Profile] = []
+        self.runstatus = -100
+        self._solution_tags = ["time", "distance", "temperature", "pressure", "volume", "velocity", "flowrate"]
+        self._speciesmode = "mass"
+        self._numbsolutionpoints = 0
+        self._solution_rawarray: dict = {}
+        self._solution_mixturearray: List[Mixture] = []
+        self._gasratemultiplier = 1.0
+
+    # ------------------------------------------------------------------ state
+    @property
+    def temperature(self) -> float:
+        return self.reactormixture.temperature
+
+    @temperature.setter
+    def temperature(self, t: float):
+        self.reactormixture.temperature = t
+
+    @property
+    def pressure(self) -> float:
+        return self.reactormixture.pressure
+
+    @pressure.setter
+    def pressure(self, p: float):
+        self.reactormixture.pressure = p
+
+    def list_composition(self, mode: str = "mole", option: str = " ", bound: float = 0.0) -> None:
+        self.reactormixture.list_composition(mode, option, bound)
+
+    # ------------------------------------------------------------------ keywords
+    def setkeyword(self, key: str, value: Union[bool, int, float, str]) -> None:
+        """Set a Chemkin keyword (reference reactormodel.py:861-914)."""
+        k = key.upper()
+        if Keyword.noFullKeyword and k in Keyword._protectedkeywords and not getattr(self, "_internal_set", False):
+            raise ReactorError(f"keyword {k} must be set through the reactor properties")
+        if k in self._keyword_index:
+            i = self._keyword_index.index(k)
+            if isinstance(value, bool) and not value:
+                del self._keyword_list[i]
+                del self._keyword_index[i]
+            else:
+                self._keyword_list[i].resetvalue(value)
+            return
+        if isinstance(value, bool) and not value:
+            return
+        self._keyword_list.append(Keyword(k, value))
+        self._keyword_index.append(k)
+
+    def _set_internal(self, key: str, value) -> None:
+        self._internal_set = True
+        try:
+            self.setkeyword(key, value)
+        finally:
+            self._internal_set = False
+
+    def removekeyword(self, key: str) -> None:
+        k = key.upper()
+        if k in self._keyword_index:
+            i = self._keyword_index.index(k)
+            del self._keyword_list[i]
+            del self._keyword_index[i]
+
+    def getkeyword(self, key: str, default=None):
+        k = key.upper()
+        if k in self._keyword_index:
+            return self._keyword_list[self._keyword_index.index(k)].value
+        return default
+
+    def showkeywordinputlines(self) -> None:
+        print("** INPUT KEYWORDS: \n")
+        print("=" * 40)
+        for k in self._keyword_list:
+            print(k.getvalue_as_string()[1])
+        for p in self._profiles_list:
+            for x, y in zip(p.x, p.y):
+                print(f"{p.profilekey}    {x}  {y}")
+        print("=" * 40)
+
+    def setprofile(self, profile: Profile) -> None:
+        if profile.profilekey in self._profiles_index:
+            self._profiles_list[self._profiles_index.index(profile.profilekey)] = profile
+        else:
+            self._profiles_index.append(profile.profilekey)
+            self._profiles_list.append(profile)
+
+    def getprofile(self, key: str):
+        k = key.upper()
+        if k in self._profiles_index:
+            return self._profiles_list[self._profiles_index.index(k)]
+        return None
+
+    @property
+    def gasratemultiplier(self) -> float:
+        return self._gasratemultiplier
+
+    @gasratemultiplier.setter
+    def gasratemultiplier(self, value: float):
+        if value <= 0.0:
+            raise ReactorError("gas rate multiplier must be > 0")
+        self._gasratemultiplier = float(value)
+        self._set_internal("GFAC", float(value))
+
+    # ------------------------------------------------------------------ status
+    def setrunstatus(self, code: int) -> None:
+        self.runstatus = int(code)
+
+    def getrunstatus(self, mode: str = "silent") -> int:
+        if mode != "silent":
+            if self.runstatus == -100:
+                logger.info("reactor %s has not been run", self.label)
+            elif self.runstatus != 0:
+                logger.info("reactor %s failed with status %d", self.label, self.runstatus)
+        return self.runstatus
+
+    def getrawsolutionstatus(self) -> bool:
+        return bool(self._solution_rawarray)
+
+    def getmixturesolutionstatus(self) -> bool:
+        return bool(self._solution_mixturearray)
+
+    def getnumbersolutionpoints(self) -> int:
+        return self._numbsolutionpoints

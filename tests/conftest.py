@@ -1,0 +1,92 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+CHEM = os.path.join(ROOT, "data", "grimech30_chem.inp")
+THERM = os.path.join(ROOT, "data", "grimech30_thermo.dat")
+P_ATM = 1.01325e6
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+
+
+def golden(name):
+    with open(os.path.join(ROOT, "tests", "golden", name + ".json")) as f:
+        return json.load(f)
+
+
+def gpu_available():
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def mech():
+    from pychemkin_amd.mechanism import Mechanism
+
+    return Mechanism.from_files(CHEM, THERM)
+
+
+@pytest.fixture(scope="session")
+def tables(mech):
+    return mech.to_tables()
+
+
+@pytest.fixture(scope="session")
+def oracle(mech):
+    from oracle.oracle import Oracle
+
+    return Oracle(mech)
+
+
+@pytest.fixture(scope="session")
+def chem():
+    import pychemkin_amd as ck
+
+    c = ck.Chemistry(label="GRI 3.0")
+    c.chemfile = CHEM
+    c.thermfile = THERM
+    c.preprocess()
+    return c
+
+
+def ch4_air_Y(mech, phi):
+    phi = np.atleast_1d(np.asarray(phi, dtype=np.float64))
+    X = np.zeros((phi.size, mech.KK))
+    alpha = 2.0 / 0.21
+    X[:, mech.species.index("CH4")] = phi
+    X[:, mech.species.index("O2")] = 0.21 * alpha
+    X[:, mech.species.index("N2")] = 0.79 * alpha
+    X /= X.sum(axis=1, keepdims=True)
+    Y = X * mech.wt
+    return Y / Y.sum(axis=1, keepdims=True)
+
+
+def h2_air_Y(mech):
+    """H2:O2:N2 = 2:1:3.76 (closed_homogeneous__transient.py:62)."""
+    X = np.zeros(mech.KK)
+    X[mech.species.index("H2")] = 2.0
+    X[mech.species.index("O2")] = 1.0
+    X[mech.species.index("N2")] = 3.76
+    X /= X.sum()
+    Y = X * mech.wt
+    return Y / Y.sum()
+
+
+def within(a, b, atol, rtol):
+    """Symmetric golden tolerance |a - b| <= atol + rtol |b| (SURVEY.md section 4 comparator fix)."""
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return np.abs(a - b) <= atol + rtol * np.abs(b)

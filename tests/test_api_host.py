@@ -1,0 +1,115 @@
+"""Host-side logic of the drop-in API (no GPU calls): composition, keywords, output grid."""
+import numpy as np
+import pytest
+
+import pychemkin_amd as ck
+from conftest import P_ATM, golden
+from pychemkin_amd import _native
+from pychemkin_amd.batchreactor import save_times
+from pychemkin_amd.reactormodel import ReactorError
+
+
+def test_preprocess_sizes(chem):
+    assert chem.KK == 53 and chem.IIGas == 325 and chem.MM == 5
+    assert chem.get_specindex("H2") == 0  # the reference rejects index 0 (chemistry.py:911-916)
+    assert chem.get_specindex("n2") == 47
+    assert chem.SpeciesComposition().shape == (5, 53)
+    assert chem.SpeciesComposition(elemindex=1, specindex=chem.get_specindex("CH4")) == 4
+
+
+def test_air_density_and_conversions(chem):
+    air = ck.Mixture(chem)
+    air.pressure = P_ATM
+    air.temperature = 300.0
+    air.X = ck.Air.X()
+    g = golden("simple")
+    assert abs(air.RHO / g["state-density"][0] - 1) < 1e-15
+    y = air.Y
+    x = ck.Mixture.mass_fraction_to_mole_fraction(y, chem.WT)
+    assert np.allclose(x, air.X, rtol=1e-14)
+    assert abs(air.WTM - (0.21 * chem.WT[3] + 0.79 * chem.WT[47])) < 1e-12
+
+
+def test_equivalence_ratio_matches_conv_baseline(chem):
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    pre = ck.Mixture(chem)
+    assert pre.X_by_Equivalence_Ratio(chem, fuel.X, air.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"], 0.7) == 0
+    assert abs(pre.X[chem.get_specindex("CH4")] / golden("CONV")["species-CH4_mole_fraction"][0] - 1) < 1e-14
+    pre2 = ck.Mixture(chem)
+    pre2.X_by_Equivalence_Ratio(chem, fuel.X, air.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"], 1.0)
+    assert abs(pre2.X[chem.get_specindex("CH4")] - 0.0950226) < 1e-7
+
+
+def test_output_grid_matches_golden_times():
+    g = golden("closed_homogeneous__transient")
+    ts = save_times(5e-4, 5e-4 / 100)
+    assert ts.tolist() == g["state-time"]
+    g2 = golden("CONV")
+    assert save_times(0.1, 0.01).tolist() == g2["state-time"]
+
+
+def _reactor(chem):
+    m = ck.Mixture(chem)
+    m.X = [("H2", 2.0), ("N2", 3.76), ("O2", 1.0)]
+    m.pressure = P_ATM
+    m.temperature = 1000.0
+    return ck.GivenPressureBatchReactor_EnergyConservation(m, label="tran")
+
+
+def test_keywords_to_cfg(chem):
+    r = _reactor(chem)
+    with pytest.raises(ReactorError):
+        r.reactor_cfg()  # TIME required
+    r.time = 5e-4
+    r.volume = 1.0
+    r.tolerances = (1e-30, 1e-14)
+    assert r.tolerances == (1e-20, 1e-12)  # clamps of batchreactor.py:193-214
+    r.force_nonnegative = True
+    r.set_ignition_delay(method="T_rise", val=400)
+    r.stop_after_ignition()
+    r.set_solver_max_timestep_size(1e-5)
+    cfg = r.reactor_cfg()
+    assert (cfg.energy, cfg.t_end, cfg.atol, cfg.rtol, cfg.nneg, cfg.ign_mode, cfg.ign_val, cfg.ign_stop, cfg.hmax) == \
+        (1, 5e-4, 1e-20, 1e-12, 1, 2, 400.0, 1, 1e-5)
+    r.set_ignition_delay(method="Species_peak", target="OH")
+    cfg = r.reactor_cfg()
+    assert cfg.ign_mode == 4 and cfg.ign_species == chem.get_specindex("OH")
+    with pytest.raises(ReactorError):
+        r.setkeyword("TIME", 1.0)  # protected (reactormodel.py:60-93)
+    with pytest.raises(ReactorError):
+        r.set_ignition_delay(method="bogus")
+
+
+def test_volume_profile_cfg(chem):
+    m = ck.Mixture(chem)
+    m.X = [("CH4", 0.1), ("O2", 0.2), ("N2", 0.7)]
+    m.pressure = 3 * P_ATM
+    m.temperature = 800.0
+    r = ck.GivenVolumeBatchReactor_EnergyConservation(m, label="RCM")
+    r.volume = 10.0
+    r.time = 0.1
+    r.set_volume_profile([0.0, 0.01, 2.0], [10.0, 4.0, 4.0])
+    cfg = r.reactor_cfg()
+    assert cfg.nprof == 3 and list(cfg.prof_v[:3]) == [10.0, 4.0, 4.0]
+    r.heat_loss_rate = 5.0
+    with pytest.raises(ReactorError):
+        r.reactor_cfg()
+
+
+def test_afactor_get_set(chem):
+    A0 = chem.get_reaction_AFactor(1)
+    assert A0 == 1.2e17
+    chem.set_reaction_AFactor(1, 2.4e17)
+    assert chem.get_reaction_parameters()[0][0] == 2.4e17
+    chem.set_reaction_AFactor(1, A0)
+    assert chem.get_gas_reaction_string(52) == "H+CH3(+M)<=>CH4(+M)"
+    with pytest.raises(Exception):
+        chem.set_reaction_AFactor(0, 1.0)
+
+
+def test_make_cfg_rejects_long_profiles():
+    with pytest.raises(ValueError):
+        _native.make_cfg(profile=(np.arange(70.0), np.ones(70)))

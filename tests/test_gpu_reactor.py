@@ -1,0 +1,229 @@
+"""Batch-reactor kernel (ckmi_reactor_run) vs the CPU oracle and the reference goldens.
+
+Parity bar (BASELINE.json north_star): ignition delay within 0.5 % relative, final T and major
+species within rtol 1e-4.  The kernel runs the oracle's integrator step for step, so in
+practice the agreement is ~1e-8 or better; the tests assert the north_star bar plus a tighter
+"same algorithm" bar on tau (1e-6).
+"""
+import numpy as np
+import pytest
+
+from conftest import P_ATM, ch4_air_Y, golden, h2_air_Y, within
+
+pytestmark = pytest.mark.gpu
+
+MAJOR = ("CH4", "O2", "N2", "H2O", "CO2", "CO", "H2")
+
+
+@pytest.fixture(scope="module")
+def dm(tables):
+    from pychemkin_amd import _native
+
+    return _native.DeviceMechanism(tables)
+
+
+def _run_both(dm, oracle, mech, cases, **cfg):
+    from pychemkin_amd import _native
+
+    T0 = np.array([c[0] for c in cases], float)
+    P0 = np.array([c[1] for c in cases], float) * P_ATM
+    Y0 = np.stack([ch4_air_Y(mech, c[2])[0] for c in cases])
+    prob = np.array([c[3] for c in cases], np.int32)
+    V0 = np.ones(len(cases))
+    res = dm.reactor_run(_native.make_cfg(**cfg), prob, T0, P0, V0, Y0)
+    res = {k: v.cpu().numpy() for k, v in res.items()}
+    ref = [oracle.reactor(T0[i], P0[i], 1.0, Y0[i], problem=int(prob[i]), **cfg) for i in range(len(cases))]
+    return res, ref
+
+
+def _check(res, ref, mech, tau_rtol=1e-6):
+    for i, (r, Ye) in enumerate(ref):
+        assert res["stats"][i, 6] == r.status == 0
+        if r.tau > 0:
+            assert abs(res["tau"][i] / r.tau - 1) < min(tau_rtol, 5e-3)
+        else:
+            assert res["tau"][i] == r.tau
+        assert abs(res["T"][i] / r.T - 1) < 1e-4
+        for sp in MAJOR:
+            k = mech.species.index(sp)
+            assert abs(res["Y"][i, k] - Ye[k]) <= 1e-4 * max(abs(Ye[k]), 1e-3)
+
+
+CASES = [(1200, 1, 1.0, 1), (1200, 1, 1.0, 2), (1100, 1, 0.5, 1), (1700, 100, 2.0, 1), (1000, 3, 0.7, 2),
+         (1400, 10, 1.0, 1), (1550, 30, 1.5, 2), (1300, 100, 0.5, 2)]
+
+
+def test_conp_conv_energy_tifp(dm, oracle, mech):
+    res, ref = _run_both(dm, oracle, mech, CASES, energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
+    _check(res, ref, mech)
+    # the kernel reproduces the oracle's step sequence
+    assert np.array_equal(res["stats"][:, 0], np.array([r.nst for r, _ in ref]))
+
+
+def test_given_temperature(dm, oracle, mech):
+    res, ref = _run_both(dm, oracle, mech, CASES[:4], energy=2, t_end=2e-3, atol=1e-12, rtol=1e-7)
+    _check(res, ref, mech)
+    assert np.allclose(res["T"], [c[0] for c in CASES[:4]], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("mode,val,target,stop", [("T_rise", 400.0, None, True), ("T_ignition", 1800.0, None, False),
+                                                  ("Species_peak", 0.0, "OH", False)])
+def test_ignition_definitions(dm, oracle, mech, mode, val, target, stop):
+    sp = mech.species.index(target) if target else 0
+    res, ref = _run_both(dm, oracle, mech, CASES[:6], energy=1, t_end=0.5, atol=1e-10, rtol=1e-8, ign_mode=mode,
+                         ign_val=val, ign_species=sp, ign_stop=stop, nneg=True)
+    _check(res, ref, mech)
+    assert np.all(res["tau"] > 0)
+
+
+def test_h2_air_golden_through_drop_in_api(chem):
+    """closed_homogeneous__transient.py:61-131 through the PyChemkin-style API on the GPU."""
+    import pychemkin_amd as ck
+
+    g = golden("closed_homogeneous__transient")
+    m = ck.Mixture(chem)
+    m.X = [("H2", 2.0), ("O2", 1.0), ("N2", 3.76)]
+    m.temperature = 1000.0
+    m.pressure = P_ATM
+    r = ck.GivenPressureBatchReactor_EnergyConservation(m, label="tran")
+    r.time = 5e-4
+    r.tolerances = (1e-20, 1e-8)
+    r.force_nonnegative = True
+    r.timestep_for_saving_solution = 5e-4 / 100
+    r.set_ignition_delay(method="T_rise", val=400)
+    assert r.run() == 0
+    r.process_solution()
+    t = r.get_solution_variable_profile("time")
+    T = r.get_solution_variable_profile("temperature")
+    assert t.tolist() == g["state-time"]
+    Tg = np.asarray(g["state-temperature"])
+    assert within(T, Tg, *g["tolerance-var"]).sum() >= 90
+    assert abs(T[-1] / Tg[-1] - 1) < 2e-5
+    tg = np.interp(1400.0, Tg, t)
+    assert abs(r.get_ignition_delay() * 1e-3 / tg - 1) < 2e-3
+    rho = np.array([r.get_solution_mixture_at_index(i).RHO for i in range(len(t))])
+    assert np.all(np.abs(rho / np.asarray(g["state-density"]) - 1) < 2e-3)
+
+
+def test_rcm_conv_volume_profile_golden(chem, oracle, mech):
+    """CONV.py:62-140 on the GPU: VPRO 10 -> 4 cm3 in 10 ms, then hold; CONV + ENERGY, TIFP."""
+    import pychemkin_amd as ck
+
+    g = golden("CONV")
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    m = ck.Mixture(chem)
+    m.X_by_Equivalence_Ratio(chem, fuel.X, air.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"], 0.7)
+    m.temperature = 800.0
+    m.pressure = 3 * P_ATM
+    r = ck.GivenVolumeBatchReactor_EnergyConservation(m, label="RCM")
+    r.volume = 10.0
+    r.time = 0.1
+    r.tolerances = (1e-10, 1e-8)
+    r.force_nonnegative = True
+    r.timestep_for_saving_solution = 0.01
+    r.set_volume_profile([0.0, 0.01, 2.0], [10.0, 4.0, 4.0])
+    r.set_ignition_delay(method="T_inflection")
+    assert r.run() == 0
+    r.process_solution()
+    T = r.get_solution_variable_profile("temperature")
+    assert np.all(within(T, g["state-temperature"], *g["tolerance-var"]))
+    k = chem.get_specindex("CH4")
+    x = np.array([r.get_solution_mixture_at_index(i).X[k] for i in range(len(T))])
+    assert np.all(within(x, g["species-CH4_mole_fraction"], *g["tolerance-frac"]))
+    assert 30.0 < r.get_ignition_delay() < 40.0
+    res, _ = oracle.reactor(800.0, 3 * P_ATM, 10.0, m.Y, problem=2, energy=1, t_end=0.1, atol=1e-10, rtol=1e-8,
+                            nneg=True, ign_mode="TIFP", profile=([0.0, 0.01, 2.0], [10.0, 4.0, 4.0]))
+    assert abs(r.get_ignition_delay() * 1e-3 / res.tau - 1) < 1e-6
+
+
+def test_pressure_profile_conp(dm, oracle, mech):
+    from pychemkin_amd import _native
+
+    prof = ([0.0, 1e-3, 1.0], [P_ATM, 5 * P_ATM, 5 * P_ATM])
+    cfg = dict(energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP", profile=prof)
+    Y0 = ch4_air_Y(mech, 1.0)
+    res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1], np.int32), [1300.0], [P_ATM], [1.0], Y0)
+    r, Ye = oracle.reactor(1300.0, P_ATM, 1.0, Y0[0], problem=1, **cfg)
+    assert r.status == 0 and int(res["stats"][0, 6]) == 0
+    assert abs(res["tau"][0].item() / r.tau - 1) < 1e-6
+    assert abs(res["P"][0].item() / (5 * P_ATM) - 1) < 1e-12
+
+
+def test_save_points_match_oracle_dense_output(dm, oracle, mech):
+    from pychemkin_amd import _native
+
+    ts = np.linspace(0.0, 2e-3, 41)
+    cfg = dict(energy=1, t_end=2e-3, atol=1e-12, rtol=1e-8, ign_mode="TIFP")
+    Y0 = ch4_air_Y(mech, 1.0)
+    res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1], np.int32), [1500.0], [10 * P_ATM], [1.0], Y0, t_save=ts)
+    _, _, (_, ys, _, _) = oracle.reactor(1500.0, 10 * P_ATM, 1.0, Y0[0], t_save=ts, problem=1, **cfg)
+    got = res["y_save"][0].cpu().numpy()
+    assert np.max(np.abs(got[:, 0] / ys[:, 0] - 1)) < 1e-6
+    assert np.max(np.abs(got[:, 1:] - ys[:, 1:])) < 1e-6
+
+
+def test_determinism_and_batch_order_invariance(dm, mech):
+    from pychemkin_amd import _native
+
+    import bench
+
+    T0, P0, Y0 = bench.sweep(mech, 1, 0, nT=8, nphi=4, nP=4)
+    n = T0.size
+    cfg = _native.make_cfg(**bench.RUN)
+    prob = np.ones(n, np.int32)
+    a = {k: v.cpu().numpy() for k, v in dm.reactor_run(cfg, prob, T0, P0, np.ones(n), Y0).items()}
+    b = {k: v.cpu().numpy() for k, v in dm.reactor_run(cfg, prob, T0, P0, np.ones(n), Y0).items()}
+    perm = np.random.default_rng(1).permutation(n)
+    c = {k: v.cpu().numpy() for k, v in dm.reactor_run(cfg, prob, T0[perm], P0[perm], np.ones(n), Y0[perm]).items()}
+    for k in ("tau", "T", "Y", "stats"):
+        assert np.array_equal(a[k], b[k]), k
+        assert np.array_equal(a[k][perm], c[k]), k
+
+
+def test_sweep_properties_at_scale(dm, mech):
+    """Size-independent properties on 4096 reactors (a 1/16 slice of the bench sweep)."""
+    from pychemkin_amd import _native
+
+    import bench
+
+    T0, P0, Y0 = bench.sweep(mech, 1, 0, nT=16, nphi=16, nP=16)
+    n = T0.size
+    res = {k: v.cpu().numpy() for k, v in dm.reactor_run(_native.make_cfg(**bench.RUN), np.ones(n, np.int32), T0, P0,
+                                                          np.ones(n), Y0).items()}
+    assert np.all(res["stats"][:, 6] == 0)
+    assert np.all(res["tau"] > 0) and np.all(res["tau"] < 1.0)
+    assert np.all(res["T"] > T0 + 300.0)
+    assert np.allclose(res["Y"].sum(axis=1), 1.0, atol=1e-7)
+    ncf = mech.ncf.astype(float)
+    e0 = (Y0 / mech.wt) @ ncf.T
+    e1 = (res["Y"] / mech.wt) @ ncf.T
+    assert np.max(np.abs(e1 - e0) / np.max(e0, axis=1, keepdims=True)) < 1e-7
+    tau = res["tau"].reshape(16, 16, 16)  # (T0, phi, P)
+    assert np.all(np.diff(np.log(tau), axis=0) < 0)  # hotter ignites sooner (no NTC at 1100-1700 K)
+    assert np.all(np.diff(np.log(tau), axis=2) < 0.02)  # higher pressure does not delay (within 2 %)
+
+
+def test_batch_sweep_api_and_sharding(chem, mech):
+    import pychemkin_amd as ck
+
+    T0 = np.linspace(1100, 1600, 12)
+    Y0 = ch4_air_Y(mech, 1.0)
+    sw = ck.BatchSweep(chem, problem="CONP", energy="ENERGY", t_end=1.0, atol=1e-10, rtol=1e-8)
+    r = sw.run(T0, 10 * P_ATM, Y0=Y0)
+    assert np.all(r.status == 0) and np.all(np.diff(r.tau) < 0)
+    r2 = ck.BatchSweep(chem, problem="CONP", energy="ENERGY", t_end=1.0, atol=1e-10, rtol=1e-8, devices=[0, 0]).run(
+        T0, 10 * P_ATM, Y0=Y0)
+    assert np.array_equal(r.tau, r2.tau)
+
+
+def test_invalid_config_fails_loudly(dm, mech):
+    from pychemkin_amd import _native
+
+    Y0 = ch4_air_Y(mech, 1.0)
+    with pytest.raises(_native.NativeError):
+        dm.reactor_run(_native.make_cfg(t_end=-1.0), np.array([1], np.int32), [1200.0], [P_ATM], [1.0], Y0)
+    with pytest.raises(_native.NativeError):
+        dm.reactor_run(_native.make_cfg(t_end=1.0), np.array([3], np.int32), [1200.0], [P_ATM], [1.0], Y0)
