@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reactors", type=int, default=0, help="override reactors per GPU (0 = full 65,536 shard)")
     ap.add_argument("--rop-states", type=int, default=10_000_000)
-    ap.add_argument("--cpu-sample", type=int, default=8192, help="max reactors in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
     args = ap.parse_args()
