@@ -17,7 +17,9 @@ import numpy as np
 import torch  # noqa: F401  (must be loaded before libckmi.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libckmi.so")
+# CKMI_LIB selects another in-tree build of the same ABI (the phase-timer diagnostic build,
+# _lib/libckmi_prof.so, used by scripts/phase_profile.py); it is never a CPU path.
+LIB_PATH = os.environ.get("CKMI_LIB") or os.path.join(_HERE, "_lib", "libckmi.so")
 
 SLOTS = 4
 NSTAT = 8

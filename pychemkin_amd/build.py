@@ -24,16 +24,20 @@ def needs_build() -> bool:
     return any(os.path.getmtime(p) > t for p in [SRC] + DEPS)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+PROF_OUT = os.path.join(HERE, "_lib", "libckmi_prof.so")  # diagnostic phase-timer build
+
+
+def build(force: bool = False, verbose: bool = False, prof: bool = False) -> str:
+    out = PROF_OUT if prof else OUT
+    if not force and not prof and not needs_build():
         return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + ["-o", OUT, SRC]
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + ["-o", out, SRC]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    return OUT
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, prof="--prof" in sys.argv))

@@ -30,334 +30,21 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 enum { NF_FIRST = 0, NF_CONV_FAIL = 1, NF_ERR_FAIL = 2 };
+
+// Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py): per-reactor shader
+// cycles spent in each phase, written to a debug buffer no other code reads.
+enum { PH_RHS = 0, PH_JAC = 1, PH_LU = 2, PH_SOLVE = 3, PH_TOTAL = 4, PH_N = 8 };
+#ifdef CKMI_PHASE_TIMERS
+__device__ unsigned long long* g_phase_buf = nullptr;
+#define PH_T0() const unsigned long long _ph0 = __builtin_amdgcn_s_memtime()
+#define PH_ADD(slot) ph[slot] += __builtin_amdgcn_s_memtime() - _ph0
+#else
+#define PH_T0() (void)0
+#define PH_ADD(slot) (void)0
+#endif
 enum { CF_NONE = 0, CF_BAD_J = 1, CF_OTHER = 2 };
 
 // ---------------------------------------------------------------- reactor kernel
-template <int N>
-struct Wave {
-  const MechDev& M;
-  const RunCtx& R;
-  const Lds& L;
-  int lane, n, ld;
-  int order, permv;
-  double rdiag;
-
-  __device__ Wave(const MechDev& m, const RunCtx& r, const Lds& l, int lane_, int n_, int ld_)
-      : M(m), R(r), L(l), lane(lane_), n(n_), ld(ld_), order(0), permv(0), rdiag(1.0) {}
-
-  __device__ __forceinline__ double f(double t, double yl) { return reactor_rhs<false>(M, R, t, yl, L, lane, n, ld); }
-  __device__ __forceinline__ double fj(double t, double yl) { return reactor_rhs<true>(M, R, t, yl, L, lane, n, ld); }
-
-  // M = I - gamma J from the Jacobian in LDS, factored in LDS (row-per-lane)
-  __device__ __forceinline__ bool build_and_factor(double gamma) {
-    if (lane < n) {
-      const double* jr = L.J + (size_t)lane * ld;
-      double* ar = L.A + (size_t)lane * ld;
-      for (int j = 0; j < n; ++j) ar[j] = (j == lane ? 1.0 : 0.0) - gamma * jr[j];
-    }
-    __syncthreads();
-    return lu_factor_lds(L.A, ld, lane, n, order, permv, rdiag);
-  }
-  __device__ __forceinline__ double solve(double b) { return lu_solve_lds(L.A, ld, lane, n, order, permv, rdiag, b); }
-};
-
-template <int N>
-__device__ __forceinline__ int bdf_nls(Bdf& b, BdfS& S, Wave<N>& w, int nflag) {
-  const int n = w.n;
-  const bool act = w.lane < n;
-  int convfail = (nflag == NF_FIRST || nflag == NF_ERR_FAIL) ? CF_NONE : CF_OTHER;
-  int call_setup = (nflag != NF_FIRST) || S.nst == 0 || S.nst >= S.nstlp + MSBP || fabs(S.gamrat - 1.0) > DGMAX;
-  for (;;) {
-    b.y = b.zn[0];
-    b.ftemp = w.f(S.tn, b.y);
-    S.nfe++;
-    if (call_setup) {
-      const double dgamma = fabs(S.gamma / S.gammap - 1.0);
-      const int jbad = S.nst == 0 || S.nst >= S.nstlj + MSBJ || (convfail == CF_BAD_J && dgamma < DGMAX) ||
-                       convfail == CF_OTHER;
-      if (jbad) {
-        (void)w.fj(S.tn, b.y);
-        S.nfe++;
-        S.nje++;
-        S.nstlj = S.nst;
-        S.jcur = 1;
-      } else {
-        S.jcur = 0;
-      }
-      const bool ok = w.build_and_factor(S.gamma);
-      S.nlu++;
-      S.crate = 1.0;
-      S.gammap = S.gamma;
-      S.gamrat = 1.0;
-      S.nstlp = S.nst;
-      if (!ok) return 1;
-    }
-    b.acor = 0.0;
-    double delp = 0.0;
-    int mm = 0;
-    int failed = 0;
-    for (;;) {
-      const double rhs = act ? S.gamma * b.ftemp - (S.rl1 * b.zn[1] + b.acor) : 0.0;
-      double x = w.solve(rhs);
-      S.nni++;
-      if (S.gamrat != 1.0) x *= 2.0 / (1.0 + S.gamrat);
-      if (!act) x = 0.0;
-      const double del = wrms_lane(x, b.ewt, n);
-      b.acor += x;
-      b.y = b.zn[0] + b.acor;
-      if (mm > 0) S.crate = fmax(CRDOWN * S.crate, del / delp);
-      const double dcon = del * fmin(1.0, S.crate) / S.tq[4];
-      if (dcon <= 1.0) {
-        if (S.nneg) {
-          const bool neg = act && w.lane >= 1 && b.y < 0.0;
-          const double xn = neg ? b.y * b.ewt : 0.0;
-          const double s = wave_sum(xn * xn);
-          if (s > 0.0) {
-            if (sqrt(s / n) > NNEG_TOL) {
-              failed = 2;
-              break;
-            }
-            if (neg) {
-              b.y = 0.0;
-              b.acor = -b.zn[0];
-            }
-            S.acnrm = wrms_lane(b.acor, b.ewt, n);
-            S.jcur = 0;
-            return 0;
-          }
-        }
-        S.acnrm = (mm == 0) ? del : wrms_lane(b.acor, b.ewt, n);
-        S.jcur = 0;
-        return 0;
-      }
-      mm++;
-      if (mm == MAXCOR || (mm >= 2 && del > RDIV * delp)) {
-        failed = 1;
-        break;
-      }
-      delp = del;
-      b.ftemp = w.f(S.tn, b.y);
-      S.nfe++;
-    }
-    if (failed == 1 && !S.jcur) {
-      convfail = CF_BAD_J;
-      call_setup = 1;
-      continue;
-    }
-    return 1;
-  }
-}
-
-template <int N>
-__device__ __forceinline__ double bdf_initial_step(Bdf& b, BdfS& S, Wave<N>& w, double tout) {
-  const int n = w.n;
-  const bool act = w.lane < n;
-  const double t0 = S.tn;
-  const double tdist = fabs(tout - t0);
-  const double tround = UROUND * fmax(fabs(t0), fabs(tout));
-  const double hlb = 100.0 * tround;
-  double hub = 0.1 * tdist;
-  const double num = act ? fabs(b.zn[1]) : 0.0;
-  const double den = 0.1 * fabs(b.zn[0]) + S.atol;
-  const double hub_inv = wave_max(act ? num / (den > 0 ? den : 1e-300) : 0.0);
-  if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
-  double hg = sqrt(hlb * hub);
-  if (hub < hlb) return hg;
-  double hnew = hg;
-  for (int count = 1; count <= 4; ++count) {
-    const double y1 = b.zn[0] + hg * b.zn[1];
-    double f1 = w.f(t0 + hg, y1);
-    S.nfe++;
-    f1 = act ? (f1 - b.zn[1]) / hg : 0.0;
-    const double yddnrm = wrms_lane(f1, b.ewt, n);
-    hnew = (yddnrm * hub * hub > 2.0) ? sqrt(2.0 / yddnrm) : sqrt(hg * hub);
-    if (count == 4) break;
-    const double hrat = hnew / hg;
-    if (hrat > 0.5 && hrat < 2.0) break;
-    if (count >= 2 && hrat > 2.0) {
-      hnew = hg;
-      break;
-    }
-    hg = hnew;
-  }
-  double h0 = 0.5 * hnew;
-  if (h0 < hlb) h0 = hlb;
-  if (h0 > hub) h0 = hub;
-  return h0;
-}
-
-template <int N>
-__device__ __forceinline__ void bdf_start(Bdf& b, BdfS& S, Wave<N>& w, double t, double yl, double tout, double h0, double hmax) {
-  const bool act = w.lane < w.n;
-  S.tn = t;
-  b.zn[0] = act ? yl : 0.0;
-#pragma unroll
-  for (int j = 1; j <= QMAX; ++j) b.zn[j] = 0.0;
-  b.ewt = act ? 1.0 / (S.rtol * fabs(b.zn[0]) + S.atol) : 0.0;
-  b.zn[1] = w.f(t, b.zn[0]);
-  S.nfe++;
-  if (!act) b.zn[1] = 0.0;
-  double h = h0 > 0.0 ? h0 : bdf_initial_step(b, S, w, tout);
-  if (h > hmax) h = hmax;
-  if (h > tout - t) h = tout - t;
-  b.zn[1] *= h;
-  S.h = S.hscale = S.hprime = h;
-  S.q = S.qprime = 1;
-  S.L = 2;
-  S.qwait = S.L;
-  S.etamax = ETAMX1;
-  S.nst = 0;
-  S.nstlp = 0;
-  S.nstlj = 0;
-  S.jcur = 0;
-  S.crate = 1.0;
-  S.gammap = S.gamma = S.h;
-  S.gamrat = 1.0;
-  S.saved_tq5 = 0.0;
-#pragma unroll
-  for (int i = 0; i <= QMAX + 1; ++i) S.tau[i] = 0.0;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) S.tq[i] = 0.0;
-  S.hu = 0.0;
-}
-
-template <int N>
-__device__ __forceinline__ int bdf_step(Bdf& b, BdfS& S, Wave<N>& w, int& nst_global) {
-  const int n = w.n;
-  const bool act = w.lane < n;
-  const double saved_t = S.tn;
-  int ncf = 0, nef = 0, nflag = NF_FIRST;
-  double dsm;
-  if (S.nst > 0 && S.hprime != S.h) {
-    if (S.qprime != S.q) {
-      bdf_adjust_order(b, S, S.qprime - S.q);
-      S.q = S.qprime;
-      S.L = S.q + 1;
-      S.qwait = S.L;
-    }
-    bdf_rescale(b, S);
-  }
-  for (;;) {
-    bdf_predict(b, S);
-    bdf_set(b, S);
-    const int r = bdf_nls<N>(b, S, w, nflag);
-    if (r != 0) {
-      ncf++;
-      S.ncf_tot++;
-      S.etamax = 1.0;
-      bdf_restore(b, S, saved_t);
-      if (fabs(S.h) <= S.hmin * ONEPSM || ncf == MXNCF) return CKMI_RUN_CONVFAIL;
-      S.eta = fmax(ETACF, S.hmin / fabs(S.h));
-      nflag = NF_CONV_FAIL;
-      bdf_rescale(b, S);
-      continue;
-    }
-    dsm = S.acnrm * S.tq[2];
-    if (dsm <= 1.0) break;
-    nef++;
-    S.nef_tot++;
-    nflag = NF_ERR_FAIL;
-    bdf_restore(b, S, saved_t);
-    if (fabs(S.h) <= S.hmin * ONEPSM || nef == MXNEF) return CKMI_RUN_ERRTEST;
-    S.etamax = 1.0;
-    if (nef <= MXNEF1) {
-      S.eta = 1.0 / (pow(BIAS2 * dsm, 1.0 / S.L) + ADDON);
-      S.eta = fmax(ETAMIN, fmax(S.eta, S.hmin / fabs(S.h)));
-      if (nef >= SMALL_NEF) S.eta = fmin(S.eta, ETAMXF);
-      bdf_rescale(b, S);
-      continue;
-    }
-    if (S.q > 1) {
-      S.eta = fmax(ETAMIN, S.hmin / fabs(S.h));
-      bdf_adjust_order(b, S, -1);
-      S.L = S.q;
-      S.q--;
-      S.qwait = S.L;
-      bdf_rescale(b, S);
-      continue;
-    }
-    S.eta = fmax(ETAMIN, S.hmin / fabs(S.h));
-    S.h *= S.eta;
-    S.hscale = S.h;
-    S.qwait = LONG_WAIT;
-    const double fz = w.f(S.tn, b.zn[0]);
-    S.nfe++;
-    b.zn[1] = act ? S.h * fz : 0.0;
-  }
-  // complete the step
-  S.nst++;
-  nst_global++;
-  S.hu = S.h;
-#pragma unroll
-  for (int i = QMAX; i >= 2; --i)
-    if (i <= S.q) S.tau[i] = S.tau[i - 1];
-  if (S.q == 1 && S.nst > 1) S.tau[2] = S.tau[1];
-  S.tau[1] = S.h;
-#pragma unroll
-  for (int j = 0; j <= QMAX; ++j)
-    if (j <= S.q) b.zn[j] += S.l[j] * b.acor;
-  S.qwait--;
-  if (S.qwait == 1 && S.q != QMAX) {
-    b.zn[QMAX] = b.acor;
-    S.saved_tq5 = S.tq[5];
-  }
-  // prepare the next step
-  if (S.etamax == 1.0) {
-    if (S.qwait < 2) S.qwait = 2;
-    S.qprime = S.q;
-    S.hprime = S.h;
-    S.eta = 1.0;
-  } else {
-    const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / S.L) + ADDON);
-    if (S.qwait != 0) {
-      S.eta = etaq;
-      S.qprime = S.q;
-    } else {
-      S.qwait = 2;
-      double etaqm1 = 0.0, etaqp1 = 0.0;
-      if (S.q > 1) {
-        double znq = 0.0;
-#pragma unroll
-        for (int j = 0; j <= QMAX; ++j)
-          if (j == S.q) znq = b.zn[j];
-        const double ddn = wrms_lane(act ? znq : 0.0, b.ewt, n) * S.tq[1];
-        etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / S.q) + ADDON);
-      }
-      if (S.q != QMAX && S.saved_tq5 != 0.0) {
-        const double cquot = (S.tq[5] / S.saved_tq5) * pow(S.h / S.tau[2], (double)S.L);
-        const double tv = act ? b.acor - cquot * b.zn[QMAX] : 0.0;
-        const double dup = wrms_lane(tv, b.ewt, n) * S.tq[3];
-        etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (S.L + 1)) + ADDON);
-      }
-      const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
-      if (etam < THRESH) {
-        S.eta = 1.0;
-        S.qprime = S.q;
-      } else if (etam == etaq) {
-        S.eta = etaq;
-        S.qprime = S.q;
-      } else if (etam == etaqm1) {
-        S.eta = etaqm1;
-        S.qprime = S.q - 1;
-      } else {
-        S.eta = etaqp1;
-        S.qprime = S.q + 1;
-        b.zn[QMAX] = b.acor;
-      }
-    }
-    if (S.eta < THRESH) {
-      S.eta = 1.0;
-      S.hprime = S.h;
-    } else {
-      S.eta = fmin(S.eta, S.etamax);
-      S.eta /= fmax(1.0, fabs(S.h) * S.hmax_inv * S.eta);
-      S.hprime = S.h * S.eta;
-    }
-  }
-  S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-  return 0;
-}
-
 // ignition monitor (uniform scalars), mirrors oracle ign_* helpers
 struct Ign {
   int mode, comp, found, started, have_prev, have_next;
@@ -416,12 +103,12 @@ __device__ __forceinline__ double crit_time(const ckmi_reactor_cfg* c, double te
   return tend;
 }
 
-__device__ __forceinline__ void state_PV(const MechDev& M, const RunCtx& R, double t, double yl, int lane, double& P,
+__device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, double t, double yl, int lane, double& P,
                                          double& V) {
   const int KK = M.KK;
   const bool isp = lane >= 1 && lane <= KK;
   const double T = bcast(yl, 0);
-  const double Wb = 1.0 / wave_sum(isp ? yl * M.rwt[lane - 1] : 0.0);
+  const double Wb = 1.0 / wave_sum(isp ? yl * M.rwt()[lane - 1] : 0.0);
   double d;
   if (R.conp) {
     profile_eval(R.cfg, R.cfg->nprof, t, R.P0, P, d);
@@ -434,180 +121,718 @@ __device__ __forceinline__ void state_PV(const MechDev& M, const RunCtx& R, doub
   }
 }
 
-template <int N>
-__global__ __launch_bounds__(WAVE) void reactor_kernel(MechDev M, const ckmi_reactor_cfg* __restrict__ cfg, int nreact,
-                                                       const int* __restrict__ problem, const double* __restrict__ T0v,
-                                                       const double* __restrict__ P0v, const double* __restrict__ V0v,
-                                                       const double* __restrict__ Y0v, double* __restrict__ tau_o,
-                                                       double* __restrict__ T_o, double* __restrict__ P_o,
-                                                       double* __restrict__ V_o, double* __restrict__ Y_o,
-                                                       int* __restrict__ stats_o, int nsave,
-                                                       const double* __restrict__ t_save,
-                                                       double* __restrict__ y_save) {
-  extern __shared__ double lds[];
-  const int r = blockIdx.x;
-  if (r >= nreact) return;
-  const int lane = threadIdx.x;
-  const int KK = M.KK;
-  const int n = KK + 1;
-  const int ld = (n & 1) ? n : n + 1;
-  const int VL = (KK + WAVE - 1) / WAVE * WAVE;
-  Lds L;
-  L.J = lds;
-  L.A = L.J + ((n * ld + 1) & ~1);
-  L.C = L.A + ((n * ld + 1) & ~1);
-  L.gRT = L.C + VL;
-  L.hRT = L.gRT + VL;
-  L.wdot = L.hRT + VL;
-  L.dwdT = L.wdot + VL;
-  L.ek = L.dwdT + VL;
-  L.Mg = L.ek + VL;
+struct ReactorIO {
+  const int* problem;
+  const double *T0, *P0, *V0, *Y0;
+  double *tau, *T, *P, *V, *Y;
+  int* stats;
+  int nsave;
+  const double* t_save;
+  double* y_save;
+};
 
+// Integrator control state of one wave (wave-uniform scalars, kept in the wave's LDS slice).
+struct Ctl {
+  int r, first, nflag, convfail, call_setup, failed, mm, ncf, nef, rc, isave, icrit, ncrit, status, nst, stopped;
+  int is_count, max_steps;
+  double delp, saved_t, told, dsm, tc, tend, hmax, T0;
+  double st_h0, st_tout, st_h, is_hg, is_hub, is_hlb, is_t0;
+};
+
+// Per-wave LDS slice: 6 species vectors, third-body sums, integrator scalars, control state,
+// ignition monitor.
+__host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
+__host__ __device__ constexpr int slice_vec_bytes(int G) { return align16(8 * (6 * VL + (G > 0 ? G : 1))); }
+__host__ __device__ constexpr int slice_bytes(int G) {
+  return slice_vec_bytes(G) + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign));
+}
+template <int N>
+__host__ __device__ constexpr int jscratch_bytes() {
+  return align16(8 * N * LDJ) + 16;  // + lock
+}
+
+// integrator states; the ones marked (f) resume after the RHS requested by their predecessor
+enum {
+  ST_NEXT = 0,       // pull the next reactor
+  ST_START_F,        // (f) f(t, y0) for the Nordsieck history
+  ST_INITSTEP_F,     // (f) one probe of the initial step-size estimate
+  ST_START_FINISH,   // initial step chosen: set up the history
+  ST_IGN0_F,         // (f) dT/dt at t = 0 for the inflection-point monitor
+  ST_STEP_BEGIN,     // top of the time loop
+  ST_STEP_ATTEMPT,   // predict + coefficients, begin a Newton solve
+  ST_NLS_ATTEMPT,    // request f at the predictor
+  ST_NLS_F,          // (f) f at the predictor; decide the Newton-matrix setup
+  ST_NLS_J,          // (f) fresh Jacobian is in the shared scratch
+  ST_SETUP,          // M = I - gamma J, LU
+  ST_NEWTON_ITER,    // one Newton iteration
+  ST_NEWTON_F,       // (f) f at the Newton iterate
+  ST_NLS_FAIL,       // Newton failure: retry with a fresh J or fail the step
+  ST_STEP_CONVFAIL,  // step failed to converge: shrink h
+  ST_ERRTEST,        // local error test
+  ST_ERR_F,          // (f) f after repeated error-test failures at order 1
+  ST_STEP_COMPLETE,  // accept the step, choose the next h and q
+  ST_STEP_END,       // outputs, ignition monitor, stops, critical-time restarts
+  ST_FINISH,         // write the reactor's results
+  ST_EXIT
+};
+
+// Persistent reactor kernel: one workgroup of RWAVES waves per CU slot.  The workgroup stages
+// the mechanism image into LDS once; each wave then pulls reactor indices from an HBM work
+// counter until the batch is exhausted (dynamic balancing: step counts differ by 10x across a
+// T0 / phi / P sweep).  No workgroup barrier after staging, so waves run independently.
+//
+// The integrator (CVODE-style variable-order BDF with modified Newton, control flow identical
+// to oracle/ckoracle.c) is written as a wave-uniform state machine whose only RHS evaluation,
+// LU factorisation and triangular solve each appear ONCE in the loop: the LU factors of
+// M = I - gamma J then stay in VGPRs for the life of the wave without spilling.
+constexpr int RWAVES = 8;
+template <int N>
+__global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, const ckmi_reactor_cfg* __restrict__ cfg,
+                                                               int nreact, int* __restrict__ queue,
+                                                               double* __restrict__ jws, ReactorIO io) {
+  const int oJ = img.bytes;
+  const int olock = oJ + align16(8 * N * LDJ);
+  if (threadIdx.x == 0) *lds_at<int>(olock) = 0;
+  stage_image(0, img);
+  const MechView V = make_view(0, img);
+  const int wid = threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  const int ows = oJ + jscratch_bytes<N>() + wid * slice_bytes(img.G);
+  WaveLds L;
+  L.base = ows;
+  const int oS = ows + slice_vec_bytes(img.G);
+  BdfS& S = *lds_at<BdfS>(oS);
+  Ctl& c = *lds_at<Ctl>(oS + align16((int)sizeof(BdfS)));
+  Ign& g = *lds_at<Ign>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)));
+  double* Jg = jws + ((size_t)blockIdx.x * RWAVES + wid) * N * WAVE;
+  const int KK = V.KK;
+  const int n = KK + 1;
   const bool isp = lane >= 1 && lane <= KK;
   const bool act = lane < n;
-  const int prob = problem[r];
-  const double T0 = T0v[r], P0 = P0v[r];
-  double yl = 0.0;
-  if (lane == 0) yl = T0;
-  if (isp) yl = Y0v[(size_t)r * KK + lane - 1];
-  const double Wbar0 = 1.0 / wave_sum(isp ? yl * M.rwt[lane - 1] : 0.0);
-  const double rho0 = P0 * Wbar0 / (RU * T0);
   RunCtx R;
-  R.conp = (prob == 1);
-  R.energy = cfg->energy;
-  R.rho0 = rho0;
   R.cfg = cfg;
-  R.V0 = (!R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : V0v[r];
-  R.P0 = (R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : P0;
-
-  Wave<N> w(M, R, L, lane, n, ld);
-  __shared__ BdfS S;
-  __shared__ Ign g;
+  NewtonMatrix<N> M;
   Bdf b;
-  S.rtol = cfg->rtol;
-  S.atol = cfg->atol;
-  S.nneg = cfg->nneg;
-  S.ncf_tot = S.nef_tot = S.nlu = S.nfe = S.nje = S.nni = 0;
-  const double tend = cfg->t_end;
-  const double hmax = cfg->hmax > 0.0 ? cfg->hmax : tend / 100.0;
-  S.hmax_inv = 1.0 / hmax;
-  S.hmin = 0.0;
-  const int ncrit = n_crit(cfg, tend);
-  int icrit = 0;
-  bdf_start<N>(b, S, w, 0.0, yl, crit_time(cfg, tend, 0), cfg->h0, hmax);
+  double fe = 0.0, y_e = 0.0, t_e = 0.0;
+  bool with_j = false;
+#ifdef CKMI_PHASE_TIMERS
+  unsigned long long ph[PH_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long t_r0 = 0;
+#endif
+  int st = ST_NEXT;
 
-  g.mode = cfg->ign_mode;
-  g.comp = (g.mode == 4) ? 1 + cfg->ign_species : 0;
-  g.found = g.started = g.have_prev = g.have_next = 0;
-  g.thresh = 0.0;
-  g.best = -1e300;
-  g.tbest = g.tprev = g.vprev = g.tnext = g.vnext = g.tlast = g.vlast = 0.0;
-  g.tau = -1.0;
-  if (g.mode == 2) g.thresh = T0 + cfg->ign_val;
-  if (g.mode == 3) g.thresh = cfg->ign_val;
+  // request f at (t, y): sets the evaluation point and the state that consumes it
+#define REQUEST_F(T_, Y_, NEXT_) \
+  do {                           \
+    t_e = (T_);                  \
+    y_e = (Y_);                  \
+    with_j = false;              \
+    st = (NEXT_);                \
+    want = true;                 \
+  } while (0)
+  // bdf_start: history at (t, y), then the initial step size (oracle bdf_start)
+#define START_BEGIN(T_, Y_, TOUT_, H0_)                                 \
+  do {                                                                 \
+    S.tn = (T_);                                                       \
+    b.zn[0] = act ? (Y_) : 0.0;                                        \
+    _Pragma("unroll") for (int j_ = 1; j_ <= QMAX; ++j_) b.zn[j_] = 0.0; \
+    b.ewt = act ? 1.0 / (S.rtol * fabs(b.zn[0]) + S.atol) : 0.0;       \
+    c.st_tout = (TOUT_);                                               \
+    c.st_h0 = (H0_);                                                   \
+    REQUEST_F(S.tn, b.zn[0], ST_START_F);                              \
+  } while (0)
 
-  int isave = 0;
-  while (isave < nsave && t_save[isave] <= 0.0) {
-    if (act) y_save[((size_t)r * nsave + isave) * n + lane] = yl;
-    isave++;
-  }
-  if (g.mode == 1 || g.mode == 4) {
-    const double f0 = w.f(0.0, yl);
-    S.nfe++;
-    ign_peak_update(g, 0.0, g.mode == 1 ? bcast(f0, 0) : bcast(yl, g.comp));
-  }
-  int status = 0, nst = 0, stopped = 0;
-  const int max_steps = cfg->max_steps > 0 ? cfg->max_steps : 200000;
-  while (S.tn < tend * (1.0 - 1e-15)) {
-    const double tc = crit_time(cfg, tend, icrit);
-    if (S.tn + S.hprime > tc) {
-      const double hp = tc - S.tn;
-      S.eta = hp / S.h;
-      if (S.nst > 0) {
-        S.hprime = hp;
-      } else {
-        bdf_rescale(b, S);
-        S.hprime = S.h;
+  for (;;) {
+    bool want = false;
+    while (!want && st != ST_EXIT) {
+      switch (st) {
+        case ST_NEXT: {
+          int r = 0;
+          if (lane == 0) r = atomicAdd(queue, 1);
+          r = uni(bcast(r, 0));
+          if (r >= nreact) {
+            st = ST_EXIT;
+            break;
+          }
+          c.r = r;
+          const int prob = io.problem[r];
+          const double T0 = io.T0[r], P0 = io.P0[r];
+          double yl = 0.0;
+          if (lane == 0) yl = T0;
+          if (isp) yl = io.Y0[(size_t)r * KK + lane - 1];
+          const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
+          R.conp = (prob == 1);
+          R.energy = cfg->energy;
+          R.rho0 = P0 * Wbar0 / (RU * T0);
+          R.V0 = (!R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : io.V0[r];
+          R.P0 = (R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : P0;
+          c.T0 = T0;
+          S.rtol = cfg->rtol;
+          S.atol = cfg->atol;
+          S.nneg = cfg->nneg;
+          S.ncf_tot = S.nef_tot = S.nlu = S.nfe = S.nje = S.nni = 0;
+          c.tend = cfg->t_end;
+          c.hmax = cfg->hmax > 0.0 ? cfg->hmax : c.tend / 100.0;
+          S.hmax_inv = 1.0 / c.hmax;
+          S.hmin = 0.0;
+          c.ncrit = n_crit(cfg, c.tend);
+          c.icrit = 0;
+          c.first = 1;
+          c.max_steps = cfg->max_steps > 0 ? cfg->max_steps : 200000;
+#ifdef CKMI_PHASE_TIMERS
+#pragma unroll
+          for (int k = 0; k < PH_N; ++k) ph[k] = 0;
+          t_r0 = __builtin_amdgcn_s_memtime();
+#endif
+          START_BEGIN(0.0, yl, crit_time(cfg, c.tend, 0), cfg->h0);
+          break;
+        }
+        case ST_START_F: {
+          b.zn[1] = act ? fe : 0.0;
+          S.nfe++;
+          if (c.st_h0 > 0.0) {
+            c.st_h = c.st_h0;
+            st = ST_START_FINISH;
+            break;
+          }
+          // initial step estimate (oracle bdf_initial_step)
+          const double t0 = S.tn, tout = c.st_tout;
+          const double tdist = fabs(tout - t0);
+          const double tround = UROUND * fmax(fabs(t0), fabs(tout));
+          const double hlb = 100.0 * tround;
+          double hub = 0.1 * tdist;
+          const double num = act ? fabs(b.zn[1]) : 0.0;
+          const double den = 0.1 * fabs(b.zn[0]) + S.atol;
+          const double hub_inv = wave_max(act ? num / (den > 0 ? den : 1e-300) : 0.0);
+          if (hub * hub_inv > 1.0) hub = 1.0 / hub_inv;
+          const double hg = sqrt(hlb * hub);
+          if (hub < hlb) {
+            c.st_h = hg;
+            st = ST_START_FINISH;
+            break;
+          }
+          c.is_t0 = t0;
+          c.is_hg = hg;
+          c.is_hub = hub;
+          c.is_hlb = hlb;
+          c.is_count = 1;
+          REQUEST_F(t0 + hg, b.zn[0] + hg * b.zn[1], ST_INITSTEP_F);
+          break;
+        }
+        case ST_INITSTEP_F: {
+          S.nfe++;
+          const double hg = c.is_hg, hub = c.is_hub;
+          const double f1 = act ? (fe - b.zn[1]) / hg : 0.0;
+          const double yddnrm = wrms_lane(f1, b.ewt, n);
+          double hnew = (yddnrm * hub * hub > 2.0) ? sqrt(2.0 / yddnrm) : sqrt(hg * hub);
+          bool done = c.is_count == 4;
+          if (!done) {
+            const double hrat = hnew / hg;
+            if (hrat > 0.5 && hrat < 2.0) {
+              done = true;
+            } else if (c.is_count >= 2 && hrat > 2.0) {
+              hnew = hg;
+              done = true;
+            }
+          }
+          if (!done) {
+            c.is_hg = hnew;
+            c.is_count++;
+            REQUEST_F(c.is_t0 + hnew, b.zn[0] + hnew * b.zn[1], ST_INITSTEP_F);
+            break;
+          }
+          double h0 = 0.5 * hnew;
+          if (h0 < c.is_hlb) h0 = c.is_hlb;
+          if (h0 > hub) h0 = hub;
+          c.st_h = h0;
+          st = ST_START_FINISH;
+          break;
+        }
+        case ST_START_FINISH: {
+          double h = c.st_h;
+          if (h > c.hmax) h = c.hmax;
+          if (h > c.st_tout - S.tn) h = c.st_tout - S.tn;
+          b.zn[1] *= h;
+          S.h = S.hscale = S.hprime = h;
+          S.q = S.qprime = 1;
+          S.L = 2;
+          S.qwait = S.L;
+          S.etamax = ETAMX1;
+          S.nst = 0;
+          S.nstlp = 0;
+          S.nstlj = 0;
+          S.jcur = 0;
+          S.crate = 1.0;
+          S.gammap = S.gamma = S.h;
+          S.gamrat = 1.0;
+          S.saved_tq5 = 0.0;
+#pragma unroll
+          for (int i = 0; i <= QMAX + 1; ++i) S.tau[i] = 0.0;
+#pragma unroll
+          for (int i = 0; i < 6; ++i) S.tq[i] = 0.0;
+          S.hu = 0.0;
+          st = ST_STEP_BEGIN;
+          if (c.first) {
+            c.first = 0;
+            g.mode = cfg->ign_mode;
+            g.comp = (g.mode == 4) ? 1 + cfg->ign_species : 0;
+            g.found = g.started = g.have_prev = g.have_next = 0;
+            g.thresh = 0.0;
+            g.best = -1e300;
+            g.tbest = g.tprev = g.vprev = g.tnext = g.vnext = g.tlast = g.vlast = 0.0;
+            g.tau = -1.0;
+            if (g.mode == 2) g.thresh = c.T0 + cfg->ign_val;
+            if (g.mode == 3) g.thresh = cfg->ign_val;
+            c.isave = 0;
+            while (c.isave < io.nsave && io.t_save[c.isave] <= 0.0) {
+              if (act) io.y_save[((size_t)c.r * io.nsave + c.isave) * n + lane] = b.zn[0];
+              c.isave++;
+            }
+            c.status = 0;
+            c.nst = 0;
+            c.stopped = 0;
+            if (g.mode == 1 || g.mode == 4) REQUEST_F(0.0, b.zn[0], ST_IGN0_F);
+          }
+          break;
+        }
+        case ST_IGN0_F: {
+          S.nfe++;
+          ign_peak_update(g, 0.0, g.mode == 1 ? bcast(fe, 0) : bcast(b.zn[0], g.comp));
+          st = ST_STEP_BEGIN;
+          break;
+        }
+        case ST_STEP_BEGIN: {
+          if (!(S.tn < c.tend * (1.0 - 1e-15))) {
+            st = ST_FINISH;
+            break;
+          }
+          c.tc = crit_time(cfg, c.tend, c.icrit);
+          if (S.tn + S.hprime > c.tc) {
+            const double hp = c.tc - S.tn;
+            S.eta = hp / S.h;
+            if (S.nst > 0) {
+              S.hprime = hp;
+            } else {
+              bdf_rescale(b, S);
+              S.hprime = S.h;
+            }
+          }
+          b.ewt = act ? 1.0 / (S.rtol * fabs(b.zn[0]) + S.atol) : 0.0;
+          c.told = S.tn;
+          c.saved_t = S.tn;
+          c.ncf = c.nef = 0;
+          c.nflag = NF_FIRST;
+          if (S.nst > 0 && S.hprime != S.h) {
+            if (S.qprime != S.q) {
+              bdf_adjust_order(b, S, S.qprime - S.q);
+              S.q = S.qprime;
+              S.L = S.q + 1;
+              S.qwait = S.L;
+            }
+            bdf_rescale(b, S);
+          }
+          st = ST_STEP_ATTEMPT;
+          break;
+        }
+        case ST_STEP_ATTEMPT: {
+          bdf_predict(b, S);
+          bdf_set(b, S);
+          c.convfail = (c.nflag == NF_FIRST || c.nflag == NF_ERR_FAIL) ? CF_NONE : CF_OTHER;
+          c.call_setup = (c.nflag != NF_FIRST) || S.nst == 0 || S.nst >= S.nstlp + MSBP || fabs(S.gamrat - 1.0) > DGMAX;
+          st = ST_NLS_ATTEMPT;
+          break;
+        }
+        case ST_NLS_ATTEMPT: {
+          b.y = b.zn[0];
+          REQUEST_F(S.tn, b.y, ST_NLS_F);
+          break;
+        }
+        case ST_NLS_F: {
+          b.ftemp = fe;
+          S.nfe++;
+          if (!c.call_setup) {
+            b.acor = 0.0;
+            c.delp = 0.0;
+            c.mm = 0;
+            st = ST_NEWTON_ITER;
+            break;
+          }
+          const double dgamma = fabs(S.gamma / S.gammap - 1.0);
+          const int jbad = S.nst == 0 || S.nst >= S.nstlj + MSBJ || (c.convfail == CF_BAD_J && dgamma < DGMAX) ||
+                           c.convfail == CF_OTHER;
+          if (jbad) {
+            // exclusive use of the workgroup's J scratch until it is copied out
+            for (;;) {
+              int got = 0;
+              if (lane == 0) got = atomicCAS(lds_at<int>(olock), 0, 1) == 0;
+              if (uni(bcast(got, 0))) break;
+              __builtin_amdgcn_s_sleep(4);
+            }
+            wave_lds_sync();
+            REQUEST_F(S.tn, b.y, ST_NLS_J);
+            with_j = true;
+          } else {
+            S.jcur = 0;
+            st = ST_SETUP;
+          }
+          break;
+        }
+        case ST_NLS_J: {
+          {
+            const double* Jsh = lds_at<const double>(oJ);
+#pragma unroll 2
+            for (int j = 0; j < N; ++j) Jg[j * WAVE + lane] = Jsh[j * LDJ + lane];
+          }
+          wave_lds_sync();
+          if (lane == 0) atomicExch(lds_at<int>(olock), 0);
+          S.nfe++;
+          S.nje++;
+          S.nstlj = S.nst;
+          S.jcur = 1;
+          st = ST_SETUP;
+          break;
+        }
+        case ST_SETUP: {
+#ifdef CKMI_PHASE_TIMERS
+          const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+          // each lane reads back only the J entries it wrote itself (same-address order)
+          M.build(Jg, WAVE, S.gamma, lane, n);
+          const bool ok = M.factor(lane, n);
+#ifdef CKMI_PHASE_TIMERS
+          ph[PH_LU] += __builtin_amdgcn_s_memtime() - t0;
+#endif
+          S.nlu++;
+          S.crate = 1.0;
+          S.gammap = S.gamma;
+          S.gamrat = 1.0;
+          S.nstlp = S.nst;
+          if (!ok) {
+            st = ST_STEP_CONVFAIL;
+            break;
+          }
+          b.acor = 0.0;
+          c.delp = 0.0;
+          c.mm = 0;
+          st = ST_NEWTON_ITER;
+          break;
+        }
+        case ST_NEWTON_ITER: {
+          const double rhs = act ? S.gamma * b.ftemp - (S.rl1 * b.zn[1] + b.acor) : 0.0;
+#ifdef CKMI_PHASE_TIMERS
+          const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+          double x = M.solve(rhs, lane, n);
+#ifdef CKMI_PHASE_TIMERS
+          ph[PH_SOLVE] += __builtin_amdgcn_s_memtime() - t0;
+#endif
+          S.nni++;
+          if (S.gamrat != 1.0) x *= 2.0 / (1.0 + S.gamrat);
+          if (!act) x = 0.0;
+          const double del = wrms_lane(x, b.ewt, n);
+          b.acor += x;
+          b.y = b.zn[0] + b.acor;
+          if (c.mm > 0) S.crate = fmax(CRDOWN * S.crate, del / c.delp);
+          const double dcon = del * fmin(1.0, S.crate) / S.tq[4];
+          if (dcon <= 1.0) {
+            bool negfail = false, negfix = false;
+            if (S.nneg) {
+              const bool neg = act && lane >= 1 && b.y < 0.0;
+              const double xn = neg ? b.y * b.ewt : 0.0;
+              const double ss = wave_sum(xn * xn);
+              if (ss > 0.0) {
+                if (sqrt(ss / n) > NNEG_TOL) {
+                  negfail = true;
+                } else {
+                  negfix = true;
+                  if (neg) {
+                    b.y = 0.0;
+                    b.acor = -b.zn[0];
+                  }
+                }
+              }
+            }
+            if (negfail) {
+              c.failed = 2;
+              st = ST_NLS_FAIL;
+              break;
+            }
+            S.acnrm = (c.mm == 0 && !negfix) ? del : wrms_lane(b.acor, b.ewt, n);
+            S.jcur = 0;
+            st = ST_ERRTEST;
+            break;
+          }
+          c.mm++;
+          if (c.mm == MAXCOR || (c.mm >= 2 && del > RDIV * c.delp)) {
+            c.failed = 1;
+            st = ST_NLS_FAIL;
+            break;
+          }
+          c.delp = del;
+          REQUEST_F(S.tn, b.y, ST_NEWTON_F);
+          break;
+        }
+        case ST_NEWTON_F: {
+          b.ftemp = fe;
+          S.nfe++;
+          st = ST_NEWTON_ITER;
+          break;
+        }
+        case ST_NLS_FAIL: {
+          if (c.failed == 1 && !S.jcur) {
+            c.convfail = CF_BAD_J;
+            c.call_setup = 1;
+            st = ST_NLS_ATTEMPT;
+          } else {
+            st = ST_STEP_CONVFAIL;
+          }
+          break;
+        }
+        case ST_STEP_CONVFAIL: {
+          c.ncf++;
+          S.ncf_tot++;
+          S.etamax = 1.0;
+          bdf_restore(b, S, c.saved_t);
+          if (fabs(S.h) <= S.hmin * ONEPSM || c.ncf == MXNCF) {
+            c.rc = CKMI_RUN_CONVFAIL;
+            st = ST_STEP_END;
+            break;
+          }
+          S.eta = fmax(ETACF, S.hmin / fabs(S.h));
+          c.nflag = NF_CONV_FAIL;
+          bdf_rescale(b, S);
+          st = ST_STEP_ATTEMPT;
+          break;
+        }
+        case ST_ERRTEST: {
+          c.dsm = S.acnrm * S.tq[2];
+          if (c.dsm <= 1.0) {
+            st = ST_STEP_COMPLETE;
+            break;
+          }
+          c.nef++;
+          S.nef_tot++;
+          c.nflag = NF_ERR_FAIL;
+          bdf_restore(b, S, c.saved_t);
+          if (fabs(S.h) <= S.hmin * ONEPSM || c.nef == MXNEF) {
+            c.rc = CKMI_RUN_ERRTEST;
+            st = ST_STEP_END;
+            break;
+          }
+          S.etamax = 1.0;
+          st = ST_STEP_ATTEMPT;
+          if (c.nef <= MXNEF1) {
+            S.eta = 1.0 / (pow(BIAS2 * c.dsm, 1.0 / S.L) + ADDON);
+            S.eta = fmax(ETAMIN, fmax(S.eta, S.hmin / fabs(S.h)));
+            if (c.nef >= SMALL_NEF) S.eta = fmin(S.eta, ETAMXF);
+            bdf_rescale(b, S);
+            break;
+          }
+          if (S.q > 1) {
+            S.eta = fmax(ETAMIN, S.hmin / fabs(S.h));
+            bdf_adjust_order(b, S, -1);
+            S.L = S.q;
+            S.q--;
+            S.qwait = S.L;
+            bdf_rescale(b, S);
+            break;
+          }
+          S.eta = fmax(ETAMIN, S.hmin / fabs(S.h));
+          S.h *= S.eta;
+          S.hscale = S.h;
+          S.qwait = LONG_WAIT;
+          REQUEST_F(S.tn, b.zn[0], ST_ERR_F);
+          break;
+        }
+        case ST_ERR_F: {
+          S.nfe++;
+          b.zn[1] = act ? S.h * fe : 0.0;
+          st = ST_STEP_ATTEMPT;
+          break;
+        }
+        case ST_STEP_COMPLETE: {
+          const double dsm = c.dsm;
+          S.nst++;
+          c.nst++;
+          S.hu = S.h;
+#pragma unroll
+          for (int i = QMAX; i >= 2; --i)
+            if (i <= S.q) S.tau[i] = S.tau[i - 1];
+          if (S.q == 1 && S.nst > 1) S.tau[2] = S.tau[1];
+          S.tau[1] = S.h;
+#pragma unroll
+          for (int j = 0; j <= QMAX; ++j)
+            if (j <= S.q) b.zn[j] += S.l[j] * b.acor;
+          S.qwait--;
+          if (S.qwait == 1 && S.q != QMAX) {
+            b.zn[QMAX] = b.acor;
+            S.saved_tq5 = S.tq[5];
+          }
+          if (S.etamax == 1.0) {
+            if (S.qwait < 2) S.qwait = 2;
+            S.qprime = S.q;
+            S.hprime = S.h;
+            S.eta = 1.0;
+          } else {
+            const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / S.L) + ADDON);
+            if (S.qwait != 0) {
+              S.eta = etaq;
+              S.qprime = S.q;
+            } else {
+              S.qwait = 2;
+              double etaqm1 = 0.0, etaqp1 = 0.0;
+              if (S.q > 1) {
+                double znq = 0.0;
+#pragma unroll
+                for (int j = 0; j <= QMAX; ++j)
+                  if (j == S.q) znq = b.zn[j];
+                const double ddn = wrms_lane(act ? znq : 0.0, b.ewt, n) * S.tq[1];
+                etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / S.q) + ADDON);
+              }
+              if (S.q != QMAX && S.saved_tq5 != 0.0) {
+                const double cquot = (S.tq[5] / S.saved_tq5) * pow(S.h / S.tau[2], (double)S.L);
+                const double tv = act ? b.acor - cquot * b.zn[QMAX] : 0.0;
+                const double dup = wrms_lane(tv, b.ewt, n) * S.tq[3];
+                etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (S.L + 1)) + ADDON);
+              }
+              const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
+              if (etam < THRESH) {
+                S.eta = 1.0;
+                S.qprime = S.q;
+              } else if (etam == etaq) {
+                S.eta = etaq;
+                S.qprime = S.q;
+              } else if (etam == etaqm1) {
+                S.eta = etaqm1;
+                S.qprime = S.q - 1;
+              } else {
+                S.eta = etaqp1;
+                S.qprime = S.q + 1;
+                b.zn[QMAX] = b.acor;
+              }
+            }
+            if (S.eta < THRESH) {
+              S.eta = 1.0;
+              S.hprime = S.h;
+            } else {
+              S.eta = fmin(S.eta, S.etamax);
+              S.eta /= fmax(1.0, fabs(S.h) * S.hmax_inv * S.eta);
+              S.hprime = S.h * S.eta;
+            }
+          }
+          S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+          c.rc = 0;
+          st = ST_STEP_END;
+          break;
+        }
+        case ST_STEP_END: {
+          if (c.rc != 0) {
+            c.status = c.rc;
+            st = ST_FINISH;
+            break;
+          }
+          const double tn = S.tn;
+          while (c.isave < io.nsave && io.t_save[c.isave] <= tn) {
+            const double ys = dky0_lane(b, S, io.t_save[c.isave]);
+            if (act) io.y_save[((size_t)c.r * io.nsave + c.isave) * n + lane] = ys;
+            c.isave++;
+          }
+          if (g.mode == 1) {
+            ign_peak_update(g, tn, bcast(b.zn[1], 0) / S.h);
+          } else if (g.mode == 4) {
+            ign_peak_update(g, tn, bcast(b.zn[0], g.comp));
+          } else if ((g.mode == 2 || g.mode == 3) && !g.found && bcast(b.zn[0], 0) >= g.thresh) {
+            double lo = c.told, hi = tn;
+            for (int it = 0; it < 60; ++it) {
+              const double mid = 0.5 * (lo + hi);
+              if (bcast(dky0_lane(b, S, mid), 0) >= g.thresh) hi = mid;
+              else lo = mid;
+            }
+            g.found = 1;
+            g.tau = hi;
+          }
+          st = ST_STEP_BEGIN;
+          if (cfg->ign_stop) {
+            if ((g.mode == 2 || g.mode == 3) && g.found) {
+              c.stopped = 1;
+              st = ST_FINISH;
+              break;
+            }
+            if (g.mode == 1 && g.have_next && g.vlast < 0.1 * g.best && bcast(b.zn[0], 0) > c.T0 + 200.0) {
+              c.stopped = 1;
+              st = ST_FINISH;
+              break;
+            }
+          }
+          if (c.nst >= c.max_steps) {
+            c.status = CKMI_RUN_MAXSTEPS;
+            st = ST_FINISH;
+            break;
+          }
+          if (tn >= c.tc * (1.0 - 1e-15) && c.icrit < c.ncrit - 1) {
+            c.icrit++;
+            START_BEGIN(tn, b.zn[0], crit_time(cfg, c.tend, c.icrit), 0.0);
+          }
+          break;
+        }
+        case ST_FINISH: {
+          double yf;
+          double tf = c.tend;
+          if (c.stopped || c.status) {
+            tf = S.tn;
+            yf = b.zn[0];
+          } else {
+            yf = dky0_lane(b, S, c.tend);
+          }
+          if (g.mode == 1 || g.mode == 4) g.tau = ign_peak_time(g);
+          double Pf, Vf;
+          state_PV(V, R, tf, yf, lane, Pf, Vf);
+          const int r = c.r;
+          if (lane == 0) {
+            io.tau[r] = g.tau;
+            io.T[r] = yf;
+            io.P[r] = Pf;
+            io.V[r] = Vf;
+            int* sto = io.stats + (size_t)r * CKMI_NSTAT;
+            sto[CKMI_STAT_NST] = c.nst;
+            sto[CKMI_STAT_NFE] = S.nfe;
+            sto[CKMI_STAT_NJE] = S.nje;
+            sto[CKMI_STAT_NLU] = S.nlu;
+            sto[CKMI_STAT_NCF] = S.ncf_tot;
+            sto[CKMI_STAT_NEF] = S.nef_tot;
+            sto[CKMI_STAT_STATUS] = c.status;
+            sto[CKMI_STAT_NNI] = S.nni;
+          }
+          if (isp) io.Y[(size_t)r * KK + lane - 1] = yf;
+#ifdef CKMI_PHASE_TIMERS
+          ph[PH_TOTAL] = __builtin_amdgcn_s_memtime() - t_r0;
+          if (g_phase_buf && lane < PH_N) {
+            unsigned long long v = 0;
+#pragma unroll
+            for (int k = 0; k < PH_N; ++k) v = (lane == k) ? ph[k] : v;
+            g_phase_buf[(size_t)r * PH_N + lane] = v;
+          }
+#endif
+          st = ST_NEXT;
+          break;
+        }
+        default:
+          st = ST_EXIT;
+          break;
       }
     }
-    b.ewt = act ? 1.0 / (S.rtol * fabs(b.zn[0]) + S.atol) : 0.0;
-    const double told = S.tn;
-    const int rc = bdf_step<N>(b, S, w, nst);
-    if (rc != 0) {
-      status = rc;
-      break;
-    }
-    const double tn = S.tn;
-    while (isave < nsave && t_save[isave] <= tn) {
-      const double ys = dky0_lane(b, S, t_save[isave]);
-      if (act) y_save[((size_t)r * nsave + isave) * n + lane] = ys;
-      isave++;
-    }
-    if (g.mode == 1) {
-      ign_peak_update(g, tn, bcast(b.zn[1], 0) / S.h);
-    } else if (g.mode == 4) {
-      ign_peak_update(g, tn, bcast(b.zn[0], g.comp));
-    } else if ((g.mode == 2 || g.mode == 3) && !g.found && bcast(b.zn[0], 0) >= g.thresh) {
-      double lo = told, hi = tn;
-      for (int it = 0; it < 60; ++it) {
-        const double mid = 0.5 * (lo + hi);
-        if (bcast(dky0_lane(b, S, mid), 0) >= g.thresh) hi = mid;
-        else lo = mid;
-      }
-      g.found = 1;
-      g.tau = hi;
-    }
-    if (cfg->ign_stop) {
-      if ((g.mode == 2 || g.mode == 3) && g.found) {
-        stopped = 1;
-        break;
-      }
-      if (g.mode == 1 && g.have_next && g.vlast < 0.1 * g.best && bcast(b.zn[0], 0) > T0 + 200.0) {
-        stopped = 1;
-        break;
-      }
-    }
-    if (nst >= max_steps) {
-      status = CKMI_RUN_MAXSTEPS;
-      break;
-    }
-    if (tn >= tc * (1.0 - 1e-15) && icrit < ncrit - 1) {
-      const double yc = b.zn[0];
-      icrit++;
-      const int nlu = S.nlu, ncf = S.ncf_tot, nef = S.nef_tot;
-      bdf_start<N>(b, S, w, tn, yc, crit_time(cfg, tend, icrit), 0.0, hmax);
-      S.nlu = nlu;
-      S.ncf_tot = ncf;
-      S.nef_tot = nef;
-    }
+    if (st == ST_EXIT) break;
+    // the single RHS (+ Jacobian) evaluation site of the integrator
+#ifdef CKMI_PHASE_TIMERS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+    fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j);
+#ifdef CKMI_PHASE_TIMERS
+    ph[with_j ? PH_JAC : PH_RHS] += __builtin_amdgcn_s_memtime() - t0;
+#endif
   }
-  double yf;
-  double tf = tend;
-  if (stopped || status) {
-    tf = S.tn;
-    yf = b.zn[0];
-  } else {
-    yf = dky0_lane(b, S, tend);
-  }
-  if (g.mode == 1 || g.mode == 4) g.tau = ign_peak_time(g);
-  double Pf, Vf;
-  state_PV(M, R, tf, yf, lane, Pf, Vf);
-  if (lane == 0) {
-    tau_o[r] = g.tau;
-    T_o[r] = yf;
-    P_o[r] = Pf;
-    V_o[r] = Vf;
-    int* st = stats_o + (size_t)r * CKMI_NSTAT;
-    st[CKMI_STAT_NST] = nst;
-    st[CKMI_STAT_NFE] = S.nfe;
-    st[CKMI_STAT_NJE] = S.nje;
-    st[CKMI_STAT_NLU] = S.nlu;
-    st[CKMI_STAT_NCF] = S.ncf_tot;
-    st[CKMI_STAT_NEF] = S.nef_tot;
-    st[CKMI_STAT_STATUS] = status;
-    st[CKMI_STAT_NNI] = S.nni;
-  }
-  if (isp) Y_o[(size_t)r * KK + lane - 1] = yf;
+#undef REQUEST_F
+#undef START_BEGIN
 }
 
 // ---------------------------------------------------------------- ROP kernels
@@ -717,6 +942,7 @@ struct ckmi_mech {
   int device;
   int KK, II, IIpad, G;
   MechDev d;
+  MechImage img;  // compact LDS image (device copy in img.blob)
   std::vector<void*> allocs;
   // host copies of the forward Arrhenius (original order) for get/set
   std::vector<double> lnA_orig, b_orig, E_orig;
@@ -737,12 +963,136 @@ int upload(ckmi_mech* m, const std::vector<T>& v, const T** out) {
   return CKMI_OK;
 }
 
-size_t reactor_lds_bytes(int KK, int G) {
-  const int n = KK + 1;
-  const int ld = (n & 1) ? n : n + 1;
-  const int VL = (KK + WAVE - 1) / WAVE * WAVE;
-  return sizeof(double) * (size_t)(2 * ((n * ld + 1) & ~1) + 6 * VL + std::max(G, 1));
+// Pack the compact mechanism image (ckmi_image.hpp) from the device-slot tables.
+int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& slots, const std::vector<int>& flags,
+                const std::vector<int>& nrp, const std::vector<int4>& rsp, const std::vector<int4>& psp,
+                const std::vector<double>& rnu, const std::vector<double>& pnu, const std::vector<double>& lnA,
+                const std::vector<double>& beta, const std::vector<double>& Ea, const std::vector<double>& lnA0,
+                const std::vector<double>& beta0, const std::vector<double>& Ea0, const std::vector<double>& fp,
+                const std::vector<double>& rlnA, const std::vector<double>& rbeta, const std::vector<double>& rEa,
+                const std::vector<int>& tb, const std::vector<int>& gptr, const std::vector<int>& gsp,
+                const std::vector<double>& geff, const std::vector<double>& wt, const std::vector<double>& rwt) {
+  const int KK = m->KK, IIp = m->IIpad, G = m->G;
+  const int KKp = (KK + WAVE - 1) / WAVE * WAVE;
+  if (KK > 255) return fail(CKMI_ERR_UNSUPPORTED, "more than 255 species not supported by the mechanism image");
+  std::vector<uint32_t> urs(IIp, 0), ups(IIp, 0), unu(IIp, 0), uinfo(IIp, 0);
+  std::vector<double> aux;
+  int naux = 0;
+  for (int s = 0; s < IIp; ++s) {
+    const int nr = nrp[s] & 0xff, np = nrp[s] >> 8;
+    uint32_t a = 0, b = 0, nu = 0;
+    const int* r4 = &rsp[s].x;
+    const int* p4 = &psp[s].x;
+    for (int u = 0; u < nr; ++u) {
+      const int c = (int)rnu[u * IIp + s];
+      if (c > 15) return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficient > 15");
+      a |= (uint32_t)r4[u] << (8 * u);
+      nu |= (uint32_t)c << (4 * u);
+    }
+    for (int u = 0; u < np; ++u) {
+      const int c = (int)pnu[u * IIp + s];
+      if (c > 15) return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficient > 15");
+      b |= (uint32_t)p4[u] << (8 * u);
+      nu |= (uint32_t)c << (16 + 4 * u);
+    }
+    urs[s] = a;
+    ups[s] = b;
+    unu[s] = nu;
+    const int fl = flags[s];
+    const int type = fl & 3;
+    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)nr << 7) | ((uint32_t)np << 10);
+    if (slots[s] >= 0 && (type == 2 || (fl & 8))) {
+      double rec[AUXW] = {lnA0[s], beta0[s], Ea0[s], fp[0 * IIp + s], fp[1 * IIp + s], fp[2 * IIp + s],
+                          fp[3 * IIp + s], fp[4 * IIp + s], rlnA[s], rbeta[s], rEa[s], 0.0};
+      aux.insert(aux.end(), rec, rec + AUXW);
+      inf |= (uint32_t)naux << 16;
+      ++naux;
+    }
+    uinfo[s] = inf;
+  }
+  if (naux == 0) aux.assign(AUXW, 0.0), naux = 1;
+  std::vector<double> th(15 * KKp, 0.0), wtp(KKp, 0.0), rwtp(KKp, 0.0);
+  for (int k = 0; k < KK; ++k) {
+    th[0 * KKp + k] = d->thermo[17 * k + 1];
+    for (int c = 0; c < 7; ++c) {
+      th[(1 + c) * KKp + k] = d->thermo[17 * k + 3 + c];
+      th[(8 + c) * KKp + k] = d->thermo[17 * k + 10 + c];
+    }
+    wtp[k] = wt[k];
+    rwtp[k] = rwt[k];
+  }
+  std::vector<char> blob;
+  auto put = [&](const void* p, size_t bytes) -> int {
+    const int off = (int)blob.size();
+    blob.insert(blob.end(), (const char*)p, (const char*)p + bytes);
+    blob.resize(align16((int)blob.size()), 0);
+    return off;
+  };
+  MechImage& I = m->img;
+  I.KK = KK;
+  I.KKp = KKp;
+  I.II = m->II;
+  I.IIp = IIp;
+  I.G = G;
+  I.naux = naux;
+  I.o_th = put(th.data(), th.size() * 8);
+  I.o_wt = put(wtp.data(), KKp * 8);
+  I.o_rwt = put(rwtp.data(), KKp * 8);
+  I.o_lnA = put(lnA.data(), IIp * 8);
+  I.o_beta = put(beta.data(), IIp * 8);
+  I.o_Ea = put(Ea.data(), IIp * 8);
+  I.o_rsp = put(urs.data(), IIp * 4);
+  I.o_psp = put(ups.data(), IIp * 4);
+  I.o_nu = put(unu.data(), IIp * 4);
+  I.o_info = put(uinfo.data(), IIp * 4);
+  I.o_tb = put(tb.data(), IIp * 4);
+  I.o_aux = put(aux.data(), aux.size() * 8);
+  I.o_gptr = put(gptr.data(), gptr.size() * 4);
+  const int zero = 0;
+  const double dzero = 0.0;
+  I.o_gsp = gsp.empty() ? put(&zero, 4) : put(gsp.data(), gsp.size() * 4);
+  I.o_geff = geff.empty() ? put(&dzero, 8) : put(geff.data(), geff.size() * 8);
+  I.bytes = (int)blob.size();
+  void* p = nullptr;
+  HIP_CHECK(hipMalloc(&p, blob.size()));
+  m->allocs.push_back(p);
+  HIP_CHECK(hipMemcpy(p, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  I.blob = (const uint4*)p;
+  return CKMI_OK;
 }
+
+template <int N>
+size_t reactor_lds_bytes(const ckmi_mech* m) {
+  return (size_t)m->img.bytes + jscratch_bytes<N>() + (size_t)RWAVES * slice_bytes(m->G);
+}
+// Grid = (CUs x resident workgroups per CU), capped by the batch; J workspace = one
+// column-major N x 64 matrix per wave slot, allocated stream-ordered (~55 MB for GRI-3.0).
+template <int N>
+int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t stream) {
+  const size_t lds = reactor_lds_bytes<N>(m);
+  static thread_local std::map<int, int> max_lds_set;
+  if (lds > 64 * 1024 && max_lds_set[m->device] < (int)lds) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)reactor_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    max_lds_set[m->device] = (int)lds;
+  }
+  int ncu = 0, per_cu = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reactor_kernel<N>, RWAVES * WAVE, lds));
+  if (per_cu < 1) return fail(CKMI_ERR_SIZE, "reactor kernel does not fit on a CU (LDS " + std::to_string(lds) + " B)");
+  const int want = (n + RWAVES - 1) / RWAVES;
+  const int grid = std::max(1, std::min(ncu * per_cu, want));
+  const size_t jbytes = (size_t)grid * RWAVES * N * WAVE * sizeof(double);
+  void* ws = nullptr;
+  HIP_CHECK(hipMallocAsync(&ws, jbytes + 256, stream));
+  int* queue = (int*)((char*)ws + jbytes);
+  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(int), stream));
+  hipLaunchKernelGGL(reactor_kernel<N>, dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, m->cfg_dev, n, queue,
+                     (double*)ws, io);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipFreeAsync(ws, stream));
+  return CKMI_OK;
+}
+
 size_t rop_lds_bytes(int KK, int G) {
   const int VL = (KK + WAVE - 1) / WAVE * WAVE;
   return sizeof(double) * (size_t)(3 * VL + std::max(G, 1));
@@ -753,6 +1103,14 @@ size_t rop_lds_bytes(int KK, int G) {
 extern "C" {
 
 const char* ckmi_last_error(void) { return g_err.c_str(); }
+
+#ifdef CKMI_PHASE_TIMERS
+// diagnostic build only: buf = device u64 [n][8] (rhs, jac, lu, solve, total cycles)
+int ckmi_debug_phase_buffer(void* buf) {
+  HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_phase_buf), &buf, sizeof(buf)));
+  return CKMI_OK;
+}
+#endif
 int ckmi_version(void) { return 1; }
 
 int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
@@ -923,6 +1281,8 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   rc |= upload(m, gptr, &D.gptr);
   rc |= upload(m, gsp, &D.gsp);
   rc |= upload(m, geff, &D.geff);
+  rc |= build_image(m, d, slots, flags, nrp, rsp, psp, rnu, pnu, lnA, beta, Ea, lnA0, beta0, Ea0, fp, rlnA, rbeta, rEa,
+                    tb, gptr, gsp, geff, wt, rwt);
   void* cp = nullptr;
   if (hipMalloc(&cp, sizeof(ckmi_reactor_cfg)) != hipSuccess) rc |= CKMI_ERR_HIP;
   else m->allocs.push_back(cp);
@@ -965,6 +1325,8 @@ int ckmi_set_afactor(ckmi_mech* m, int32_t irxn, double A) {
   m->lnA_orig[irxn] = lnA;
   const int s = m->slot_of[irxn];
   HIP_CHECK(hipMemcpy(const_cast<double*>(m->d.lnA) + s, &lnA, sizeof(double), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy((char*)m->img.blob + m->img.o_lnA + sizeof(double) * s, &lnA, sizeof(double),
+                      hipMemcpyHostToDevice));
   return CKMI_OK;
 }
 
@@ -1012,18 +1374,13 @@ int ckmi_reactor_run(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t n,
   if (nsave > 0 && (!t_save || !y_save)) return fail(CKMI_ERR_ARG, "t_save / y_save required when nsave > 0");
   if (n == 0) return CKMI_OK;
   HIP_CHECK(hipMemcpyAsync(m->cfg_dev, cfg, sizeof(ckmi_reactor_cfg), hipMemcpyHostToDevice, (hipStream_t)stream));
-  const size_t lds = reactor_lds_bytes(m->KK, m->G);
+  ReactorIO io{problem, T0, P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save};
   const int nvar = m->KK + 1;
-  if (nvar <= 32) {
-    hipLaunchKernelGGL(reactor_kernel<32>, dim3(n), dim3(WAVE), lds, (hipStream_t)stream, m->d, m->cfg_dev, n, problem, T0,
-                       P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save);
-  } else if (nvar <= 54) {
-    hipLaunchKernelGGL(reactor_kernel<54>, dim3(n), dim3(WAVE), lds, (hipStream_t)stream, m->d, m->cfg_dev, n, problem, T0,
-                       P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save);
-  } else {
-    hipLaunchKernelGGL(reactor_kernel<64>, dim3(n), dim3(WAVE), lds, (hipStream_t)stream, m->d, m->cfg_dev, n, problem, T0,
-                       P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save);
-  }
+  int rc;
+  if (nvar <= 32) rc = launch_reactors<32>(m, n, io, (hipStream_t)stream);
+  else if (nvar <= 54) rc = launch_reactors<54>(m, n, io, (hipStream_t)stream);
+  else rc = launch_reactors<64>(m, n, io, (hipStream_t)stream);
+  if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;
 }

@@ -68,15 +68,34 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 }
 __device__ __forceinline__ int bcast(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
+// Cross-lane reductions on the DPP path (quad_perm / row_half_mirror / row_mirror inside each
+// 16-lane row, then four readlanes across rows): no LDS round trips, unlike ds_bpermute-based
+// __shfl_xor.  Every lane of a row computes the same commutative pairings, so the result is
+// identical in all lanes and deterministic.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+constexpr int DPP_QUAD_1032 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_QUAD_2301 = 0x4E;  // quad_perm [2,3,0,1]
+constexpr int DPP_ROW_HALF_MIRROR = 0x141;
+constexpr int DPP_ROW_MIRROR = 0x140;
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, WAVE);
-  return uni(v);
+  v += dpp_mov<DPP_QUAD_1032>(v);
+  v += dpp_mov<DPP_QUAD_2301>(v);
+  v += dpp_mov<DPP_ROW_HALF_MIRROR>(v);
+  v += dpp_mov<DPP_ROW_MIRROR>(v);
+  return uni((bcast(v, 0) + bcast(v, 16)) + (bcast(v, 32) + bcast(v, 48)));
 }
 __device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, WAVE));
-  return uni(v);
+  v = fmax(v, dpp_mov<DPP_QUAD_1032>(v));
+  v = fmax(v, dpp_mov<DPP_QUAD_2301>(v));
+  v = fmax(v, dpp_mov<DPP_ROW_HALF_MIRROR>(v));
+  v = fmax(v, dpp_mov<DPP_ROW_MIRROR>(v));
+  return uni(fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48))));
 }
 
 // C^nu for the integral stoichiometric coefficients accepted by ckmi_mech_create

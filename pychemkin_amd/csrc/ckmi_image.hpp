@@ -1,0 +1,236 @@
+// ckmi_image.hpp -- compact mechanism image, staged once per workgroup into LDS.
+//
+// ckmi_mech_create packs every table the rate kernels read into one contiguous byte image
+// (~28 KB for GRI-Mech 3.0).  A kernel workgroup copies it from HBM into LDS with 16-byte
+// loads once, and all of its waves (one reactor or one state each) then read rate
+// parameters, stoichiometry and NASA-7 coefficients at LDS latency instead of L2 latency.
+//
+// Layout (all per-reaction arrays have IIp entries, per-species arrays KKp; reactions are
+// ordered elementary -> third-body -> falloff so a 64-lane strip is type-uniform):
+//   th    double [15][KKp]  tmid, low a1..a7, high a1..a7 (coefficient-major: lane = species)
+//   wt    double [KKp], rwt double [KKp]
+//   lnA, beta, Ea  double [IIp]
+//   rsp, psp  u32 [IIp]   four species indices, one byte each
+//   nu        u32 [IIp]   eight 4-bit integer coefficients (reactants bits 0..15, products 16..31)
+//   info      u32 [IIp]   type:2 rev:1 hasrev:1 ftype:3 nr:3 np:3 | aux index << 16
+//   tb        i32 [IIp]   >= 0 third-body group, <= -2 single collider species -(tb+2), -1 none
+//   aux       double [naux][12]  lnA0 b0 E0/R, falloff p0..p4, REV lnA b E/R, pad
+//   gptr i32 [G+1], gsp i32 [ng], geff double [ng]   third-body efficiency lists (eff - 1)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ckmi {
+
+constexpr int AUXW = 12;
+
+struct MechImage {
+  const uint4* blob;  // device copy of the image
+  int bytes;          // multiple of 16
+  int KK, KKp, II, IIp, G, naux;
+  int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff;
+};
+
+// Dynamic LDS of every kernel that stages the image.  Views hold byte OFFSETS into it, not
+// pointers, so that every access is re-derived from this __shared__ symbol and compiles to
+// ds_* instructions even where a view struct is spilled or passed by reference (a generic
+// pointer reloaded from memory would turn every LDS access into a flat_* access).
+extern __shared__ __attribute__((aligned(16))) char ck_smem[];
+template <typename T>
+__device__ __forceinline__ T* lds_at(int off) {
+  return reinterpret_cast<T*>(ck_smem + off);
+}
+
+struct MechView {
+  int KK, KKp, IIp, G;
+  int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff;
+  __device__ __forceinline__ const double* th() const { return lds_at<const double>(o_th); }
+  __device__ __forceinline__ const double* wt() const { return lds_at<const double>(o_wt); }
+  __device__ __forceinline__ const double* rwt() const { return lds_at<const double>(o_rwt); }
+  __device__ __forceinline__ const double* lnA() const { return lds_at<const double>(o_lnA); }
+  __device__ __forceinline__ const double* beta() const { return lds_at<const double>(o_beta); }
+  __device__ __forceinline__ const double* Ea() const { return lds_at<const double>(o_Ea); }
+  __device__ __forceinline__ const uint32_t* rsp() const { return lds_at<const uint32_t>(o_rsp); }
+  __device__ __forceinline__ const uint32_t* psp() const { return lds_at<const uint32_t>(o_psp); }
+  __device__ __forceinline__ const uint32_t* nu() const { return lds_at<const uint32_t>(o_nu); }
+  __device__ __forceinline__ const uint32_t* info() const { return lds_at<const uint32_t>(o_info); }
+  __device__ __forceinline__ const int* tb() const { return lds_at<const int>(o_tb); }
+  __device__ __forceinline__ const double* aux() const { return lds_at<const double>(o_aux); }
+  __device__ __forceinline__ const int* gptr() const { return lds_at<const int>(o_gptr); }
+  __device__ __forceinline__ const int* gsp() const { return lds_at<const int>(o_gsp); }
+  __device__ __forceinline__ const double* geff() const { return lds_at<const double>(o_geff); }
+};
+
+// view of an image staged at LDS byte offset `base`
+__device__ __forceinline__ MechView make_view(int base, const MechImage& I) {
+  MechView V;
+  V.KK = I.KK;
+  V.KKp = I.KKp;
+  V.IIp = I.IIp;
+  V.G = I.G;
+  V.o_th = base + I.o_th;
+  V.o_wt = base + I.o_wt;
+  V.o_rwt = base + I.o_rwt;
+  V.o_lnA = base + I.o_lnA;
+  V.o_beta = base + I.o_beta;
+  V.o_Ea = base + I.o_Ea;
+  V.o_rsp = base + I.o_rsp;
+  V.o_psp = base + I.o_psp;
+  V.o_nu = base + I.o_nu;
+  V.o_info = base + I.o_info;
+  V.o_tb = base + I.o_tb;
+  V.o_aux = base + I.o_aux;
+  V.o_gptr = base + I.o_gptr;
+  V.o_gsp = base + I.o_gsp;
+  V.o_geff = base + I.o_geff;
+  return V;
+}
+
+// All threads of the workgroup copy the image into LDS; ends with a workgroup barrier.
+__device__ __forceinline__ void stage_image(int base, const MechImage& I) {
+  uint4* dst = lds_at<uint4>(base);
+  const int n16 = I.bytes >> 4;
+  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = I.blob[i];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ info / packing helpers
+__device__ __forceinline__ int rx_type(uint32_t inf) { return inf & 3; }
+__device__ __forceinline__ bool rx_rev(uint32_t inf) { return (inf >> 2) & 1; }
+__device__ __forceinline__ bool rx_hasrev(uint32_t inf) { return (inf >> 3) & 1; }
+__device__ __forceinline__ int rx_ftype(uint32_t inf) { return (inf >> 4) & 7; }
+__device__ __forceinline__ int rx_nr(uint32_t inf) { return (inf >> 7) & 7; }
+__device__ __forceinline__ int rx_np(uint32_t inf) { return (inf >> 10) & 7; }
+__device__ __forceinline__ int rx_aux(uint32_t inf) { return inf >> 16; }
+__device__ __forceinline__ int sp_of(uint32_t packed, int u) { return (packed >> (8 * u)) & 0xff; }
+__device__ __forceinline__ int nur_of(uint32_t nu, int u) { return (nu >> (4 * u)) & 0xf; }
+__device__ __forceinline__ int nup_of(uint32_t nu, int u) { return (nu >> (16 + 4 * u)) & 0xf; }
+
+// C^nu for a small non-negative integer nu
+__device__ __forceinline__ double powi(double c, int nu) {
+  if (nu == 1) return c;
+  if (nu == 2) return c * c;
+  if (nu == 0) return 1.0;
+  double r = c * c * c;
+  for (int k = 3; k < nu; ++k) r *= c;
+  return r;
+}
+
+// ------------------------------------------------------------------ NASA-7 (lane = species)
+struct Thermo7 {
+  double cpR, hRT, sR;
+};
+__device__ __forceinline__ Thermo7 nasa7_img(const MechView& V, int k, double T, double lnT) {
+  const int KKp = V.KKp;
+  const double* t = V.th() + k;
+  const int base = (T > t[0]) ? 8 : 1;
+  const double a0 = t[(base + 0) * KKp], a1 = t[(base + 1) * KKp], a2 = t[(base + 2) * KKp];
+  const double a3 = t[(base + 3) * KKp], a4 = t[(base + 4) * KKp], a5 = t[(base + 5) * KKp];
+  const double a6 = t[(base + 6) * KKp];
+  const double T2 = T * T, T3 = T2 * T, T4 = T3 * T;
+  Thermo7 r;
+  r.cpR = a0 + a1 * T + a2 * T2 + a3 * T3 + a4 * T4;
+  r.hRT = a0 + a1 * T / 2 + a2 * T2 / 3 + a3 * T3 / 4 + a4 * T4 / 5 + a5 / T;
+  r.sR = a0 * lnT + a1 * T + a2 * T2 / 2 + a3 * T3 / 3 + a4 * T4 / 4 + a6;
+  return r;
+}
+
+// ------------------------------------------------------------------ one reaction
+struct Rxn {
+  double kf, kr, mfac, pf, pr, dlkf, dlkr;
+};
+
+// Rate coefficients and concentration products of reaction slot i at (T, C).  C, gRT, hRT
+// and Mg are LDS arrays of the calling wave.  Same arithmetic as oracle/ckoracle.c
+// eval_reaction() (standard Chemkin-II gas kinetics: Arrhenius, third body, Lindemann /
+// Troe / SRI falloff, reverse rates from equilibrium or explicit REV parameters).
+__device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t inf, uint32_t rs, uint32_t ps,
+                                            uint32_t nuw, double T, double lnT, double invT, double lnPRT,
+                                            const double* C, const double* gRT, const double* hRT, const double* Mg,
+                                            bool need_h) {
+  const int type = rx_type(inf);
+  const int nr = rx_nr(inf), np = rx_np(inf);
+  const double lnA = V.lnA()[i], b = V.beta()[i], Ea = V.Ea()[i];
+  const double kf_inf = exp(lnA + b * lnT - Ea * invT);
+  double kf = kf_inf;
+  const double dlkf = (b + Ea * invT) * invT;
+  double mfac = 1.0;
+  const double* ax = V.aux() + AUXW * rx_aux(inf);
+  if (type != 0) {
+    const int tb = V.tb()[i];
+    const double Mc = tb >= 0 ? Mg[tb] : C[-tb - 2];
+    if (type == 1) {
+      mfac = Mc;
+    } else {
+      const double k0 = exp(ax[0] + ax[1] * lnT - ax[2] * invT);
+      const double Pr = k0 * Mc / kf;
+      double F = 1.0;
+      const int ft = rx_ftype(inf);
+      if (ft == 2 || ft == 3) {
+        const double fa = ax[3], T3s = ax[4], T1s = ax[5];
+        double Fcent = (1.0 - fa) * exp(-T / T3s) + fa * exp(-T / T1s);
+        if (ft == 3) Fcent += exp(-ax[6] * invT);
+        const double lFc = log10(Fcent > 1e-300 ? Fcent : 1e-300);
+        const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
+        const double c = -0.4 - 0.67 * lFc, nn = 0.75 - 1.27 * lFc;
+        const double f1 = (lPr + c) / (nn - 0.14 * (lPr + c));
+        F = exp10(lFc / (1.0 + f1 * f1));
+      } else if (ft == 4) {
+        const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
+        const double X = 1.0 / (1.0 + lPr * lPr);
+        F = ax[6] * pow(ax[3] * exp(-ax[4] * invT) + exp(-T / ax[5]), X) * pow(T, ax[7]);
+      }
+      kf = kf * (Pr / (1.0 + Pr)) * F;
+    }
+  }
+  double kr = 0.0, dlkr = 0.0;
+  if (rx_rev(inf)) {
+    if (rx_hasrev(inf)) {
+      kr = exp(ax[8] + ax[9] * lnT - ax[10] * invT);
+      if (type == 2) kr *= kf / kf_inf;
+      dlkr = (ax[9] + ax[10] * invT) * invT;
+    } else {
+      double dG = 0.0, dH = 0.0;
+      int dnu = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u < nr) {
+          const int k = sp_of(rs, u);
+          const int nu = nur_of(nuw, u);
+          dG -= nu * gRT[k];
+          if (need_h) dH -= nu * hRT[k];
+          dnu -= nu;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u < np) {
+          const int k = sp_of(ps, u);
+          const int nu = nup_of(nuw, u);
+          dG += nu * gRT[k];
+          if (need_h) dH += nu * hRT[k];
+          dnu += nu;
+        }
+      }
+      kr = kf * exp(dG - dnu * lnPRT);
+      dlkr = dlkf - (dH - dnu) * invT;
+    }
+  }
+  double pf = 1.0, pr = 1.0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (u < nr) pf *= powi(C[sp_of(rs, u)], nur_of(nuw, u));
+    if (u < np) pr *= powi(C[sp_of(ps, u)], nup_of(nuw, u));
+  }
+  Rxn e;
+  e.kf = kf;
+  e.kr = kr;
+  e.mfac = mfac;
+  e.pf = pf;
+  e.pr = pr;
+  e.dlkf = dlkf;
+  e.dlkr = dlkr;
+  return e;
+}
+
+}  // namespace ckmi

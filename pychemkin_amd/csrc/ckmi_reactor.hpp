@@ -8,11 +8,15 @@
 //
 // Per wave (= reactor):
 //   lanes 0..n-1  one state component each (lane 0 = T, lane k = Y_{k-1}),
-//   VGPRs         the LU rows of M = I - gamma J (row-per-lane, N doubles per lane),
-//   LDS           J (n x ld doubles, reused across steps), concentrations, g/RT, h/RT,
-//                 production and dwdot/dT accumulators, third-body sums.
+//   VGPRs         the LU factors of M = I - gamma J (row-per-lane, N doubles per lane) and the
+//                 Nordsieck history,
+//   LDS           the workgroup's mechanism image (shared), a per-wave slice of species
+//                 vectors and integrator scalars, and one J assembly scratch per workgroup
+//                 (lock-protected; Jacobian evaluations are ~2 % of the RHS calls),
+//   HBM           the wave's last Jacobian (column-major), reloaded when only gamma changes.
 #pragma once
 #include "ckmi_device.hpp"
+#include "ckmi_image.hpp"
 #include "../../include/ckmi.h"
 
 namespace ckmi {
@@ -25,17 +29,20 @@ constexpr double CRDOWN = 0.3, DGMAX = 0.3, RDIV = 2.0, THRESH = 1.5, CORTES = 0
 constexpr int MSBP = 20, MSBJ = 50;
 constexpr double UROUND = 2.220446049250313e-16, NNEG_TOL = 0.01;
 
-struct Lds {
-  double* J;
-  double* A;  // LU factors of I - gamma J
-  double* C;
-  double* gRT;
-  double* hRT;
-  double* wdot;
-  double* dwdT;
-  double* ek;
-  double* Mg;
+// Per-wave LDS slice (one reactor): concentrations, g/RT, h/RT, production and dwdot/dT
+// accumulators, e_k (energy row of J), third-body sums.  Sized for KK <= 63 (VL = 64).
+constexpr int VL = WAVE;
+struct WaveLds {
+  int base;  // LDS byte offset of the slice: C, gRT, hRT, wdot, dwdT, ek [VL] then Mg [G]
+  __device__ __forceinline__ double* C() const { return lds_at<double>(base); }
+  __device__ __forceinline__ double* gRT() const { return lds_at<double>(base + 8 * VL); }
+  __device__ __forceinline__ double* hRT() const { return lds_at<double>(base + 16 * VL); }
+  __device__ __forceinline__ double* wdot() const { return lds_at<double>(base + 24 * VL); }
+  __device__ __forceinline__ double* dwdT() const { return lds_at<double>(base + 32 * VL); }
+  __device__ __forceinline__ double* ek() const { return lds_at<double>(base + 40 * VL); }
+  __device__ __forceinline__ double* Mg() const { return lds_at<double>(base + 48 * VL); }
 };
+constexpr int LDJ = WAVE + 1;  // leading dimension of the shared J scratch (odd: conflict-free columns)
 
 struct RunCtx {
   int conp, energy;
@@ -56,128 +63,149 @@ __device__ __forceinline__ void profile_eval(const ckmi_reactor_cfg* c, int npro
   dvdt = s;
 }
 
-// J[1+k][1+j] += nu_k * dq * W_k / W_j for all participants k of one reaction
-__device__ __forceinline__ void jac_scatter(const MechDev& M, const Lds& L, int ld, int nr, int np, const int4& rs,
-                                            const int4& ps, const double (&rn)[SLOTS], const double (&pn)[SLOTS],
-                                            int j, double dq) {
-  const double wj = M.rwt[j];
+// Orders the wave's LDS accesses (LDS operations of one wave complete in issue order, so
+// a compiler fence is all that is needed between a lane's store and another lane's load).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// J[1+k][1+j] += nu_k dq W_k / W_j for every participant k of one reaction (column-major
+// shared scratch Jsh[col * LDJ + row]).
+__device__ __forceinline__ void jac_scatter(const MechView& V, int oJ, int nr, int np, uint32_t rs, uint32_t ps,
+                                            uint32_t nuw, int j, double dq) {
+  double* col = lds_at<double>(oJ) + (1 + j) * LDJ + 1;
+  const double dqw = dq * V.rwt()[j];
 #pragma unroll
-  for (int u = 0; u < SLOTS; ++u) {
+  for (int u = 0; u < 4; ++u) {
     if (u < nr) {
-      const int k = slot(rs, u);
-      atomicAdd(&L.J[(1 + k) * ld + 1 + j], -rn[u] * dq * M.wt[k] * wj);
+      const int k = sp_of(rs, u);
+      atomicAdd(&col[k], -nur_of(nuw, u) * dqw * V.wt()[k]);
     }
     if (u < np) {
-      const int k = slot(ps, u);
-      atomicAdd(&L.J[(1 + k) * ld + 1 + j], pn[u] * dq * M.wt[k] * wj);
+      const int k = sp_of(ps, u);
+      atomicAdd(&col[k], nup_of(nuw, u) * dqw * V.wt()[k]);
     }
   }
 }
 
-// Right-hand side f(t, y) (returned per lane) and, if WITH_J, the approximate analytic
-// Jacobian into L.J (row-major, leading dimension ld).  Mirrors oracle reactor_rhs().
-template <bool WITH_J>
-__device__ __forceinline__ double reactor_rhs(const MechDev& M, const RunCtx& R, double t, double yl, const Lds& L, int lane, int n,
-                              int ld) {
-  const int KK = M.KK;
+// Right-hand side f(t, y) (one component per lane, lane 0 = T) and, if with_j, the
+// approximate analytic Jacobian into the workgroup's shared J scratch (column-major, the
+// caller holds its lock).  Same formulation as oracle/ckoracle.c reactor_rhs().  with_j is a
+// run-time (wave-uniform) flag and the Jacobian terms are a second pass over the reactions,
+// so the integrator has a single RHS call site and the register peak is that of one pass.
+__device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R, double t, double yl,
+                                              const WaveLds& L, int oJ, int lane, int ncol, bool with_j) {
+  const int KK = V.KK;
   const bool isp = lane >= 1 && lane <= KK;
   const int s = isp ? lane - 1 : 0;
   const double T = bcast(yl, 0);
   const double Yk = isp ? yl : 0.0;
-  const double rw = isp ? M.rwt[s] : 0.0;
-  const double Wk = isp ? M.wt[s] : 0.0;
+  const double rw = isp ? V.rwt()[s] : 0.0;
+  const double Wk = isp ? V.wt()[s] : 0.0;
   const double Wbar = 1.0 / wave_sum(Yk * rw);
   const int conp = R.conp;
-  double rho, P, V, dVdt = 0.0, dPdt = 0.0;
+  double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
   if (conp) {
     profile_eval(R.cfg, R.cfg->nprof, t, R.P0, P, dPdt);
     rho = P * Wbar / (RU * T);
-    V = R.rho0 * R.V0 / rho;
+    V_ = R.rho0 * R.V0 / rho;
   } else {
-    profile_eval(R.cfg, R.cfg->nprof, t, R.V0, V, dVdt);
-    rho = R.rho0 * R.V0 / V;
+    profile_eval(R.cfg, R.cfg->nprof, t, R.V0, V_, dVdt);
+    rho = R.rho0 * R.V0 / V_;
     P = rho * RU * T / Wbar;
   }
   const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   const double Ck = rho * Yk * rw;
-  SpThermo th;
+  Thermo7 th;
   th.cpR = th.hRT = th.sR = 0.0;
+  double* C = L.C();
   if (isp) {
-    th = nasa7(M, s, T, lnT);
-    L.C[s] = Ck;
-    L.gRT[s] = th.hRT - th.sR;
-    L.wdot[s] = 0.0;
-    if (WITH_J) {
-      L.hRT[s] = th.hRT;
-      L.dwdT[s] = 0.0;
-    }
+    th = nasa7_img(V, s, T, lnT);
+    C[s] = Ck;
+    L.gRT()[s] = th.hRT - th.sR;
+    L.wdot()[s] = 0.0;
+    L.hRT()[s] = th.hRT;
+    L.dwdT()[s] = 0.0;
   }
   const double Ctot = wave_sum(Ck);
-  if (WITH_J) {
-    for (int idx = lane; idx < n * ld; idx += WAVE) L.J[idx] = 0.0;
+  double* Jsh = lds_at<double>(oJ);
+  if (with_j) {
+    for (int idx = lane; idx < ncol * LDJ; idx += WAVE) Jsh[idx] = 0.0;
   }
-  __syncthreads();
-  for (int g = lane; g < M.G; g += WAVE) {
+  wave_lds_sync();
+  for (int g = lane; g < V.G; g += WAVE) {
     double m = Ctot;
-    for (int p = M.gptr[g]; p < M.gptr[g + 1]; ++p) m += M.geff[p] * L.C[M.gsp[p]];
-    L.Mg[g] = m;
+    for (int p = V.gptr()[g]; p < V.gptr()[g + 1]; ++p) m += V.geff()[p] * C[V.gsp()[p]];
+    L.Mg()[g] = m;
   }
-  __syncthreads();
-  const int IIp = M.IIpad;
+  wave_lds_sync();
+  const int IIp = V.IIp;
   for (int base = 0; base < IIp; base += WAVE) {
     const int i = base + lane;
-    const int nrp = M.nrp[i];
-    const int nr = nrp & 0xff, np = nrp >> 8;
+    const uint32_t inf = V.info()[i];
+    const int nr = rx_nr(inf), np = rx_np(inf);
     if (nr + np == 0) continue;
-    const RxnEval e = eval_rxn(M, i, T, lnT, invT, lnPRT, L.C, L.gRT, L.hRT, L.Mg, WITH_J);
+    const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
+    const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false);
     const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
-    const int4 rs = M.rsp[i], ps = M.psp[i];
-    double rn[SLOTS], pn[SLOTS];
 #pragma unroll
-    for (int u = 0; u < SLOTS; ++u) {
-      rn[u] = M.rnu[u * IIp + i];
-      pn[u] = M.pnu[u * IIp + i];
+    for (int u = 0; u < 4; ++u) {
+      if (u < nr) atomicAdd(&L.wdot()[sp_of(rs, u)], -nur_of(nuw, u) * q);
+      if (u < np) atomicAdd(&L.wdot()[sp_of(ps, u)], nup_of(nuw, u) * q);
     }
-#pragma unroll
-    for (int u = 0; u < SLOTS; ++u) {
-      if (u < nr) atomicAdd(&L.wdot[slot(rs, u)], -rn[u] * q);
-      if (u < np) atomicAdd(&L.wdot[slot(ps, u)], pn[u] * q);
-    }
-    if (WITH_J) {
+  }
+  if (with_j) {
+    for (int base = 0; base < IIp; base += WAVE) {
+      const int i = base + lane;
+      const uint32_t inf = V.info()[i];
+      const int nr = rx_nr(inf), np = rx_np(inf);
+      if (nr + np == 0) continue;
+      const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
+      const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), true);
+      const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
       double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
       if (conp) {
-        dqdT -= e.mfac * (M.ordf[i] * e.kf * e.pf - M.ordr[i] * e.kr * e.pr) * invT;
-        if ((M.flags[i] & 3) == 1) dqdT -= q * invT;
+        int ordf = 0, ordr = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (u < nr) ordf += nur_of(nuw, u);
+          if (u < np) ordr += nup_of(nuw, u);
+        }
+        dqdT -= e.mfac * (ordf * e.kf * e.pf - ordr * e.kr * e.pr) * invT;
+        if (rx_type(inf) == 1) dqdT -= q * invT;
       }
 #pragma unroll
-      for (int u = 0; u < SLOTS; ++u) {
-        if (u < nr) atomicAdd(&L.dwdT[slot(rs, u)], -rn[u] * dqdT);
-        if (u < np) atomicAdd(&L.dwdT[slot(ps, u)], pn[u] * dqdT);
+      for (int u = 0; u < 4; ++u) {
+        if (u < nr) atomicAdd(&L.dwdT()[sp_of(rs, u)], -nur_of(nuw, u) * dqdT);
+        if (u < np) atomicAdd(&L.dwdT()[sp_of(ps, u)], nup_of(nuw, u) * dqdT);
       }
-      // dq/dC_j for every reactant slot (forward) and product slot (reverse), scattered
-      // into the rows of all participating species
+      // dq/dC_j for every reactant slot (forward) and product slot (reverse)
 #pragma unroll
-      for (int sl = 0; sl < SLOTS; ++sl) {
+      for (int sl = 0; sl < 4; ++sl) {
         if (sl < nr && e.kf != 0.0) {
-          double d = rn[sl] * powi_nu(L.C[slot(rs, sl)], rn[sl] - 1.0);
+          const int nus = nur_of(nuw, sl);
+          double d = nus * powi(C[sp_of(rs, sl)], nus - 1);
 #pragma unroll
-          for (int u = 0; u < SLOTS; ++u)
-            if (u < nr && u != sl) d *= powi_nu(L.C[slot(rs, u)], rn[u]);
-          jac_scatter(M, L, ld, nr, np, rs, ps, rn, pn, slot(rs, sl), e.mfac * e.kf * d);
+          for (int u = 0; u < 4; ++u)
+            if (u < nr && u != sl) d *= powi(C[sp_of(rs, u)], nur_of(nuw, u));
+          jac_scatter(V, oJ, nr, np, rs, ps, nuw, sp_of(rs, sl), e.mfac * e.kf * d);
         }
         if (sl < np && e.kr != 0.0) {
-          double d = pn[sl] * powi_nu(L.C[slot(ps, sl)], pn[sl] - 1.0);
+          const int nus = nup_of(nuw, sl);
+          double d = nus * powi(C[sp_of(ps, sl)], nus - 1);
 #pragma unroll
-          for (int u = 0; u < SLOTS; ++u)
-            if (u < np && u != sl) d *= powi_nu(L.C[slot(ps, u)], pn[u]);
-          jac_scatter(M, L, ld, nr, np, rs, ps, rn, pn, slot(ps, sl), -e.mfac * e.kr * d);
+          for (int u = 0; u < 4; ++u)
+            if (u < np && u != sl) d *= powi(C[sp_of(ps, u)], nup_of(nuw, u));
+          jac_scatter(V, oJ, nr, np, rs, ps, nuw, sp_of(ps, sl), -e.mfac * e.kr * d);
         }
       }
     }
   }
-  __syncthreads();
+  wave_lds_sync();
   const double rinv = 1.0 / rho;
-  const double fY = isp ? L.wdot[s] * Wk * rinv : 0.0;
+  const double fY = isp ? L.wdot()[s] * Wk * rinv : 0.0;
   double fl = fY;
   if (R.energy == 1) {
     const double cpk = th.cpR * RU * rw;
@@ -188,85 +216,118 @@ __device__ __forceinline__ double reactor_rhs(const MechDev& M, const RunCtx& R,
     const double sum = wave_sum(ek * fY);
     double fT = -sum / cpm;
     if (conp) fT += dPdt / (rho * cpm);
-    else fT -= P * dVdt / (V * rho * cpm);
+    else fT -= P * dVdt / (V_ * rho * cpm);
     if (lane == 0) fl = fT;
-    if (WITH_J) {
-      const double JkT = isp ? L.dwdT[s] * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;
+    if (with_j) {
+      const double JkT = isp ? L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;
       if (isp) {
-        L.J[(1 + s) * ld] = JkT;
-        L.ek[s] = ek;
+        Jsh[1 + s] = JkT;  // column 0 (d/dT), row 1+s
+        L.ek()[s] = ek;
       }
-      __syncthreads();
+      wave_lds_sync();
       if (isp) {
+        const double* col = Jsh + (1 + s) * LDJ + 1;
+        const double* ekv = L.ek();
         double acc = 0.0;
-        for (int k = 0; k < KK; ++k) acc += L.ek[k] * L.J[(1 + k) * ld + 1 + s];
-        L.J[1 + s] = -acc / cpm - fT * ck / cpm;
+        for (int k = 0; k < KK; ++k) acc += ekv[k] * col[k];
+        Jsh[(1 + s) * LDJ] = -acc / cpm - fT * ck / cpm;  // row 0, column 1+s
       }
       const double s2 = wave_sum(ck * fY + ek * JkT);
-      if (lane == 0) L.J[0] = -s2 / cpm;
+      if (lane == 0) Jsh[0] = -s2 / cpm;
     }
   } else {
     if (lane == 0) fl = 0.0;
-    if (WITH_J && isp) L.J[(1 + s) * ld] = L.dwdT[s] * Wk * rinv + (conp ? fY * invT : 0.0);
+    if (with_j && isp) Jsh[1 + s] = L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0);
   }
-  if (WITH_J) __syncthreads();
+  wave_lds_sync();
   return fl;
 }
 
-// ----------------------------------------------------------------- LDS LU
-// Row-per-lane LU with partial pivoting of the n x n matrix A (LDS, row-major, odd leading
-// dimension ld so that lane i's row accesses are bank-conflict free).  Lane i owns row i.
-// Pivot rows are chosen by a wave arg-max; rows are never moved: the permutation is kept as
-// (pivot step of each lane = `order`, pivot lane of step k in lane k = `permv`).
-__device__ __forceinline__ bool lu_factor_lds(double* A, int ld, int lane, int n, int& order, int& permv,
-                                              double& rdiag) {
-  bool pivoted = lane >= n;
-  order = pivoted ? (1 << 20) : 0;
-  permv = 0;
-  rdiag = 1.0;
-  bool ok = true;
-  double* row = A + (size_t)(lane < n ? lane : 0) * ld;
-  for (int k = 0; k < n; ++k) {
-    const double v = pivoted ? -1.0 : fabs(row[k]);
-    const double vmax = wave_max(v);
-    if (!(vmax > 0.0)) ok = false;
-    const uint64_t mask = __ballot(!pivoted && v == vmax);
-    const int p = uni(mask ? (int)__ffsll((unsigned long long)mask) - 1 : 0);
-    const double* prow = A + (size_t)p * ld;
-    const double rp = 1.0 / prow[k];
-    if (lane == p) {
-      pivoted = true;
-      order = k;
-      rdiag = rp;
-    }
-    if (lane == k) permv = p;
-    if (!pivoted) {
-      const double l = row[k] * rp;
-      row[k] = l;
-      for (int j = k + 1; j < n; ++j) row[j] = fma(-l, prow[j], row[j]);
-    }
-    __syncthreads();
-  }
-  return ok;
+// ----------------------------------------------------------------- Newton matrix in VGPRs
+// M = I - gamma J is held row-per-lane in registers: lane i owns row i as a[0..N-1]
+// (N = compile-time padded size >= n; columns >= n are zero, lanes >= n are inert).  LU with
+// partial pivoting never moves rows: `order` = elimination step at which this lane's row was
+// the pivot, lane k of `permv` = pivot lane of step k.  Pivot rows are broadcast with
+// v_readlane, the pivot search is a DPP wave max, so the factorisation and the triangular
+// solves never touch LDS.
+// The lane index laundered through an empty volatile asm: comparisons of it with the
+// unrolled loop constants below must be computed where they are used.  Left visible, LICM
+// hoists all N (lane == j) masks / identity entries out of the persistent reactor loop and
+// keeps them live (spilled) across the whole integrator.
+__device__ __forceinline__ int opaque_lane(int lane) {
+  asm volatile("" : "+v"(lane));
+  return lane;
 }
 
-__device__ __forceinline__ double lu_solve_lds(const double* A, int ld, int lane, int n, int order, int permv,
-                                               double rdiag, double b) {
-  const double* row = A + (size_t)(lane < n ? lane : 0) * ld;
-  for (int k = 0; k < n; ++k) {
-    const int p = bcast(permv, k);
-    const double sv = bcast(b, p);
-    if (order > k && lane < n) b = fma(-row[k], sv, b);
+template <int N>
+struct NewtonMatrix {
+  double a[N];
+  int order, permv;
+  double rdiag;
+
+  // a = I - gamma J, J column-major with leading dimension ldj >= 64 (every lane reads its own
+  // row; rows >= n are zero)
+  __device__ __forceinline__ void build(const double* J, int ldj, double gamma, int lane_in, int n) {
+    const int lane = opaque_lane(lane_in);
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = (j == lane ? 1.0 : 0.0) - gamma * J[j * ldj + lane];
   }
-  double x = 0.0;
-  for (int k = n - 1; k >= 0; --k) {
-    const int p = bcast(permv, k);
-    const double xk = bcast(b, p) * bcast(rdiag, p);
-    if (lane == k) x = xk;
-    if (order < k && lane < n) b = fma(-row[k], xk, b);
+
+  __device__ __forceinline__ bool factor(int lane_in, int n) {
+    const int lane = opaque_lane(lane_in);
+    bool pivoted = lane >= n;
+    order = pivoted ? (1 << 20) : 0;
+    permv = 0;
+    rdiag = 1.0;
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (k < n) {
+        const double v = pivoted ? -1.0 : fabs(a[k]);
+        const double vmax = wave_max(v);
+        if (!(vmax > 0.0)) ok = false;
+        const uint64_t mask = __ballot(!pivoted && v == vmax);
+        const int p = uni(mask ? (int)__ffsll((unsigned long long)mask) - 1 : 0);
+        const double rp = 1.0 / bcast(a[k], p);
+        if (lane == p) {
+          pivoted = true;
+          order = k;
+          rdiag = rp;
+        }
+        if (lane == k) permv = p;
+        const double l = pivoted ? 0.0 : a[k] * rp;
+        if (!pivoted) a[k] = l;
+#pragma unroll
+        for (int j = k + 1; j < N; ++j) a[j] = fma(-l, bcast(a[j], p), a[j]);
+      }
+    }
+    return ok;
   }
-  return x;
-}
+
+  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
+    const int lane = opaque_lane(lane_in);
+    if (lane >= n) b = 0.0;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (k < n) {
+        const int p = bcast(permv, k);
+        const double sv = bcast(b, p);
+        b = fma(order > k ? -a[k] : 0.0, sv, b);
+      }
+    }
+    double x = 0.0;
+#pragma unroll
+    for (int k = N - 1; k >= 0; --k) {
+      if (k < n) {
+        const int p = bcast(permv, k);
+        const double xk = bcast(b, p) * bcast(rdiag, p);
+        if (lane == k) x = xk;
+        b = fma(order < k ? -a[k] : 0.0, xk, b);
+      }
+    }
+    return x;
+  }
+};
 
 // uniform small-array access with runtime index (keeps the arrays in SGPRs)
 template <int S>
