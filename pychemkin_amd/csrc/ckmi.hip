@@ -33,7 +33,8 @@ enum { NF_FIRST = 0, NF_CONV_FAIL = 1, NF_ERR_FAIL = 2 };
 
 // Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py): per-reactor shader
 // cycles spent in each phase, written to a debug buffer no other code reads.
-enum { PH_RHS = 0, PH_JAC = 1, PH_LU = 2, PH_SOLVE = 3, PH_TOTAL = 4, PH_N = 8 };
+// Slots 8..31 accumulate the cycles spent in each integrator state (RHS, LU, solve excluded).
+enum { PH_RHS = 0, PH_JAC = 1, PH_LU = 2, PH_SOLVE = 3, PH_TOTAL = 4, PH_STATE = 8, PH_N = 32 };
 #ifdef CKMI_PHASE_TIMERS
 __device__ unsigned long long* g_phase_buf = nullptr;
 #define PH_T0() const unsigned long long _ph0 = __builtin_amdgcn_s_memtime()
@@ -143,8 +144,14 @@ struct Ctl {
 // ignition monitor.
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 __host__ __device__ constexpr int slice_vec_bytes(int G) { return align16(8 * (6 * VL + (G > 0 ? G : 1))); }
+#ifdef CKMI_PHASE_TIMERS
+constexpr int PH_SLICE = 8 * 32;  // per-state cycle counters of the wave
+#else
+constexpr int PH_SLICE = 0;
+#endif
 __host__ __device__ constexpr int slice_bytes(int G) {
-  return slice_vec_bytes(G) + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign));
+  return slice_vec_bytes(G) + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)) +
+         PH_SLICE;
 }
 template <int N>
 __host__ __device__ constexpr int jscratch_bytes() {
@@ -216,8 +223,10 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
   double fe = 0.0, y_e = 0.0, t_e = 0.0;
   bool with_j = false;
 #ifdef CKMI_PHASE_TIMERS
-  unsigned long long ph[PH_N] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_r0 = 0;
+  unsigned long long* phs = lds_at<unsigned long long>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) +
+                                                     align16((int)sizeof(Ign)));
 #endif
   int st = ST_NEXT;
 
@@ -245,6 +254,10 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
   for (;;) {
     bool want = false;
     while (!want && st != ST_EXIT) {
+#ifdef CKMI_PHASE_TIMERS
+      const int st_in = st;
+      const unsigned long long t_st = __builtin_amdgcn_s_memtime();
+#endif
       switch (st) {
         case ST_NEXT: {
           int r = 0;
@@ -263,6 +276,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
           R.conp = (prob == 1);
           R.energy = cfg->energy;
+          R.nprof = cfg->nprof;
           R.rho0 = P0 * Wbar0 / (RU * T0);
           R.V0 = (!R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : io.V0[r];
           R.P0 = (R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : P0;
@@ -281,7 +295,8 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           c.max_steps = cfg->max_steps > 0 ? cfg->max_steps : 200000;
 #ifdef CKMI_PHASE_TIMERS
 #pragma unroll
-          for (int k = 0; k < PH_N; ++k) ph[k] = 0;
+          for (int k = 0; k < 8; ++k) ph[k] = 0;
+          if (lane < 32) phs[lane] = 0;
           t_r0 = __builtin_amdgcn_s_memtime();
 #endif
           START_BEGIN(0.0, yl, crit_time(cfg, c.tend, 0), cfg->h0);
@@ -622,7 +637,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           S.etamax = 1.0;
           st = ST_STEP_ATTEMPT;
           if (c.nef <= MXNEF1) {
-            S.eta = 1.0 / (pow(BIAS2 * c.dsm, 1.0 / S.L) + ADDON);
+            S.eta = 1.0 / (eta_root(BIAS2 * c.dsm, S.L) + ADDON);
             S.eta = fmax(ETAMIN, fmax(S.eta, S.hmin / fabs(S.h)));
             if (c.nef >= SMALL_NEF) S.eta = fmin(S.eta, ETAMXF);
             bdf_rescale(b, S);
@@ -674,7 +689,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
             S.hprime = S.h;
             S.eta = 1.0;
           } else {
-            const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / S.L) + ADDON);
+            const double etaq = 1.0 / (eta_root(BIAS2 * dsm, S.L) + ADDON);
             if (S.qwait != 0) {
               S.eta = etaq;
               S.qprime = S.q;
@@ -687,13 +702,16 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
                 for (int j = 0; j <= QMAX; ++j)
                   if (j == S.q) znq = b.zn[j];
                 const double ddn = wrms_lane(act ? znq : 0.0, b.ewt, n) * S.tq[1];
-                etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / S.q) + ADDON);
+                etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, S.q) + ADDON);
               }
               if (S.q != QMAX && S.saved_tq5 != 0.0) {
-                const double cquot = (S.tq[5] / S.saved_tq5) * pow(S.h / S.tau[2], (double)S.L);
+                const double hr = S.h / S.tau[2];
+                double hrL = hr;
+                for (int j = 1; j < S.L; ++j) hrL *= hr;
+                const double cquot = (S.tq[5] / S.saved_tq5) * hrL;
                 const double tv = act ? b.acor - cquot * b.zn[QMAX] : 0.0;
                 const double dup = wrms_lane(tv, b.ewt, n) * S.tq[3];
-                etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (S.L + 1)) + ADDON);
+                etaqp1 = 1.0 / (eta_root(BIAS3 * dup, S.L + 1) + ADDON);
               }
               const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
               if (etam < THRESH) {
@@ -806,10 +824,11 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           if (isp) io.Y[(size_t)r * KK + lane - 1] = yf;
 #ifdef CKMI_PHASE_TIMERS
           ph[PH_TOTAL] = __builtin_amdgcn_s_memtime() - t_r0;
+          wave_lds_sync();
           if (g_phase_buf && lane < PH_N) {
-            unsigned long long v = 0;
+            unsigned long long v = lane >= PH_STATE ? phs[lane - PH_STATE] : 0;
 #pragma unroll
-            for (int k = 0; k < PH_N; ++k) v = (lane == k) ? ph[k] : v;
+            for (int k = 0; k < 8; ++k) v = (lane == k) ? ph[k] : v;
             g_phase_buf[(size_t)r * PH_N + lane] = v;
           }
 #endif
@@ -820,15 +839,26 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           st = ST_EXIT;
           break;
       }
+#ifdef CKMI_PHASE_TIMERS
+      if (st_in != ST_NEXT && st_in != ST_FINISH && lane == 0) phs[st_in] += __builtin_amdgcn_s_memtime() - t_st;
+#endif
     }
     if (st == ST_EXIT) break;
     // the single RHS (+ Jacobian) evaluation site of the integrator
 #ifdef CKMI_PHASE_TIMERS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-    fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j);
 #ifdef CKMI_PHASE_TIMERS
+    unsigned long long sub[3] = {0, 0, 0};
+    fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j, sub);
     ph[with_j ? PH_JAC : PH_RHS] += __builtin_amdgcn_s_memtime() - t0;
+    if (!with_j) {
+      ph[5] += sub[0];
+      ph[6] += sub[1];
+      ph[7] += sub[2];
+    }
+#else
+    fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j);
 #endif
   }
 #undef REQUEST_F
@@ -1052,6 +1082,10 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   const double dzero = 0.0;
   I.o_gsp = gsp.empty() ? put(&zero, 4) : put(gsp.data(), gsp.size() * 4);
   I.o_geff = geff.empty() ? put(&dzero, 8) : put(geff.data(), geff.size() * 8);
+  std::vector<double> geffd((size_t)std::max(G, 1) * KKp, 0.0);
+  for (int g = 0; g < G; ++g)
+    for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)g * KKp + gsp[e]] = geff[e];
+  I.o_geffd = put(geffd.data(), geffd.size() * 8);
   I.bytes = (int)blob.size();
   void* p = nullptr;
   HIP_CHECK(hipMalloc(&p, blob.size()));

@@ -16,6 +16,7 @@ constexpr double BOLTZMANN = 1.3806504e-16;
 constexpr double AVOGADRO = 6.02214179e23;
 constexpr double RU = BOLTZMANN * AVOGADRO;  // erg/mol-K (reference constants.py:37)
 constexpr double PATM = 1.01325e6;           // dyn/cm2  (reference constants.py:28)
+constexpr double LN_PATM_RU = -4.407419774071825;  // ln(PATM / RU): ln(PATM / (RU T)) = LN_PATM_RU - ln T
 
 // Device-resident mechanism tables.  Reactions are re-ordered by type (elementary first,
 // then third-body, then falloff) so that a 64-lane strip is type-uniform; `orig` maps a

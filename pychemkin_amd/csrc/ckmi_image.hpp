@@ -16,6 +16,7 @@
 //   tb        i32 [IIp]   >= 0 third-body group, <= -2 single collider species -(tb+2), -1 none
 //   aux       double [naux][12]  lnA0 b0 E0/R, falloff p0..p4, REV lnA b E/R, pad
 //   gptr i32 [G+1], gsp i32 [ng], geff double [ng]   third-body efficiency lists (eff - 1)
+//   geffd double [G][KKp]   the same lists dense (eff - 1, 0 for unlisted species)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,7 +29,7 @@ struct MechImage {
   const uint4* blob;  // device copy of the image
   int bytes;          // multiple of 16
   int KK, KKp, II, IIp, G, naux;
-  int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff;
+  int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff, o_geffd;
 };
 
 // Dynamic LDS of every kernel that stages the image.  Views hold byte OFFSETS into it, not
@@ -43,7 +44,7 @@ __device__ __forceinline__ T* lds_at(int off) {
 
 struct MechView {
   int KK, KKp, IIp, G;
-  int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff;
+  int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff, o_geffd;
   __device__ __forceinline__ const double* th() const { return lds_at<const double>(o_th); }
   __device__ __forceinline__ const double* wt() const { return lds_at<const double>(o_wt); }
   __device__ __forceinline__ const double* rwt() const { return lds_at<const double>(o_rwt); }
@@ -59,6 +60,7 @@ struct MechView {
   __device__ __forceinline__ const int* gptr() const { return lds_at<const int>(o_gptr); }
   __device__ __forceinline__ const int* gsp() const { return lds_at<const int>(o_gsp); }
   __device__ __forceinline__ const double* geff() const { return lds_at<const double>(o_geff); }
+  __device__ __forceinline__ const double* geffd() const { return lds_at<const double>(o_geffd); }
 };
 
 // view of an image staged at LDS byte offset `base`
@@ -83,6 +85,7 @@ __device__ __forceinline__ MechView make_view(int base, const MechImage& I) {
   V.o_gptr = base + I.o_gptr;
   V.o_gsp = base + I.o_gsp;
   V.o_geff = base + I.o_geff;
+  V.o_geffd = base + I.o_geffd;
   return V;
 }
 

@@ -45,7 +45,7 @@ struct WaveLds {
 constexpr int LDJ = WAVE + 1;  // leading dimension of the shared J scratch (odd: conflict-free columns)
 
 struct RunCtx {
-  int conp, energy;
+  int conp, energy, nprof;
   double rho0, V0, P0;
   const ckmi_reactor_cfg* cfg;
 };
@@ -96,7 +96,22 @@ __device__ __forceinline__ void jac_scatter(const MechView& V, int oJ, int nr, i
 // run-time (wave-uniform) flag and the Jacobian terms are a second pass over the reactions,
 // so the integrator has a single RHS call site and the register peak is that of one pass.
 __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R, double t, double yl,
-                                              const WaveLds& L, int oJ, int lane, int ncol, bool with_j) {
+                                              const WaveLds& L, int oJ, int lane, int ncol, bool with_j
+#ifdef CKMI_PHASE_TIMERS
+                                              , unsigned long long (&sub)[3]
+#endif
+) {
+#ifdef CKMI_PHASE_TIMERS
+  unsigned long long tsub = __builtin_amdgcn_s_memtime();
+#define SUB_PHASE(k)                                      \
+  do {                                                    \
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime(); \
+    sub[k] += t2 - tsub;                                  \
+    tsub = t2;                                            \
+  } while (0)
+#else
+#define SUB_PHASE(k) (void)0
+#endif
   const int KK = V.KK;
   const bool isp = lane >= 1 && lane <= KK;
   const int s = isp ? lane - 1 : 0;
@@ -108,15 +123,15 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const int conp = R.conp;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
   if (conp) {
-    profile_eval(R.cfg, R.cfg->nprof, t, R.P0, P, dPdt);
+    profile_eval(R.cfg, R.nprof, t, R.P0, P, dPdt);
     rho = P * Wbar / (RU * T);
     V_ = R.rho0 * R.V0 / rho;
   } else {
-    profile_eval(R.cfg, R.cfg->nprof, t, R.V0, V_, dVdt);
+    profile_eval(R.cfg, R.nprof, t, R.V0, V_, dVdt);
     rho = R.rho0 * R.V0 / V_;
     P = rho * RU * T / Wbar;
   }
-  const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
+  const double lnT = log(T), invT = 1.0 / T, lnPRT = LN_PATM_RU - lnT;
   const double Ck = rho * Yk * rw;
   Thermo7 th;
   th.cpR = th.hRT = th.sR = 0.0;
@@ -135,12 +150,30 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     for (int idx = lane; idx < ncol * LDJ; idx += WAVE) Jsh[idx] = 0.0;
   }
   wave_lds_sync();
+  // third-body concentrations [M]_g = Ctot + sum_k (eff_gk - 1) C_k, lane g
+#ifdef CKMI_MG_DENSE
+  for (int g = lane; g < V.G; g += WAVE) {
+    const double* e = V.geffd() + g * V.KKp;
+    double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+    int k = 0;
+    for (; k + 4 <= KK; k += 4) {
+      m0 = fma(e[k], C[k], m0);
+      m1 = fma(e[k + 1], C[k + 1], m1);
+      m2 = fma(e[k + 2], C[k + 2], m2);
+      m3 = fma(e[k + 3], C[k + 3], m3);
+    }
+    for (; k < KK; ++k) m0 = fma(e[k], C[k], m0);
+    L.Mg()[g] = Ctot + ((m0 + m1) + (m2 + m3));
+  }
+#else
   for (int g = lane; g < V.G; g += WAVE) {
     double m = Ctot;
     for (int p = V.gptr()[g]; p < V.gptr()[g + 1]; ++p) m += V.geff()[p] * C[V.gsp()[p]];
     L.Mg()[g] = m;
   }
+#endif
   wave_lds_sync();
+  SUB_PHASE(0);
   const int IIp = V.IIp;
   for (int base = 0; base < IIp; base += WAVE) {
     const int i = base + lane;
@@ -204,6 +237,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     }
   }
   wave_lds_sync();
+  SUB_PHASE(1);
   const double rinv = 1.0 / rho;
   const double fY = isp ? L.wdot()[s] * Wk * rinv : 0.0;
   double fl = fY;
@@ -240,16 +274,20 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     if (with_j && isp) Jsh[1 + s] = L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0);
   }
   wave_lds_sync();
+  SUB_PHASE(2);
+#undef SUB_PHASE
   return fl;
 }
 
 // ----------------------------------------------------------------- Newton matrix in VGPRs
 // M = I - gamma J is held row-per-lane in registers: lane i owns row i as a[0..N-1]
 // (N = compile-time padded size >= n; columns >= n are zero, lanes >= n are inert).  LU with
-// partial pivoting never moves rows: `order` = elimination step at which this lane's row was
-// the pivot, lane k of `permv` = pivot lane of step k.  Pivot rows are broadcast with
-// v_readlane, the pivot search is a DPP wave max, so the factorisation and the triangular
-// solves never touch LDS.
+// partial pivoting: the pivot search is a DPP wave max, the pivot row is broadcast with
+// v_readlane, rows are not moved during elimination.  Afterwards the rows are permuted with
+// ds_bpermute so that lane k holds the k-th pivot row (L multipliers left of the diagonal,
+// U / u_kk right of it, 1 / u_kk in rdiag): both triangular sweeps then broadcast from a
+// compile-time lane and never touch LDS memory.
+
 // The lane index laundered through an empty volatile asm: comparisons of it with the
 // unrolled loop constants below must be computed where they are used.  Left visible, LICM
 // hoists all N (lane == j) masks / identity entries out of the persistent reactor loop and
@@ -259,11 +297,17 @@ __device__ __forceinline__ int opaque_lane(int lane) {
   return lane;
 }
 
+__device__ __forceinline__ double bpermute(int src_lane, double v) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane * 4, __double2loint(v));
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane * 4, __double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+
 template <int N>
 struct NewtonMatrix {
   double a[N];
-  int order, permv;
-  double rdiag;
+  int permv;     // lane k: the lane whose row was the pivot of step k
+  double rdiag;  // 1 / u_kk of this lane's (permuted) row
 
   // a = I - gamma J, J column-major with leading dimension ldj >= 64 (every lane reads its own
   // row; rows >= n are zero)
@@ -276,8 +320,7 @@ struct NewtonMatrix {
   __device__ __forceinline__ bool factor(int lane_in, int n) {
     const int lane = opaque_lane(lane_in);
     bool pivoted = lane >= n;
-    order = pivoted ? (1 << 20) : 0;
-    permv = 0;
+    permv = lane;
     rdiag = 1.0;
     bool ok = true;
 #pragma unroll
@@ -291,7 +334,6 @@ struct NewtonMatrix {
         const double rp = 1.0 / bcast(a[k], p);
         if (lane == p) {
           pivoted = true;
-          order = k;
           rdiag = rp;
         }
         if (lane == k) permv = p;
@@ -301,31 +343,30 @@ struct NewtonMatrix {
         for (int j = k + 1; j < N; ++j) a[j] = fma(-l, bcast(a[j], p), a[j]);
       }
     }
+    // lane k <- row of lane permv[k]; scale the U part by 1 / u_kk
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = bpermute(permv, a[j]);
+    rdiag = bpermute(permv, rdiag);
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = (j > lane) ? a[j] * rdiag : a[j];
     return ok;
   }
 
+  // x = M^-1 b (lane k: component k), using P M = L U from factor()
   __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
     const int lane = opaque_lane(lane_in);
+    b = bpermute(permv, b);
     if (lane >= n) b = 0.0;
 #pragma unroll
     for (int k = 0; k < N; ++k) {
-      if (k < n) {
-        const int p = bcast(permv, k);
-        const double sv = bcast(b, p);
-        b = fma(order > k ? -a[k] : 0.0, sv, b);
-      }
+      if (k < n) b = fma(lane > k ? -a[k] : 0.0, bcast(b, k), b);
     }
-    double x = 0.0;
+    b *= rdiag;
 #pragma unroll
     for (int k = N - 1; k >= 0; --k) {
-      if (k < n) {
-        const int p = bcast(permv, k);
-        const double xk = bcast(b, p) * bcast(rdiag, p);
-        if (lane == k) x = xk;
-        b = fma(order < k ? -a[k] : 0.0, xk, b);
-      }
+      if (k < n) b = fma(lane < k ? -a[k] : 0.0, bcast(b, k), b);
     }
-    return x;
+    return b;
   }
 };
 
@@ -336,6 +377,14 @@ __device__ __forceinline__ double pick(const double (&v)[S], int i) {
 #pragma unroll
   for (int k = 1; k < S; ++k) r = (i == k) ? v[k] : r;
   return r;
+}
+
+// x^(1/p) for the step-size / order heuristics (eta = 1 / (BIAS * dsm)^(1/L) + ...): computed
+// with the hardware f32 log2 / exp2.  The heuristic only picks the next h; its ~1e-7 relative
+// error is far below anything the error test resolves, and it replaces an FP64 pow
+// (~200 dependent instructions) on every step.
+__device__ __forceinline__ double eta_root(double x, int p) {
+  return (double)exp2f(log2f((float)x) / (float)p);
 }
 
 // ----------------------------------------------------------------- BDF state

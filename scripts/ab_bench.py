@@ -1,0 +1,59 @@
+"""A/B timing of libckmi variants on the same GPU (alternating processes, same workload).
+
+    python scripts/ab_bench.py pychemkin_amd/_lib/libA.so pychemkin_amd/_lib/libB.so [--reps 3] [--n 16384]
+
+Each rep runs every library in its own process (CKMI_LIB=...) on a strided subsample of the
+bench sweep and reports the kernel time from HIP events; prints the per-library median.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r"""
+import os, sys, json, numpy as np
+sys.path.insert(0, %r)
+import torch, bench
+from pychemkin_amd import _native
+n = %d
+mech = bench.mechanism()
+dm = _native.DeviceMechanism(mech.to_tables(), device=0)
+T0, P0, Y0 = bench.sweep(mech, 1, 0)
+idx = np.arange(0, len(T0), max(1, len(T0) // n))[:n]
+args = (np.ones(len(idx), np.int32), T0[idx], P0[idx], np.ones(len(idx)), Y0[idx])
+cfg = _native.make_cfg(**bench.RUN)
+dm.reactor_run(cfg, *args); torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record(); res = dm.reactor_run(cfg, *args); e1.record(); torch.cuda.synchronize()
+st = res["stats"].cpu().numpy()
+print(json.dumps({"ms": e0.elapsed_time(e1), "steps": float(st[:, 0].mean()), "fail": int((st[:, 6] != 0).sum()),
+                  "tau0": float(res["tau"][0].item())}))
+"""
+
+
+def main():
+    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+    reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
+    n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 16384
+    out = {lib: [] for lib in libs}
+    for _ in range(reps):
+        for lib in libs:
+            env = dict(os.environ, CKMI_LIB=os.path.abspath(lib))
+            r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, n)], env=env, capture_output=True, text=True,
+                               timeout=300)
+            if r.returncode != 0:
+                print(r.stderr[-2000:], file=sys.stderr)
+                sys.exit(r.returncode)
+            d = json.loads(r.stdout.strip().splitlines()[-1])
+            out[lib].append(d)
+            print(os.path.basename(lib), d, flush=True)
+    summary = {os.path.basename(k): {"median_ms": sorted(x["ms"] for x in v)[len(v) // 2],
+                                     "reactors_per_s": n / (sorted(x["ms"] for x in v)[len(v) // 2] / 1e3)}
+               for k, v in out.items()}
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
