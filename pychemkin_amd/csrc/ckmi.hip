@@ -192,7 +192,10 @@ enum {
 // to oracle/ckoracle.c) is written as a wave-uniform state machine whose only RHS evaluation,
 // LU factorisation and triangular solve each appear ONCE in the loop: the LU factors of
 // M = I - gamma J then stay in VGPRs for the life of the wave without spilling.
-constexpr int RWAVES = 8;
+#ifndef CKMI_RWAVES
+#define CKMI_RWAVES 8
+#endif
+constexpr int RWAVES = CKMI_RWAVES;
 template <int N>
 __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, const ckmi_reactor_cfg* __restrict__ cfg,
                                                                int nreact, int* __restrict__ queue,
@@ -1034,6 +1037,13 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     if (slots[s] >= 0 && (type == 2 || (fl & 8))) {
       double rec[AUXW] = {lnA0[s], beta0[s], Ea0[s], fp[0 * IIp + s], fp[1 * IIp + s], fp[2 * IIp + s],
                           fp[3 * IIp + s], fp[4 * IIp + s], rlnA[s], rbeta[s], rEa[s], 0.0};
+      const int ft = (fl >> 4) & 7;
+      if (ft == CKMI_FALL_TROE3 || ft == CKMI_FALL_TROE4) {  // exp(-T / T***), exp(-T / T*): store 1/T
+        rec[4] = 1.0 / rec[4];
+        rec[5] = 1.0 / rec[5];
+      } else if (ft == CKMI_FALL_SRI) {  // exp(-T / c)
+        rec[5] = 1.0 / rec[5];
+      }
       aux.insert(aux.end(), rec, rec + AUXW);
       inf |= (uint32_t)naux << 16;
       ++naux;

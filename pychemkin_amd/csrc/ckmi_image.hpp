@@ -14,7 +14,8 @@
 //   nu        u32 [IIp]   eight 4-bit integer coefficients (reactants bits 0..15, products 16..31)
 //   info      u32 [IIp]   type:2 rev:1 hasrev:1 ftype:3 nr:3 np:3 | aux index << 16
 //   tb        i32 [IIp]   >= 0 third-body group, <= -2 single collider species -(tb+2), -1 none
-//   aux       double [naux][12]  lnA0 b0 E0/R, falloff p0..p4, REV lnA b E/R, pad
+//   aux       double [naux][12]  lnA0 b0 E0/R, falloff parameters (TROE: a, 1/T***, 1/T*, T**;
+//                                SRI: a, b, 1/c, d, e), REV lnA b E/R, pad
 //   gptr i32 [G+1], gsp i32 [ng], geff double [ng]   third-body efficiency lists (eff - 1)
 //   geffd double [G][KKp]   the same lists dense (eff - 1, 0 for unlisted species)
 #pragma once
@@ -109,13 +110,13 @@ __device__ __forceinline__ int sp_of(uint32_t packed, int u) { return (packed >>
 __device__ __forceinline__ int nur_of(uint32_t nu, int u) { return (nu >> (4 * u)) & 0xf; }
 __device__ __forceinline__ int nup_of(uint32_t nu, int u) { return (nu >> (16 + 4 * u)) & 0xf; }
 
-// C^nu for a small non-negative integer nu
+// C^nu for a small non-negative integer nu, branch-free for nu <= 3
 __device__ __forceinline__ double powi(double c, int nu) {
-  if (nu == 1) return c;
-  if (nu == 2) return c * c;
-  if (nu == 0) return 1.0;
-  double r = c * c * c;
-  for (int k = 3; k < nu; ++k) r *= c;
+  double r = nu >= 1 ? c : 1.0;
+  r *= nu >= 2 ? c : 1.0;
+  r *= nu >= 3 ? c : 1.0;
+  if (nu > 3)
+    for (int k = 3; k < nu; ++k) r *= c;
   return r;
 }
 
@@ -151,10 +152,11 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
                                             uint32_t nuw, double T, double lnT, double invT, double lnPRT,
                                             const double* C, const double* gRT, const double* hRT, const double* Mg,
                                             bool need_h) {
+  constexpr double INV_LN10 = 0.43429448190325176;
   const int type = rx_type(inf);
-  const int nr = rx_nr(inf), np = rx_np(inf);
   const double lnA = V.lnA()[i], b = V.beta()[i], Ea = V.Ea()[i];
-  const double kf_inf = exp(lnA + b * lnT - Ea * invT);
+  const double lnkinf = lnA + b * lnT - Ea * invT;
+  const double kf_inf = exp(lnkinf);
   double kf = kf_inf;
   const double dlkf = (b + Ea * invT) * invT;
   double mfac = 1.0;
@@ -165,28 +167,30 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
     if (type == 1) {
       mfac = Mc;
     } else {
-      const double k0 = exp(ax[0] + ax[1] * lnT - ax[2] * invT);
-      const double Pr = k0 * Mc / kf;
+      // Pr = k0 [M] / k_inf from the Arrhenius exponents (one exp, no division)
+      const double lnPr = ax[0] + ax[1] * lnT - ax[2] * invT - lnkinf + log(Mc > 1e-300 ? Mc : 1e-300);
+      const double Pr = exp(lnPr);
+      const double lPr = fmax(lnPr * INV_LN10, -300.0);  // log10(max(Pr, 1e-300))
       double F = 1.0;
       const int ft = rx_ftype(inf);
       if (ft == 2 || ft == 3) {
-        const double fa = ax[3], T3s = ax[4], T1s = ax[5];
-        double Fcent = (1.0 - fa) * exp(-T / T3s) + fa * exp(-T / T1s);
+        const double fa = ax[3];
+        double Fcent = (1.0 - fa) * exp(-T * ax[4]) + fa * exp(-T * ax[5]);
         if (ft == 3) Fcent += exp(-ax[6] * invT);
-        const double lFc = log10(Fcent > 1e-300 ? Fcent : 1e-300);
-        const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
+        const double lnFc = log(Fcent > 1e-300 ? Fcent : 1e-300);
+        const double lFc = lnFc * INV_LN10;
         const double c = -0.4 - 0.67 * lFc, nn = 0.75 - 1.27 * lFc;
         const double f1 = (lPr + c) / (nn - 0.14 * (lPr + c));
-        F = exp10(lFc / (1.0 + f1 * f1));
+        F = exp(lnFc / (1.0 + f1 * f1));  // 10^(log10 Fcent / (1 + f1^2))
       } else if (ft == 4) {
-        const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
         const double X = 1.0 / (1.0 + lPr * lPr);
-        F = ax[6] * pow(ax[3] * exp(-ax[4] * invT) + exp(-T / ax[5]), X) * pow(T, ax[7]);
+        F = ax[6] * pow(ax[3] * exp(-ax[4] * invT) + exp(-T * ax[5]), X) * pow(T, ax[7]);
       }
-      kf = kf * (Pr / (1.0 + Pr)) * F;
+      kf = kf_inf * (Pr / (1.0 + Pr)) * F;
     }
   }
   double kr = 0.0, dlkr = 0.0;
+  const int nr = rx_nr(inf), np = rx_np(inf);
   if (rx_rev(inf)) {
     if (rx_hasrev(inf)) {
       kr = exp(ax[8] + ax[9] * lnT - ax[10] * invT);
