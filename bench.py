@@ -38,6 +38,21 @@ from pychemkin_amd.perf import count_ops, reactor_flops  # noqa: E402
 P_ATM = 1.01325e6
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak, MI355X_MICROARCH.md / SURVEY 8d
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak
+# HBM traffic per launch from rocprofv3 PMC passes of this same bench workload (FETCH_SIZE x2 per the
+# gfx950 calibration + WRITE_SIZE; scripts/pmc_traffic.sh -> scripts/traffic_summary.py)
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def load_traffic(kernel: str, units: int):
+    """Measured HBM bytes per launch of `kernel` for a launch of `units` units, or None."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)[kernel]
+    except (OSError, KeyError, ValueError):
+        return None
+    if int(t.get("units", -1)) != int(units):
+        return None
+    return float(t["bytes_per_launch"])
 
 
 def mechanism():
@@ -178,7 +193,7 @@ def main():
                 "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": ops["F_rop"] * ns / sec / 1e12 / FP64_PEAK_TFLOPS,
                 "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "hbm_frac": ops["bytes_rop"] * ns / sec / 1e9 / HBM_PEAK_GBS,
-                "traffic": None,
+                "traffic": load_traffic("rop", ns),
             },
         }
         del Ts, Ps, Ys, wdot, cp, hh
@@ -234,7 +249,7 @@ def main():
                        "mean_newton": float(stats[:, 7].mean())},
             "roofline": {"bound": "mfma", "pipe": "fp64-valu", "kernel": "reactor_kernel<54>",
                          "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
+                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": load_traffic("reactor", n),
                          "flops_per_launch": flops, "kernel_ms": kern_s * 1e3},
             "cpu_baseline": cpu,
             "rop": rop,

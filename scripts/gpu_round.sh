@@ -32,9 +32,13 @@ if [[ $STEPS == all || $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   echo "== rocprofv3 kernel trace"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv rocpd -d gpurun_out/prof_$TAG -o run -- \
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- \
     python3 bench.py --steps 2 --warmup 1 --cpu-sample 0 > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/bench_prof_$TAG.err
   rc=$?; cat gpurun_out/bench_prof_$TAG.json; tail -5 gpurun_out/bench_prof_$TAG.err; stop_unless_ok $rc rocprofv3
   find gpurun_out/prof_$TAG -name "*stats*"
+fi
+if [[ $STEPS == all || $STEPS == *traffic* ]]; then
+  echo "== PMC traffic"
+  bash scripts/pmc_traffic.sh $TAG; stop_unless_ok $? traffic
 fi
 echo "== done"
