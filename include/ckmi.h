@@ -98,10 +98,38 @@ typedef struct {
   int32_t ign_species; /* KLIM species index */
   int32_t ign_stop;    /* IGN_STOP */
   int32_t max_steps;   /* 0 = 200000 */
-  int32_t nprof;       /* VPRO (CONV) / PPRO (CONP) profile points, 0 = none (<= 64) */
+  int32_t nprof;       /* VPRO (CONV) / PPRO (CONP) / TPRO profile points, 0 = none (<= 64) */
   double prof_t[64];
   double prof_v[64];
+  int32_t prof_kind;   /* 0: the profile is VPRO (CONV) or PPRO (CONP); 1: TPRO (energy = 2) */
+  double gfac;         /* GFAC gas-phase rate multiplier (reactormodel.py:1452-1468); 0 is read as 1 */
+  double qloss;        /* QLOS heat loss rate to the surroundings [cal/s] (batchreactor.py:1884-1907) */
+  double htc;          /* HTC wall heat-transfer coefficient [cal/cm2-K-s] (:1910-1939) */
+  double areaq;        /* AREAQ heat-transfer area [cm2] (:1974-2003) */
+  double tamb;         /* TAMB ambient temperature [K] (:1942-1971) */
+  int32_t asteps;      /* ADAP/ASTEPS: extra solution point every asteps steps, 0 = off (:373-460) */
+  int32_t avar;        /* ADAP/AVAR: extra point when variable avar changed by avalue since the last
+                          one; -1 off, 0 temperature, 1 + k mass fraction of species k */
+  double avalue;       /* AVALUE */
+  int32_t nprof2;      /* second profile (energy runs), 0 = none (<= 64): */
+  int32_t prof2_kind;  /* 1 QPRO heat loss rate [cal/s] (replaces QLOS), 2 AEXT area [cm2] (replaces AREAQ) */
+  double prof2_t[64];
+  double prof2_v[64];
 } ckmi_reactor_cfg;
+
+/* Optional per-reactor inputs / outputs of ckmi_reactor_run_ex (any pointer may be NULL). */
+typedef struct {
+  /* brute-force A-factor sensitivity (sensitivity.py:141-160, chemistry.py:1636-1678): reactor r
+   * runs with the pre-exponential factor of reaction afac_rxn[r] (0-based, original order;
+   * < 0 = none) multiplied by afac[r]. */
+  const int32_t* afac_rxn; /* [n] device */
+  const double* afac;      /* [n] device */
+  /* adaptive solution points (cfg.asteps > 0): up to max_adap per reactor */
+  int32_t max_adap;
+  double* t_adap;          /* [n][max_adap] device */
+  double* y_adap;          /* [n][max_adap][KK+1] device (T, Y) */
+  int32_t* n_adap;         /* [n] device: points written */
+} ckmi_reactor_ext;
 
 /* per-reactor statistics written by ckmi_reactor_run (int32 [n][8]) */
 #define CKMI_STAT_NST 0
@@ -158,6 +186,14 @@ int ckmi_reactor_run(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int32_t
                      const double* T0, const double* P0, const double* V0, const double* Y0, double* tau,
                      double* Tend, double* Pend, double* Vend, double* Yend, int32_t* stats, int32_t nsave,
                      const double* t_save, double* y_save, void* stream);
+
+/* ckmi_reactor_run plus the optional per-reactor inputs / outputs of `ext` (NULL = none):
+ * the batched form of the reference's A-factor sensitivity loop and of adaptive saving. */
+int ckmi_reactor_run_ex(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int32_t n, const int32_t* problem,
+                        const double* T0, const double* P0, const double* V0, const double* Y0,
+                        const ckmi_reactor_ext* ext, double* tau, double* Tend, double* Pend, double* Vend,
+                        double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -49,9 +49,9 @@ typedef struct {
 } rxn_eval;
 
 static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, double lnPRT, const double* C,
-                          double Ctot, const double* g_RT, const double* h_RT, rxn_eval* e) {
+                          double Ctot, const double* g_RT, const double* h_RT, double dlnA, double gfac, rxn_eval* e) {
   const double* a = m->arr + 3 * i;
-  double kf = exp(a[0] + a[1] * lnT - a[2] * invT);
+  double kf = exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
   double dlkf = (a[1] + a[2] * invT) * invT;
   double mfac = 1.0;
   const int type = m->rtype[i];
@@ -93,7 +93,7 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
     if (m->has_rev[i]) {
       const double* r = m->revp + 3 * i;
       kr = exp(r[0] + r[1] * lnT - r[2] * invT);
-      if (type == 2) kr *= kf / exp(a[0] + a[1] * lnT - a[2] * invT);
+      if (type == 2) kr *= kf / exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
       dlkr = (r[1] + r[2] * invT) * invT;
     } else {
       double dG = 0.0, dH = 0.0, dnu = 0.0;
@@ -115,7 +115,8 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
   double pf = 1.0, pr = 1.0;
   for (int s = 0; s < m->nr[i]; ++s) pf *= powi_nu(C[m->rsp[CKO_SLOTS * i + s]], m->rnu[CKO_SLOTS * i + s]);
   for (int s = 0; s < m->np[i]; ++s) pr *= powi_nu(C[m->psp[CKO_SLOTS * i + s]], m->pnu[CKO_SLOTS * i + s]);
-  e->kf = kf; e->kr = kr; e->mfac = mfac; e->pf = pf; e->pr = pr; e->dlkf = dlkf; e->dlkr = dlkr;
+  /* GFAC scales forward and reverse rates alike */
+  e->kf = kf * gfac; e->kr = kr * gfac; e->mfac = mfac; e->pf = pf; e->pr = pr; e->dlkf = dlkf; e->dlkr = dlkr;
 }
 
 static void conc_from_Y(const cko_mech* m, double rho, const double* Y, int nneg, double* C, double* Ctot) {
@@ -146,7 +147,7 @@ void cko_rates(const cko_mech* m, double T, double P, const double* Y, double* q
   const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   for (int i = 0; i < m->II; ++i) {
     rxn_eval e;
-    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, &e);
+    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, 0.0, 1.0, &e);
     double f = e.mfac * e.kf * e.pf, r = e.mfac * e.kr * e.pr;
     if (qf) qf[i] = f;
     if (qr) qr[i] = r;
@@ -190,38 +191,55 @@ typedef struct {
   double mass_density0; /* rho0 (CONV: density at V0) */
   double V0, P0, T0;
   int nfe, nje;
+  double tsel; /* midpoint of the current integration segment (pwl_eval) */
 } rctx;
 
-static void profile_eval(const cko_cfg* c, double t, double base, double* v, double* dvdt) {
-  if (c->nprof <= 0) { *v = base; *dvdt = 0.0; return; }
-  const double* x = c->prof_t;
-  const double* y = c->prof_v;
-  int n = c->nprof;
-  if (t <= x[0]) { *v = y[0]; *dvdt = 0.0; return; }
-  if (t >= x[n - 1]) { *v = y[n - 1]; *dvdt = 0.0; return; }
+/* piecewise-linear profile at t; the linear piece is the one containing tsel, the midpoint of
+ * the current integration segment (segments end at every breakpoint), so a step ending on a
+ * breakpoint uses the left slope and the first step after the restart the right one */
+static void pwl_eval(const double* x, const double* y, int n, double t, double tsel, double* v, double* dvdt) {
+  if (tsel <= x[0]) { *v = y[0]; *dvdt = 0.0; return; }
+  if (tsel >= x[n - 1]) { *v = y[n - 1]; *dvdt = 0.0; return; }
   int j = 0;
-  while (j < n - 2 && t >= x[j + 1]) ++j;
+  while (j < n - 2 && tsel >= x[j + 1]) ++j;
   double s = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
   *v = y[j] + s * (t - x[j]);
   *dvdt = s;
 }
 
+static void profile_eval(const cko_cfg* c, double t, double tsel, double base, double* v, double* dvdt) {
+  if (c->nprof <= 0 || c->prof_kind != 0) { *v = base; *dvdt = 0.0; return; }
+  pwl_eval(c->prof_t, c->prof_v, c->nprof, t, tsel, v, dvdt);
+}
+
 /* f = dy/dt for y = (T, Y_1..Y_KK); J (n x n row-major, optional) = approximate analytic Jacobian */
+#define ERG_PER_CAL 4.184e7
+
+static double prof2_value(const cko_cfg* c, double t, double tsel, double base, int kind) {
+  if (c->nprof2 <= 0 || c->prof2_kind != kind) return base;
+  double v, d;
+  pwl_eval(c->prof2_t, c->prof2_v, c->nprof2, t, tsel, &v, &d);
+  return v;
+}
+
 static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J) {
   const cko_mech* m = c->m;
   const int KK = m->KK, n = KK + 1;
-  const double T = y[0];
+  double T = y[0], dTdt_given = 0.0;
+  const int tpro = c->cfg->prof_kind == 1 && c->cfg->energy == 2 && c->cfg->nprof > 0;
+  if (tpro) pwl_eval(c->cfg->prof_t, c->cfg->prof_v, c->cfg->nprof, t, c->tsel, &T, &dTdt_given);
+  const double dlnA_p = c->cfg->pert_rxn >= 0 ? log(c->cfg->pert_fac) : 0.0;
   const double* Y = y + 1;
   double C[NMAX], cp_R[NMAX], h_RT[NMAX], s_R[NMAX], g_RT[NMAX], Ctot;
   double rho, P, V, dVdt = 0.0, dPdt = 0.0;
   const int conp = (c->problem == 1);
   double Wbar = mean_wt(m, Y);
   if (conp) {
-    profile_eval(c->cfg, t, c->P0, &P, &dPdt);
+    profile_eval(c->cfg, t, c->tsel, c->P0, &P, &dPdt);
     rho = P * Wbar / (RU * T);
     V = c->mass_density0 * c->V0 / rho;
   } else {
-    profile_eval(c->cfg, t, c->V0, &V, &dVdt);
+    profile_eval(c->cfg, t, c->tsel, c->V0, &V, &dVdt);
     rho = c->mass_density0 * c->V0 / V;
     P = rho * RU * T / Wbar;
   }
@@ -238,7 +256,8 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
   const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   for (int i = 0; i < m->II; ++i) {
     rxn_eval e;
-    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, &e);
+    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, i == c->cfg->pert_rxn ? dlnA_p : 0.0,
+                  c->cfg->gfac, &e);
     const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
     const int* rs = m->rsp + CKO_SLOTS * i;
     const int* ps = m->psp + CKO_SLOTS * i;
@@ -294,6 +313,12 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
     double fT = -sum / cpm;
     if (conp) fT += dPdt / (rho * cpm);
     else fT -= P * dVdt / (V * rho * cpm);
+    /* heat loss to the surroundings: QLOS + HTC AREAQ (T - TAMB) [cal/s], per heat capacity m cp */
+    const double mcp = c->mass_density0 * c->V0 * cpm;
+    const double qloss = prof2_value(c->cfg, t, c->tsel, c->cfg->qloss, 1);
+    const double area = prof2_value(c->cfg, t, c->tsel, c->cfg->areaq, 2);
+    const double q1 = c->cfg->htc * area * ERG_PER_CAL;
+    fT -= (qloss * ERG_PER_CAL + q1 * (T - c->cfg->tamb)) / mcp;
     f[0] = fT;
     if (J) {
       for (int k = 0; k < KK; ++k) J[(1 + k) * n] = dwdT[k] * m->wt[k] * rinv + (conp ? f[1 + k] * invT : 0.0);
@@ -304,10 +329,10 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
       }
       double s = 0.0;
       for (int k = 0; k < KK; ++k) s += c_k[k] * f[1 + k] + e_k[k] * J[(1 + k) * n];
-      J[0] = -s / cpm;
+      J[0] = -s / cpm - q1 / mcp;
     }
   } else {
-    f[0] = 0.0;
+    f[0] = dTdt_given; /* 0 without TPRO */
     if (J) {
       for (int k = 0; k < KK; ++k) J[(1 + k) * n] = dwdT[k] * m->wt[k] * rinv + (conp ? f[1 + k] * invT : 0.0);
     }
@@ -318,7 +343,7 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
 
 void cko_rhs_jac(const cko_mech* m, const cko_cfg* cfg, double t, const double* y, double mass_density0,
                  double V0, double P0, double* f, double* J) {
-  rctx c = {m, cfg, cfg->problem, mass_density0, V0, P0, y[0], 0, 0};
+  rctx c = {m, cfg, cfg->problem, mass_density0, V0, P0, y[0], 0, 0, t};
   reactor_rhs(&c, t, y, f, J);
 }
 
@@ -877,6 +902,7 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
                 double* Yend, cko_result* res, int nsave, const double* t_save, double* y_save, double* p_save,
                 double* v_save) {
   const int KK = m->KK, n = KK + 1;
+  if (cfg->prof_kind == 1 && cfg->energy == 2 && cfg->nprof > 0) T0 = cfg->prof_v[0]; /* TPRO start */
   bdf* b = (bdf*)calloc(1, sizeof(bdf));
   b->J = (double*)calloc((size_t)n * n, sizeof(double));
   b->M = (double*)calloc((size_t)n * n, sizeof(double));
@@ -887,9 +913,9 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   const double Wbar0 = mean_wt(m, Y0);
   const double rho0 = P0 * Wbar0 / (RU * T0);
   double Vstart = V0;
-  if (cfg->problem == 2 && cfg->nprof > 0) Vstart = cfg->prof_v[0];
+  if (cfg->problem == 2 && cfg->nprof > 0 && cfg->prof_kind == 0) Vstart = cfg->prof_v[0];
   rctx ctx = {m, cfg, cfg->problem, rho0, Vstart, P0, T0, 0, 0};
-  if (cfg->problem == 1 && cfg->nprof > 0) ctx.P0 = cfg->prof_v[0];
+  if (cfg->problem == 1 && cfg->nprof > 0 && cfg->prof_kind == 0) ctx.P0 = cfg->prof_v[0];
   b->ctx = &ctx;
   const double tend = cfg->t_end;
   const double hmax = cfg->hmax > 0.0 ? cfg->hmax : tend / 100.0;
@@ -899,12 +925,26 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   y[0] = T0;
   for (int k = 0; k < KK; ++k) y[1 + k] = Y0[k];
   /* profile breakpoints are integration stop points (derivative discontinuities) */
-  double tcrit[64];
+  double tcrit[130];
   int ncrit = 0;
-  for (int i = 0; i < cfg->nprof && ncrit < 63; ++i)
+  for (int i = 0; i < cfg->nprof && ncrit < 64; ++i)
     if (cfg->prof_t[i] > 0.0 && cfg->prof_t[i] < tend) tcrit[ncrit++] = cfg->prof_t[i];
+  for (int i = 0; i < cfg->nprof2 && ncrit < 128; ++i)
+    if (cfg->prof2_t[i] > 0.0 && cfg->prof2_t[i] < tend) tcrit[ncrit++] = cfg->prof2_t[i];
+  /* sorted union of both profiles' breakpoints */
+  for (int i = 1; i < ncrit; ++i)
+    for (int j = i; j > 0 && tcrit[j - 1] > tcrit[j]; --j) {
+      const double tmp = tcrit[j]; tcrit[j] = tcrit[j - 1]; tcrit[j - 1] = tmp;
+    }
+  {
+    int u = 0;
+    for (int i = 0; i < ncrit; ++i)
+      if (u == 0 || tcrit[i] != tcrit[u - 1]) tcrit[u++] = tcrit[i];
+    ncrit = u;
+  }
   tcrit[ncrit++] = tend;
   int icrit = 0;
+  ctx.tsel = 0.5 * tcrit[0];
   bdf_start(b, 0.0, y, tcrit[0], cfg->h0, hmax);
   ignmon g;
   ign_init(&g, cfg, T0);
@@ -949,11 +989,11 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
       for (int i = 0; i < n; ++i) y_save[(size_t)isave * n + i] = ys[i];
       double Wb = mean_wt(m, ys + 1), rho, P, V, d;
       if (cfg->problem == 1) {
-        profile_eval(cfg, t_save[isave], ctx.P0, &P, &d);
+        profile_eval(cfg, t_save[isave], t_save[isave], ctx.P0, &P, &d);
         rho = P * Wb / (RU * ys[0]);
         V = rho0 * Vstart / rho;
       } else {
-        profile_eval(cfg, t_save[isave], Vstart, &V, &d);
+        profile_eval(cfg, t_save[isave], t_save[isave], Vstart, &V, &d);
         rho = rho0 * Vstart / V;
         P = rho * RU * ys[0] / Wb;
       }
@@ -988,6 +1028,7 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
       for (int i = 0; i < n; ++i) yc[i] = b->zn[0][i];
       icrit++;
       const int nlu = b->nlu, ncf = b->ncf_tot, nef = b->nef_tot;
+      ctx.tsel = 0.5 * (tn + tcrit[icrit]);
       bdf_start(b, tn, yc, tcrit[icrit], 0.0, hmax);
       b->nlu = nlu; b->ncf_tot = ncf; b->nef_tot = nef;
     }
@@ -1009,10 +1050,10 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
     res->T = yf[0];
     double Wb = mean_wt(m, yf + 1), d;
     if (cfg->problem == 1) {
-      profile_eval(cfg, tf, ctx.P0, &res->P, &d);
+      profile_eval(cfg, tf, tf, ctx.P0, &res->P, &d);
       res->V = rho0 * Vstart / (res->P * Wb / (RU * yf[0]));
     } else {
-      profile_eval(cfg, tf, Vstart, &res->V, &d);
+      profile_eval(cfg, tf, tf, Vstart, &res->V, &d);
       res->P = (rho0 * Vstart / res->V) * RU * yf[0] / Wb;
     }
     res->status = status;
@@ -1043,6 +1084,29 @@ int cko_reactor_batch(const cko_mech* m, const cko_cfg* cfg, int n, const int* p
   for (int i = 0; i < n; ++i) {
     cko_cfg c = *cfg;
     if (problem) c.problem = problem[i];
+    int r = cko_reactor(m, &c, T0[i], P0[i], V0 ? V0[i] : 1.0, Y0 + (size_t)i * KK, Yend + (size_t)i * KK,
+                        res + i, 0, NULL, NULL, NULL, NULL);
+    if (r) nfail++;
+  }
+  return nfail;
+}
+
+int cko_reactor_batch_pert(const cko_mech* m, const cko_cfg* cfg, int n, const int* problem, const double* T0,
+                           const double* P0, const double* V0, const double* Y0, const int* pert_rxn,
+                           const double* pert_fac, double* Yend, cko_result* res, int nthreads) {
+  const int KK = m->KK;
+  int nfail = 0;
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : nfail)
+#endif
+  for (int i = 0; i < n; ++i) {
+    cko_cfg c = *cfg;
+    if (problem) c.problem = problem[i];
+    if (pert_rxn) {
+      c.pert_rxn = pert_rxn[i];
+      c.pert_fac = pert_fac[i];
+    }
     int r = cko_reactor(m, &c, T0[i], P0[i], V0 ? V0[i] : 1.0, Y0 + (size_t)i * KK, Yend + (size_t)i * KK,
                         res + i, 0, NULL, NULL, NULL, NULL);
     if (r) nfail++;

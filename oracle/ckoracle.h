@@ -55,6 +55,18 @@ typedef struct {
   int nprof;        /* volume (CONV) or pressure (CONP) profile points, 0 = none */
   const double* prof_t;
   const double* prof_v;
+  int prof_kind;    /* 0 VPRO/PPRO, 1 TPRO (energy = 2): T(t) given by the profile */
+  double gfac;      /* GFAC: all gas rates x gfac */
+  double qloss;     /* QLOS [cal/s] */
+  double htc;       /* HTC [cal/cm2-K-s] */
+  double areaq;     /* AREAQ [cm2] */
+  double tamb;      /* TAMB [K] */
+  int pert_rxn;     /* reaction whose A factor is multiplied by pert_fac (-1 none) */
+  double pert_fac;
+  int nprof2;       /* second profile: QPRO [cal/s] (prof2_kind 1) or AEXT [cm2] (2), energy runs */
+  int prof2_kind;
+  const double* prof2_t;
+  const double* prof2_v;
 } cko_cfg;
 
 typedef struct {
@@ -79,6 +91,10 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
 int cko_reactor_batch(const cko_mech* m, const cko_cfg* cfg, int n, const int* problem, const double* T0,
                       const double* P0, const double* V0, const double* Y0, double* Yend,
                       cko_result* res, int nthreads);
+/* batch with a per-reactor A-factor perturbation (brute-force sensitivity) */
+int cko_reactor_batch_pert(const cko_mech* m, const cko_cfg* cfg, int n, const int* problem, const double* T0,
+                           const double* P0, const double* V0, const double* Y0, const int* pert_rxn,
+                           const double* pert_fac, double* Yend, cko_result* res, int nthreads);
 /* dense analytic Jacobian of the batch-reactor RHS (for tests) */
 void cko_rhs_jac(const cko_mech* m, const cko_cfg* cfg, double t, const double* y, double mass_density0,
                  double V0, double P0, double* f, double* J);

@@ -47,7 +47,16 @@ class ReactorCfg(ct.Structure):
         ("h0", ct.c_double), ("hmax", ct.c_double), ("nneg", ct.c_int32), ("ign_mode", ct.c_int32),
         ("ign_val", ct.c_double), ("ign_species", ct.c_int32), ("ign_stop", ct.c_int32), ("max_steps", ct.c_int32),
         ("nprof", ct.c_int32), ("prof_t", ct.c_double * 64), ("prof_v", ct.c_double * 64),
+        ("prof_kind", ct.c_int32), ("gfac", ct.c_double), ("qloss", ct.c_double), ("htc", ct.c_double),
+        ("areaq", ct.c_double), ("tamb", ct.c_double), ("asteps", ct.c_int32), ("avar", ct.c_int32),
+        ("avalue", ct.c_double), ("nprof2", ct.c_int32), ("prof2_kind", ct.c_int32), ("prof2_t", ct.c_double * 64),
+        ("prof2_v", ct.c_double * 64),
     ]
+
+
+class ReactorExt(ct.Structure):
+    _fields_ = [("afac_rxn", _P), ("afac", _P), ("max_adap", ct.c_int32), ("t_adap", _P), ("y_adap", _P),
+                ("n_adap", _P)]
 
 
 _lib: Optional[ct.CDLL] = None
@@ -66,6 +75,8 @@ PROTOTYPES = {
     "ckmi_reaction_rates": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P, _P, _P]),
     "ckmi_reactor_run": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, ct.c_int32, _P, _P, _P]),
+    "ckmi_reactor_run_ex": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P,
+                                        ct.POINTER(ReactorExt), _P, _P, _P, _P, _P, _P, ct.c_int32, _P, _P, _P]),
 }
 
 
@@ -108,8 +119,27 @@ IGN_MODES = {None: 0, "none": 0, "T_inflection": 1, "TIFP": 1, "T_rise": 2, "DTI
 
 def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: float = 1e-6, h0: float = 0.0,
              hmax: float = 0.0, nneg: bool = False, ign_mode=None, ign_val: float = 0.0, ign_species: int = 0,
-             ign_stop: bool = False, max_steps: int = 0, profile=None) -> ReactorCfg:
+             ign_stop: bool = False, max_steps: int = 0, profile=None, prof_kind: int = 0, gfac: float = 1.0,
+             qloss: float = 0.0, htc: float = 0.0, areaq: float = 0.0, tamb: float = 300.0,
+             asteps: int = 0, avar: int = -1, avalue: float = 0.0, profile2=None, prof2_kind: int = 0) -> ReactorCfg:
+    """Typed form of the reactor keywords (see include/ckmi.h ckmi_reactor_cfg).
+
+    profile: (x, v) VPRO/PPRO (prof_kind 0) or TPRO (prof_kind 1); profile2: (x, v) QPRO
+    (prof2_kind 1) or AEXT (prof2_kind 2)."""
     c = ReactorCfg()
+    c.avar, c.avalue = int(avar), float(avalue)
+    c.nprof2, c.prof2_kind = 0, int(prof2_kind)
+    if profile2 is not None:
+        x2, v2 = np.asarray(profile2[0], np.float64), np.asarray(profile2[1], np.float64)
+        if len(x2) != len(v2) or len(x2) > 64 or len(x2) == 0:
+            raise ValueError("profile2 must have matching lengths in [1, 64]")
+        c.nprof2 = len(x2)
+        for i in range(len(x2)):
+            c.prof2_t[i] = x2[i]
+            c.prof2_v[i] = v2[i]
+    c.prof_kind, c.gfac, c.qloss, c.htc, c.areaq, c.tamb = int(prof_kind), float(gfac), float(qloss), float(htc), \
+        float(areaq), float(tamb)
+    c.asteps = int(asteps)
     c.energy, c.t_end, c.atol, c.rtol = int(energy), float(t_end), float(atol), float(rtol)
     c.h0, c.hmax, c.nneg = float(h0), float(hmax), int(bool(nneg))
     c.ign_mode = IGN_MODES[ign_mode] if not isinstance(ign_mode, int) else int(ign_mode)
@@ -215,8 +245,13 @@ class DeviceMechanism:
                                          _stream_ptr(self.device)), "ckmi_reaction_rates")
         return qf, qr
 
-    def reactor_run(self, cfg: ReactorCfg, problem, T0, P0, V0, Y0, t_save=None, out=None):
-        """Integrate n independent reactors. Y0 is [n][KK]. Returns a dict of device tensors."""
+    def reactor_run(self, cfg: ReactorCfg, problem, T0, P0, V0, Y0, t_save=None, out=None, afac_rxn=None, afac=None,
+                    max_adap: int = 0):
+        """Integrate n independent reactors. Y0 is [n][KK]. Returns a dict of device tensors.
+
+        afac_rxn / afac: per-reactor A-factor perturbation (reaction index, multiplier), the
+        batched form of the reference's sensitivity loop (sensitivity.py:141-160).
+        max_adap > 0 with cfg.asteps > 0: adaptive solution points (t_adap, y_adap, n_adap)."""
         if not isinstance(problem, torch.Tensor):
             pv = np.asarray(problem)
             if pv.size and not np.all((pv == 1) | (pv == 2)):
@@ -244,10 +279,32 @@ class DeviceMechanism:
             ts = self._dev(t_save).reshape(-1)
             nsave = ts.numel()
             ys = torch.empty((n, nsave, self.KK + 1), **f64)
-        _check(lib().ckmi_reactor_run(self._h, ct.byref(cfg), n, _ptr(prob), _ptr(T0), _ptr(P0), _ptr(V0), _ptr(Y0),
-                                      _ptr(tau), _ptr(Tend), _ptr(Pend), _ptr(Vend), _ptr(Yend), _ptr(stats), nsave,
-                                      _ptr(ts), _ptr(ys), _stream_ptr(dev)), "ckmi_reactor_run")
+        ext = ReactorExt()
+        keep = []
+        if afac_rxn is not None:
+            ar = self._dev(afac_rxn, torch.int32).reshape(-1)
+            af = self._dev(afac).reshape(-1)
+            if ar.numel() != n or af.numel() != n:
+                raise ValueError("afac_rxn and afac must have n entries")
+            if bool((af <= 0).any()):
+                raise NativeError("A-factor multipliers must be > 0")
+            ext.afac_rxn, ext.afac = _ptr(ar), _ptr(af)
+            keep += [ar, af]
+        adap = None
+        if max_adap > 0:
+            adap = dict(t_adap=torch.zeros((n, max_adap), **f64), y_adap=torch.zeros((n, max_adap, self.KK + 1), **f64),
+                        n_adap=torch.zeros(n, dtype=torch.int32, device=dev))
+            ext.max_adap = int(max_adap)
+            ext.t_adap, ext.y_adap, ext.n_adap = _ptr(adap["t_adap"]), _ptr(adap["y_adap"]), _ptr(adap["n_adap"])
+        _check(lib().ckmi_reactor_run_ex(self._h, ct.byref(cfg), n, _ptr(prob), _ptr(T0), _ptr(P0), _ptr(V0),
+                                         _ptr(Y0), ct.byref(ext), _ptr(tau), _ptr(Tend), _ptr(Pend), _ptr(Vend),
+                                         _ptr(Yend), _ptr(stats), nsave, _ptr(ts), _ptr(ys), _stream_ptr(dev)),
+               "ckmi_reactor_run_ex")
         res = dict(tau=tau, T=Tend, P=Pend, V=Vend, Y=Yend, stats=stats)
+        if adap is not None:
+            res.update(adap)
+        if keep:
+            torch.cuda.current_stream(dev).synchronize()
         if ys is not None:
             res["t_save"] = ts
             res["y_save"] = ys

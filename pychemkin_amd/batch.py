@@ -55,14 +55,18 @@ class BatchSweep:
     def __init__(self, chem: Chemistry, problem="CONP", energy="ENERGY", t_end: float = 1.0, atol: float = 1.0e-12,
                  rtol: float = 1.0e-6, ignition: Optional[str] = "T_inflection", ign_val: float = 0.0,
                  ign_target: str = "", nneg: bool = False, h0: float = 0.0, hmax: float = 0.0,
-                 ign_stop: bool = False, profile=None, max_steps: int = 0, devices: Optional[Sequence[int]] = None):
+                 ign_stop: bool = False, profile=None, max_steps: int = 0, devices: Optional[Sequence[int]] = None,
+                 **keywords):
+        """keywords: the remaining typed reactor keywords of _native.make_cfg -- gfac (GFAC), qloss (QLOS,
+        cal/s), htc (HTC), areaq (AREAQ), tamb (TAMB), prof_kind (1: `profile` is TPRO), profile2 /
+        prof2_kind (QPRO / AEXT), asteps / avar / avalue (adaptive solution points)."""
         self.chem = chem
         self.problem = PROBLEMS[problem]
         sp = chem.get_specindex(ign_target) if ignition == "Species_peak" else 0
         self.cfg = _native.make_cfg(energy=ENERGIES[energy], t_end=t_end, atol=max(atol, 1e-20),
                                     rtol=max(rtol, 1e-12), h0=h0, hmax=hmax, nneg=nneg, ign_mode=ignition,
                                     ign_val=ign_val, ign_species=sp, ign_stop=ign_stop, max_steps=max_steps,
-                                    profile=profile)
+                                    profile=profile, **keywords)
         self.devices = list(devices) if devices is not None else None
 
     def _devices(self) -> List[int]:
@@ -72,8 +76,11 @@ class BatchSweep:
             return self.devices
         return list(range(torch.cuda.device_count()))
 
-    def run(self, T0, P0, X0=None, Y0=None, V0=None, problem=None) -> BatchResult:
-        """Integrate reactors i = 0..n-1 from (T0[i], P0[i], X0[i] or Y0[i], V0[i])."""
+    def run(self, T0, P0, X0=None, Y0=None, V0=None, problem=None, afac_rxn=None, afac=None) -> BatchResult:
+        """Integrate reactors i = 0..n-1 from (T0[i], P0[i], X0[i] or Y0[i], V0[i]).
+
+        afac_rxn[i] / afac[i]: reactor i runs with the A factor of reaction afac_rxn[i] (0-based,
+        -1 none) multiplied by afac[i] -- the batched form of set_reaction_AFactor + run()."""
         import torch
 
         T0 = np.asarray(T0, dtype=np.float64).reshape(-1)
@@ -102,8 +109,12 @@ class BatchSweep:
             if idx.size == 0:
                 continue
             dm = self.chem.device_mechanism(d)
+            pert = {}
+            if afac_rxn is not None:
+                pert = dict(afac_rxn=np.asarray(afac_rxn, np.int32).reshape(-1)[idx],
+                            afac=np.broadcast_to(np.asarray(afac, np.float64), (n,))[idx])
             with torch.cuda.device(d):
-                res = dm.reactor_run(self.cfg, prob[idx], T0[idx], P0[idx], V0[idx], Y0[idx])
+                res = dm.reactor_run(self.cfg, prob[idx], T0[idx], P0[idx], V0[idx], Y0[idx], **pert)
             pending.append((idx, res))
         out = BatchResult(tau=np.empty(n), T=np.empty(n), P=np.empty(n), V=np.empty(n), Y=np.empty((n, wt.size)),
                           stats=np.empty((n, _native.NSTAT), np.int32), wt=wt)
@@ -124,24 +135,24 @@ class BatchSweep:
 
 
 def afactor_sensitivity(chem: Chemistry, mixture: Mixture, factor: float = 1.001, reactions: Optional[Sequence[int]] = None,
-                        **sweep_kw) -> Dict[str, np.ndarray]:
+                        volume: float = 1.0, **sweep_kw) -> Dict[str, np.ndarray]:
     """Brute-force A-factor sensitivity of the ignition delay (reference sensitivity.py:122-160).
 
-    The reference perturbs one reaction's A by `factor` and re-runs the reactor serially
-    (326 native runs for GRI-3.0).  Here every perturbed mechanism is its own device table
-    set; the runs are issued back to back on the GPU and the result is
-    S_i = (tau_i - tau_0) / (factor - 1)   [s], indexed by 0-based reaction.
+    The reference perturbs one reaction's A by `factor` and re-runs the reactor serially (326
+    native runs for GRI-3.0).  Here the nominal reactor and every perturbed one are reactors of
+    ONE batch (per-reactor A multiplier, ckmi_reactor_run_ex), sharded over the visible GPUs.
+    Returns S_i = (tau_i - tau_0) / (factor - 1) [s] per 0-based reaction, tau_0 [s], and the
+    per-reactor status.
     """
     II = chem.IIGas
-    rx = list(range(II)) if reactions is None else list(reactions)
+    rx = np.arange(II) if reactions is None else np.asarray(list(reactions), dtype=np.int64)
+    if np.any(rx < 0) or np.any(rx >= II):
+        raise ValueError("reaction indices must be 0-based and < IIGas")
+    n = rx.size + 1
     sweep = BatchSweep(chem, **sweep_kw)
-    base = sweep.run([mixture.temperature], [mixture.pressure], Y0=mixture.Y.reshape(1, -1))
-    tau0 = float(base.tau[0])
-    A0, _, _ = chem.get_reaction_parameters()
-    sens = np.zeros(len(rx))
-    for j, i in enumerate(rx):
-        chem.set_reaction_AFactor(i + 1, A0[i] * factor)
-        r = sweep.run([mixture.temperature], [mixture.pressure], Y0=mixture.Y.reshape(1, -1))
-        chem.set_reaction_AFactor(i + 1, A0[i])
-        sens[j] = (float(r.tau[0]) - tau0) / (factor - 1.0)
-    return {"reactions": np.asarray(rx), "sensitivity": sens, "tau0": tau0}
+    afac_rxn = np.concatenate([[-1], rx]).astype(np.int32)
+    r = sweep.run(np.full(n, mixture.temperature), np.full(n, mixture.pressure), Y0=np.tile(mixture.Y, (n, 1)),
+                  V0=np.full(n, volume), afac_rxn=afac_rxn, afac=np.full(n, float(factor)))
+    tau0 = float(r.tau[0])
+    sens = (r.tau[1:] - tau0) / (factor - 1.0)
+    return {"reactions": rx, "sensitivity": sens, "tau0": tau0, "status": r.status.copy()}

@@ -88,20 +88,17 @@ __device__ __forceinline__ double ign_peak_time(const Ign& g) {
   return tv;
 }
 
-__device__ __forceinline__ int n_crit(const ckmi_reactor_cfg* c, double tend) {
-  int k = 0;
-  for (int i = 0; i < c->nprof; ++i)
-    if (c->prof_t[i] > 0.0 && c->prof_t[i] < tend) ++k;
-  return k + 1;
-}
-__device__ __forceinline__ double crit_time(const ckmi_reactor_cfg* c, double tend, int idx) {
-  int k = 0;
-  for (int i = 0; i < c->nprof; ++i)
-    if (c->prof_t[i] > 0.0 && c->prof_t[i] < tend) {
-      if (k == idx) return c->prof_t[i];
-      ++k;
-    }
-  return tend;
+// Device copy of the run configuration: the public struct plus the integration stop points
+// (the sorted union of both profiles' breakpoints in (0, t_end), where derivatives jump),
+// computed on the host by ckmi_reactor_run_ex.
+struct DevCfg {
+  ckmi_reactor_cfg c;
+  int ncrit;
+  double tcrit[128];
+};
+__device__ __forceinline__ int n_crit(const DevCfg* d) { return d->ncrit + 1; }
+__device__ __forceinline__ double crit_time(const DevCfg* d, double tend, int idx) {
+  return idx < d->ncrit ? d->tcrit[idx] : tend;
 }
 
 __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, double t, double yl, int lane, double& P,
@@ -112,11 +109,11 @@ __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, dou
   const double Wb = 1.0 / wave_sum(isp ? yl * M.rwt()[lane - 1] : 0.0);
   double d;
   if (R.conp) {
-    profile_eval(R.cfg, R.cfg->nprof, t, R.P0, P, d);
+    profile_eval(R.cfg, R.npv, t, t, R.P0, P, d);
     const double rho = P * Wb / (RU * T);
     V = R.rho0 * R.V0 / rho;
   } else {
-    profile_eval(R.cfg, R.cfg->nprof, t, R.V0, V, d);
+    profile_eval(R.cfg, R.npv, t, t, R.V0, V, d);
     const double rho = R.rho0 * R.V0 / V;
     P = rho * RU * T / Wb;
   }
@@ -130,12 +127,20 @@ struct ReactorIO {
   int nsave;
   const double* t_save;
   double* y_save;
+  // ckmi_reactor_ext
+  const int* afac_rxn;
+  const double* afac;
+  int max_adap;
+  double* t_adap;
+  double* y_adap;
+  int* n_adap;
 };
 
 // Integrator control state of one wave (wave-uniform scalars, kept in the wave's LDS slice).
 struct Ctl {
   int r, first, nflag, convfail, call_setup, failed, mm, ncf, nef, rc, isave, icrit, ncrit, status, nst, stopped;
-  int is_count, max_steps;
+  int is_count, max_steps, nadap;
+  double avar_last;
   double delp, saved_t, told, dsm, tc, tend, hmax, T0;
   double st_h0, st_tout, st_h, is_hg, is_hub, is_hlb, is_t0;
 };
@@ -197,9 +202,10 @@ enum {
 #endif
 constexpr int RWAVES = CKMI_RWAVES;
 template <int N>
-__global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, const ckmi_reactor_cfg* __restrict__ cfg,
+__global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, const DevCfg* __restrict__ dcfg,
                                                                int nreact, int* __restrict__ queue,
                                                                double* __restrict__ jws, ReactorIO io) {
+  const ckmi_reactor_cfg* __restrict__ cfg = &dcfg->c;
   const int oJ = img.bytes;
   const int olock = oJ + align16(8 * N * LDJ);
   if (threadIdx.x == 0) *lds_at<int>(olock) = 0;
@@ -250,6 +256,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
     _Pragma("unroll") for (int j_ = 1; j_ <= QMAX; ++j_) b.zn[j_] = 0.0; \
     b.ewt = act ? 1.0 / (S.rtol * fabs(b.zn[0]) + S.atol) : 0.0;       \
     c.st_tout = (TOUT_);                                               \
+    R.tsel = 0.5 * (S.tn + c.st_tout);                                 \
     c.st_h0 = (H0_);                                                   \
     REQUEST_F(S.tn, b.zn[0], ST_START_F);                              \
   } while (0)
@@ -272,17 +279,35 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           }
           c.r = r;
           const int prob = io.problem[r];
-          const double T0 = io.T0[r], P0 = io.P0[r];
+          // TPRO runs start at the profile's initial temperature
+          const double T0 = (cfg->prof_kind == 1 && cfg->energy == 2 && cfg->nprof > 0) ? cfg->prof_v[0] : io.T0[r];
+          const double P0 = io.P0[r];
           double yl = 0.0;
           if (lane == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + lane - 1];
           const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
           R.conp = (prob == 1);
           R.energy = cfg->energy;
-          R.nprof = cfg->nprof;
+          R.npv = cfg->prof_kind == 0 ? cfg->nprof : 0;
+          R.ntp = (cfg->prof_kind == 1 && cfg->energy == 2) ? cfg->nprof : 0;
           R.rho0 = P0 * Wbar0 / (RU * T0);
-          R.V0 = (!R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : io.V0[r];
-          R.P0 = (R.conp && cfg->nprof > 0) ? cfg->prof_v[0] : P0;
+          R.V0 = (!R.conp && R.npv > 0) ? cfg->prof_v[0] : io.V0[r];
+          R.P0 = (R.conp && R.npv > 0) ? cfg->prof_v[0] : P0;
+          R.mass = R.rho0 * R.V0;
+          R.gfac = cfg->gfac;
+          R.qloss = cfg->qloss;
+          R.htc = cfg->htc;
+          R.areaq = cfg->areaq;
+          R.tamb = cfg->tamb;
+          R.nq = cfg->prof2_kind == 1 ? cfg->nprof2 : 0;
+          R.na = cfg->prof2_kind == 2 ? cfg->nprof2 : 0;
+          {
+            const int ar = io.afac_rxn ? io.afac_rxn[r] : -1;
+            R.pslot = (ar >= 0 && ar < img.II) ? img.slot_of[ar] : -1;
+            R.plnf = R.pslot >= 0 ? log(io.afac[r]) : 0.0;
+          }
+          c.nadap = 0;
+          c.avar_last = bcast(yl, cfg->avar > 0 ? cfg->avar : 0);
           c.T0 = T0;
           S.rtol = cfg->rtol;
           S.atol = cfg->atol;
@@ -292,7 +317,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           c.hmax = cfg->hmax > 0.0 ? cfg->hmax : c.tend / 100.0;
           S.hmax_inv = 1.0 / c.hmax;
           S.hmin = 0.0;
-          c.ncrit = n_crit(cfg, c.tend);
+          c.ncrit = n_crit(dcfg);
           c.icrit = 0;
           c.first = 1;
           c.max_steps = cfg->max_steps > 0 ? cfg->max_steps : 200000;
@@ -302,7 +327,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           if (lane < 32) phs[lane] = 0;
           t_r0 = __builtin_amdgcn_s_memtime();
 #endif
-          START_BEGIN(0.0, yl, crit_time(cfg, c.tend, 0), cfg->h0);
+          START_BEGIN(0.0, yl, crit_time(dcfg, c.tend, 0), cfg->h0);
           break;
         }
         case ST_START_F: {
@@ -424,7 +449,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
             st = ST_FINISH;
             break;
           }
-          c.tc = crit_time(cfg, c.tend, c.icrit);
+          c.tc = crit_time(dcfg, c.tend, c.icrit);
           if (S.tn + S.hprime > c.tc) {
             const double hp = c.tc - S.tn;
             S.eta = hp / S.h;
@@ -785,6 +810,22 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
               break;
             }
           }
+          bool adap = false;
+          if (io.n_adap && c.nadap < io.max_adap) {
+            // ADAP: extra solution points every ASTEPS steps, or when AVAR moved by AVALUE
+            if (cfg->asteps > 0 && c.nst % cfg->asteps == 0) adap = true;
+            if (cfg->avar >= 0 && cfg->avalue > 0.0) {
+              const double v = bcast(b.zn[0], cfg->avar);
+              if (fabs(v - c.avar_last) >= cfg->avalue) adap = true;
+            }
+          }
+          if (adap) {
+            const size_t a = (size_t)c.r * io.max_adap + c.nadap;
+            if (lane == 0) io.t_adap[a] = tn;
+            if (act) io.y_adap[a * n + lane] = b.zn[0];
+            c.nadap++;
+            if (cfg->avar >= 0) c.avar_last = bcast(b.zn[0], cfg->avar);
+          }
           if (c.nst >= c.max_steps) {
             c.status = CKMI_RUN_MAXSTEPS;
             st = ST_FINISH;
@@ -792,7 +833,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           }
           if (tn >= c.tc * (1.0 - 1e-15) && c.icrit < c.ncrit - 1) {
             c.icrit++;
-            START_BEGIN(tn, b.zn[0], crit_time(cfg, c.tend, c.icrit), 0.0);
+            START_BEGIN(tn, b.zn[0], crit_time(dcfg, c.tend, c.icrit), 0.0);
           }
           break;
         }
@@ -825,6 +866,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
             sto[CKMI_STAT_NNI] = S.nni;
           }
           if (isp) io.Y[(size_t)r * KK + lane - 1] = yf;
+          if (io.n_adap && lane == 0) io.n_adap[r] = c.nadap;
 #ifdef CKMI_PHASE_TIMERS
           ph[PH_TOTAL] = __builtin_amdgcn_s_memtime() - t_r0;
           wave_lds_sync();
@@ -980,7 +1022,8 @@ struct ckmi_mech {
   // host copies of the forward Arrhenius (original order) for get/set
   std::vector<double> lnA_orig, b_orig, E_orig;
   std::vector<int> slot_of;  // original reaction -> device slot
-  ckmi_reactor_cfg* cfg_dev;
+  DevCfg* cfg_dev;
+  mutable DevCfg cfg_host;  // host staging of the per-call configuration
 };
 
 namespace {
@@ -1097,6 +1140,11 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)g * KKp + gsp[e]] = geff[e];
   I.o_geffd = put(geffd.data(), geffd.size() * 8);
   I.bytes = (int)blob.size();
+  {
+    const int* so = nullptr;
+    if (upload(m, m->slot_of, &so) != CKMI_OK) return CKMI_ERR_HIP;
+    I.slot_of = so;
+  }
   void* p = nullptr;
   HIP_CHECK(hipMalloc(&p, blob.size()));
   m->allocs.push_back(p);
@@ -1328,9 +1376,9 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   rc |= build_image(m, d, slots, flags, nrp, rsp, psp, rnu, pnu, lnA, beta, Ea, lnA0, beta0, Ea0, fp, rlnA, rbeta, rEa,
                     tb, gptr, gsp, geff, wt, rwt);
   void* cp = nullptr;
-  if (hipMalloc(&cp, sizeof(ckmi_reactor_cfg)) != hipSuccess) rc |= CKMI_ERR_HIP;
+  if (hipMalloc(&cp, sizeof(DevCfg)) != hipSuccess) rc |= CKMI_ERR_HIP;
   else m->allocs.push_back(cp);
-  m->cfg_dev = static_cast<ckmi_reactor_cfg*>(cp);
+  m->cfg_dev = static_cast<DevCfg*>(cp);
   if (rc) {
     ckmi_mech_destroy(m);
     return rc;
@@ -1405,20 +1453,52 @@ int ckmi_reaction_rates(const ckmi_mech* m, int32_t n, const double* T, const do
   return CKMI_OK;
 }
 
-int ckmi_reactor_run(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t n, const int32_t* problem,
-                     const double* T0, const double* P0, const double* V0, const double* Y0, double* tau, double* Tend,
-                     double* Pend, double* Vend, double* Yend, int32_t* stats, int32_t nsave, const double* t_save,
-                     double* y_save, void* stream) {
+int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t n, const int32_t* problem,
+                        const double* T0, const double* P0, const double* V0, const double* Y0,
+                        const ckmi_reactor_ext* ext, double* tau, double* Tend, double* Pend, double* Vend,
+                        double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
+                        void* stream) {
   if (!m || !cfg || n < 0) return fail(CKMI_ERR_ARG, "bad argument");
   if (cfg->nprof < 0 || cfg->nprof > 64) return fail(CKMI_ERR_ARG, "nprof must be in [0, 64]");
   if (!(cfg->t_end > 0.0) || !(cfg->rtol > 0.0) || !(cfg->atol > 0.0)) return fail(CKMI_ERR_ARG, "t_end, rtol, atol must be > 0");
   if (cfg->energy != 1 && cfg->energy != 2) return fail(CKMI_ERR_ARG, "energy must be 1 or 2");
   if (cfg->ign_mode < 0 || cfg->ign_mode > 4) return fail(CKMI_ERR_ARG, "bad ignition mode");
   if (cfg->ign_mode == 4 && (cfg->ign_species < 0 || cfg->ign_species >= m->KK)) return fail(CKMI_ERR_ARG, "bad KLIM species");
+  if (cfg->prof_kind != 0 && cfg->prof_kind != 1) return fail(CKMI_ERR_ARG, "prof_kind must be 0 (VPRO/PPRO) or 1 (TPRO)");
+  if (cfg->prof_kind == 1 && cfg->energy != 2) return fail(CKMI_ERR_ARG, "TPRO needs a given-temperature run (energy = 2)");
+  if (!(cfg->gfac >= 0.0)) return fail(CKMI_ERR_ARG, "GFAC must be >= 0");
+  if (!(cfg->htc >= 0.0) || !(cfg->areaq >= 0.0) || !(cfg->tamb > 0.0 || cfg->htc * cfg->areaq == 0.0))
+    return fail(CKMI_ERR_ARG, "HTC, AREAQ must be >= 0 and TAMB > 0");
+  if (cfg->asteps < 0) return fail(CKMI_ERR_ARG, "asteps must be >= 0");
   if (nsave > 0 && (!t_save || !y_save)) return fail(CKMI_ERR_ARG, "t_save / y_save required when nsave > 0");
+  if (ext && (ext->afac_rxn != nullptr) != (ext->afac != nullptr)) return fail(CKMI_ERR_ARG, "afac_rxn and afac go together");
+  if (ext && ext->n_adap && (ext->max_adap <= 0 || !ext->t_adap || !ext->y_adap))
+    return fail(CKMI_ERR_ARG, "n_adap needs max_adap > 0, t_adap and y_adap");
+  if (cfg->nprof2 < 0 || cfg->nprof2 > 64) return fail(CKMI_ERR_ARG, "nprof2 must be in [0, 64]");
+  if (cfg->nprof2 > 0 && cfg->prof2_kind != 1 && cfg->prof2_kind != 2)
+    return fail(CKMI_ERR_ARG, "prof2_kind must be 1 (QPRO) or 2 (AEXT)");
+  if (cfg->nprof2 > 0 && cfg->energy != 1) return fail(CKMI_ERR_ARG, "QPRO / AEXT need an energy-equation run");
+  if (cfg->avar > m->KK || cfg->avar < -1) return fail(CKMI_ERR_ARG, "avar must be -1, 0 (T) or 1 + species index");
   if (n == 0) return CKMI_OK;
-  HIP_CHECK(hipMemcpyAsync(m->cfg_dev, cfg, sizeof(ckmi_reactor_cfg), hipMemcpyHostToDevice, (hipStream_t)stream));
-  ReactorIO io{problem, T0, P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save};
+  {
+    DevCfg& dc = m->cfg_host;
+    dc.c = *cfg;
+    if (dc.c.gfac == 0.0) dc.c.gfac = 1.0;
+    std::vector<double> tc;
+    for (int i = 0; i < cfg->nprof; ++i)
+      if (cfg->prof_t[i] > 0.0 && cfg->prof_t[i] < cfg->t_end) tc.push_back(cfg->prof_t[i]);
+    for (int i = 0; i < cfg->nprof2; ++i)
+      if (cfg->prof2_t[i] > 0.0 && cfg->prof2_t[i] < cfg->t_end) tc.push_back(cfg->prof2_t[i]);
+    std::sort(tc.begin(), tc.end());
+    tc.erase(std::unique(tc.begin(), tc.end()), tc.end());
+    dc.ncrit = (int)tc.size();
+    std::copy(tc.begin(), tc.end(), dc.tcrit);
+    // pageable source: the runtime stages it before returning
+    HIP_CHECK(hipMemcpyAsync(m->cfg_dev, &dc, sizeof(DevCfg), hipMemcpyHostToDevice, (hipStream_t)stream));
+  }
+  ReactorIO io{problem, T0, P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save,
+               ext ? ext->afac_rxn : nullptr, ext ? ext->afac : nullptr, ext ? ext->max_adap : 0,
+               ext ? ext->t_adap : nullptr, ext ? ext->y_adap : nullptr, ext ? ext->n_adap : nullptr};
   const int nvar = m->KK + 1;
   int rc;
   if (nvar <= 32) rc = launch_reactors<32>(m, n, io, (hipStream_t)stream);
@@ -1427,6 +1507,14 @@ int ckmi_reactor_run(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t n,
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;
+}
+
+int ckmi_reactor_run(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t n, const int32_t* problem,
+                     const double* T0, const double* P0, const double* V0, const double* Y0, double* tau, double* Tend,
+                     double* Pend, double* Vend, double* Yend, int32_t* stats, int32_t nsave, const double* t_save,
+                     double* y_save, void* stream) {
+  return ckmi_reactor_run_ex(m, cfg, n, problem, T0, P0, V0, Y0, nullptr, tau, Tend, Pend, Vend, Yend, stats, nsave,
+                             t_save, y_save, stream);
 }
 
 }  // extern "C"

@@ -28,6 +28,7 @@ constexpr int AUXW = 12;
 
 struct MechImage {
   const uint4* blob;  // device copy of the image
+  const int* slot_of; // device: original reaction index -> device slot
   int bytes;          // multiple of 16
   int KK, KKp, II, IIp, G, naux;
   int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff, o_geffd;
@@ -151,10 +152,11 @@ struct Rxn {
 __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t inf, uint32_t rs, uint32_t ps,
                                             uint32_t nuw, double T, double lnT, double invT, double lnPRT,
                                             const double* C, const double* gRT, const double* hRT, const double* Mg,
-                                            bool need_h) {
+                                            bool need_h, int pslot = -1, double plnf = 0.0, double gfac = 1.0) {
   constexpr double INV_LN10 = 0.43429448190325176;
   const int type = rx_type(inf);
-  const double lnA = V.lnA()[i], b = V.beta()[i], Ea = V.Ea()[i];
+  // pslot / plnf: per-reactor A-factor perturbation (brute-force sensitivity)
+  const double lnA = V.lnA()[i] + (i == pslot ? plnf : 0.0), b = V.beta()[i], Ea = V.Ea()[i];
   const double lnkinf = lnA + b * lnT - Ea * invT;
   const double kf_inf = exp(lnkinf);
   double kf = kf_inf;
@@ -230,8 +232,8 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
     if (u < np) pr *= powi(C[sp_of(ps, u)], nup_of(nuw, u));
   }
   Rxn e;
-  e.kf = kf;
-  e.kr = kr;
+  e.kf = kf * gfac;  // GFAC scales forward and reverse rates alike
+  e.kr = kr * gfac;
   e.mfac = mfac;
   e.pf = pf;
   e.pr = pr;

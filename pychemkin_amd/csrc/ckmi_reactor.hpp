@@ -45,22 +45,46 @@ struct WaveLds {
 constexpr int LDJ = WAVE + 1;  // leading dimension of the shared J scratch (odd: conflict-free columns)
 
 struct RunCtx {
-  int conp, energy, nprof;
+  int conp, energy;
+  int npv;     // VPRO / PPRO profile points (0 = constant V / P)
+  int ntp;     // TPRO profile points (given-temperature runs, 0 = T from the state)
+  int pslot;   // device slot of the reaction whose A is perturbed (-1 none), and ln(factor)
+  double plnf;
+  double gfac;               // GFAC
   double rho0, V0, P0;
+  double mass;                       // rho0 V0 [g]
+  double qloss, htc, areaq, tamb;    // QLOS [cal/s], HTC, AREAQ, TAMB
+  int nq, na;                        // QPRO / AEXT profile points (prof2), 0 = constant
+  double tsel;                       // midpoint of the current integration segment (pwl_eval)
   const ckmi_reactor_cfg* cfg;
 };
 
-__device__ __forceinline__ void profile_eval(const ckmi_reactor_cfg* c, int nprof, double t, double base, double& v,
-                                             double& dvdt) {
-  if (nprof <= 0) { v = base; dvdt = 0.0; return; }
-  const double x0 = c->prof_t[0];
-  if (t <= x0) { v = c->prof_v[0]; dvdt = 0.0; return; }
-  if (t >= c->prof_t[nprof - 1]) { v = c->prof_v[nprof - 1]; dvdt = 0.0; return; }
+constexpr double ERG_PER_CAL = 4.184e7;  // reference constants.py (JOULES_PER_CALORIE x 1e7)
+
+// Piecewise-linear profile (x[np], y[np]) at t, constant outside [x0, x_np-1].  The linear piece
+// is the one that contains tsel, the midpoint of the current integration segment (segments end at
+// every breakpoint): a step that ends exactly on a breakpoint then uses the slope on its left and
+// the first step after the restart the slope on its right, as an implicit method needs.
+__device__ __forceinline__ void pwl_eval(const double* x, const double* y, int np, double t, double tsel, double& v,
+                                         double& dvdt) {
+  if (tsel <= x[0]) { v = y[0]; dvdt = 0.0; return; }
+  if (tsel >= x[np - 1]) { v = y[np - 1]; dvdt = 0.0; return; }
   int j = 0;
-  while (j < nprof - 2 && t >= c->prof_t[j + 1]) ++j;
-  const double s = (c->prof_v[j + 1] - c->prof_v[j]) / (c->prof_t[j + 1] - c->prof_t[j]);
-  v = c->prof_v[j] + s * (t - c->prof_t[j]);
+  while (j < np - 2 && tsel >= x[j + 1]) ++j;
+  const double s = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
+  v = y[j] + s * (t - x[j]);
   dvdt = s;
+}
+// VPRO / PPRO / TPRO slot
+__device__ __forceinline__ void profile_eval(const ckmi_reactor_cfg* c, int nprof, double t, double tsel, double base,
+                                             double& v, double& dvdt) {
+  if (nprof <= 0) { v = base; dvdt = 0.0; return; }
+  pwl_eval(c->prof_t, c->prof_v, nprof, t, tsel, v, dvdt);
+}
+// the second profile slot (QPRO / AEXT)
+__device__ __forceinline__ void profile2_eval(const ckmi_reactor_cfg* c, int np, double t, double tsel, double& v,
+                                              double& dvdt) {
+  pwl_eval(c->prof2_t, c->prof2_v, np, t, tsel, v, dvdt);
 }
 
 // Orders the wave's LDS accesses (LDS operations of one wave complete in issue order, so
@@ -115,7 +139,8 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const int KK = V.KK;
   const bool isp = lane >= 1 && lane <= KK;
   const int s = isp ? lane - 1 : 0;
-  const double T = bcast(yl, 0);
+  double T = bcast(yl, 0), dTdt_given = 0.0;
+  if (R.ntp > 0) profile_eval(R.cfg, R.ntp, t, R.tsel, T, T, dTdt_given);  // TPRO: T(t) is given
   const double Yk = isp ? yl : 0.0;
   const double rw = isp ? V.rwt()[s] : 0.0;
   const double Wk = isp ? V.wt()[s] : 0.0;
@@ -123,11 +148,11 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const int conp = R.conp;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
   if (conp) {
-    profile_eval(R.cfg, R.nprof, t, R.P0, P, dPdt);
+    profile_eval(R.cfg, R.npv, t, R.tsel, R.P0, P, dPdt);
     rho = P * Wbar / (RU * T);
     V_ = R.rho0 * R.V0 / rho;
   } else {
-    profile_eval(R.cfg, R.nprof, t, R.V0, V_, dVdt);
+    profile_eval(R.cfg, R.npv, t, R.tsel, R.V0, V_, dVdt);
     rho = R.rho0 * R.V0 / V_;
     P = rho * RU * T / Wbar;
   }
@@ -181,7 +206,8 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     const int nr = rx_nr(inf), np = rx_np(inf);
     if (nr + np == 0) continue;
     const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
-    const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false);
+    const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false,
+                               R.pslot, R.plnf, R.gfac);
     const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -196,7 +222,8 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       const int nr = rx_nr(inf), np = rx_np(inf);
       if (nr + np == 0) continue;
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
-      const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), true);
+      const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), true,
+                                 R.pslot, R.plnf, R.gfac);
       const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
       double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
       if (conp) {
@@ -251,6 +278,14 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     double fT = -sum / cpm;
     if (conp) fT += dPdt / (rho * cpm);
     else fT -= P * dVdt / (V_ * rho * cpm);
+    // heat loss to the surroundings (QLOS + HTC AREAQ (T - TAMB), or the QPRO / AEXT profile),
+    // per unit heat capacity of the reactor contents
+    double qloss = R.qloss, area = R.areaq, dummy;
+    if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
+    if (R.na > 0) profile2_eval(R.cfg, R.na, t, R.tsel, area, dummy);
+    const double mcp = R.mass * cpm;
+    const double q1 = R.htc * area * ERG_PER_CAL;
+    fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
     if (lane == 0) fl = fT;
     if (with_j) {
       const double JkT = isp ? L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;
@@ -267,10 +302,10 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
         Jsh[(1 + s) * LDJ] = -acc / cpm - fT * ck / cpm;  // row 0, column 1+s
       }
       const double s2 = wave_sum(ck * fY + ek * JkT);
-      if (lane == 0) Jsh[0] = -s2 / cpm;
+      if (lane == 0) Jsh[0] = -s2 / cpm - q1 / mcp;
     }
   } else {
-    if (lane == 0) fl = 0.0;
+    if (lane == 0) fl = dTdt_given;  // 0 without TPRO
     if (with_j && isp) Jsh[1 + s] = L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0);
   }
   wave_lds_sync();

@@ -85,6 +85,34 @@ def h2_air_Y(mech):
     return Y / Y.sum()
 
 
+def sensitivity_mixture(chem):
+    """sensitivity.py:66-86: C3H8:CH4:H2 = 0.1:0.8:0.1 fuel, O2:N2 = 1:3.76, phi = 1.1, 900 K, 1 atm."""
+    import pychemkin_amd as ck
+
+    oxid = ck.Mixture(chem)
+    oxid.X = [("O2", 1.0), ("N2", 3.76)]
+    fuel = ck.Mixture(chem)
+    fuel.X = [("C3H8", 0.1), ("CH4", 0.8), ("H2", 0.1)]
+    mix = ck.Mixture(chem)
+    mix.pressure = P_ATM
+    mix.temperature = 900.0
+    assert mix.X_by_Equivalence_Ratio(chem, fuel.X, oxid.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"],
+                                      equivalenceratio=1.1) == 0
+    return mix
+
+
+# sensitivity.py:95-122: CONP + ENERGY, V = 10 cm3, t_end = 2 s, 1e-10/1e-8, TIFP; perturbation 0.1 %
+SENS_RUN = dict(energy=1, t_end=2.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
+SENS_FACTOR = 1.001
+
+
+def top5(sens):
+    """Indices of the 5 largest positive and 5 most negative coefficients (sensitivity.py:166-174)."""
+    pos = np.argpartition(sens, -5)[-5:]
+    neg = np.argpartition(-sens, -5)[-5:]
+    return set(pos.tolist()), set(neg.tolist())
+
+
 def within(a, b, atol, rtol):
     """Symmetric golden tolerance |a - b| <= atol + rtol |b| (SURVEY.md section 4 comparator fix)."""
     a = np.asarray(a, dtype=np.float64)

@@ -95,8 +95,32 @@ def test_volume_profile_cfg(chem):
     cfg = r.reactor_cfg()
     assert cfg.nprof == 3 and list(cfg.prof_v[:3]) == [10.0, 4.0, 4.0]
     r.heat_loss_rate = 5.0
-    with pytest.raises(ReactorError):
+    r.heat_transfer_coefficient = 1e-3
+    r.heat_transfer_area = 20.0
+    r.ambient_temperature = 350.0
+    r.gasratemultiplier = 2.0
+    r.adaptive_solution_saving(True, steps=20)
+    cfg = r.reactor_cfg()
+    assert (cfg.qloss, cfg.htc, cfg.areaq, cfg.tamb, cfg.gfac, cfg.asteps) == (5.0, 1e-3, 20.0, 350.0, 2.0, 20)
+    r.set_heat_loss_profile([0.0, 0.05], [0.0, 10.0])
+    cfg = r.reactor_cfg()
+    assert cfg.prof2_kind == 1 and cfg.nprof2 == 2 and cfg.nprof == 3
+    r.set_heat_transfer_area_profile([0.0, 0.05], [1.0, 2.0])
+    with pytest.raises(ReactorError):  # QPRO together with AEXT is not on the device path yet
         r.reactor_cfg()
+
+
+def test_temperature_profile_cfg(chem):
+    m = ck.Mixture(chem)
+    m.X = [("CH4", 0.1), ("O2", 0.2), ("N2", 0.7)]
+    m.pressure = P_ATM
+    m.temperature = 1000.0
+    r = ck.GivenPressureBatchReactor_FixedTemperature(m, label="TPRO")
+    r.time = 1e-3
+    r.set_temperature_profile([0.0, 5e-4, 1e-3], [1000.0, 1500.0, 1500.0])
+    r.adaptive_solution_saving(True, value_change=10.0, target="temperature")
+    cfg = r.reactor_cfg()
+    assert cfg.energy == 2 and cfg.prof_kind == 1 and cfg.nprof == 3 and cfg.avar == 0 and cfg.avalue == 10.0
 
 
 def test_afactor_get_set(chem):

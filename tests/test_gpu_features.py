@@ -1,0 +1,129 @@
+"""§8f rows on the GPU path against the oracle and the reference goldens: batched brute-force
+A-factor sensitivity (sensitivity.baseline), GFAC, heat loss (QLOS / HTC / QPRO), TPRO and
+adaptive solution saving (ASTEPS / AVAR)."""
+import numpy as np
+import pytest
+
+from conftest import P_ATM, SENS_FACTOR, SENS_RUN, ch4_air_Y, golden, sensitivity_mixture, top5
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dm(tables):
+    from pychemkin_amd import _native
+
+    return _native.DeviceMechanism(tables)
+
+
+def test_batched_afactor_sensitivity_golden(chem, oracle, mech):
+    """The reference's 326 serial runs (sensitivity.py:141-160) as one batch of 326 reactors."""
+    import pychemkin_amd as ck
+
+    g = golden("sensitivity")
+    mix = sensitivity_mixture(chem)
+    out = ck.afactor_sensitivity(chem, mix, factor=SENS_FACTOR, volume=10.0, problem="CONP", energy="ENERGY",
+                                 t_end=2.0, atol=1e-10, rtol=1e-8, ignition="T_inflection")
+    assert np.all(out["status"] == 0)
+    sens = out["sensitivity"] * 1e3  # ms per unit relative perturbation, as the golden
+    pos, neg = top5(sens)
+    assert pos == set(g["state-index_positive"]) and neg == set(g["state-index_negative"])
+    idx = g["state-index_positive"] + g["state-index_negative"]
+    ref = np.array(g["rate-sensitivity_positive"] + g["rate-sensitivity_negative"])
+    assert np.all(np.abs(sens[idx] / ref - 1) < 0.03)
+    # the same coefficients from the oracle's restatement (finite differences amplify the
+    # ~1e-6 relative tau differences of two integrations 1000-fold)
+    r0, _ = oracle.reactor(900.0, P_ATM, 10.0, mix.Y, **SENS_RUN)
+    assert abs(out["tau0"] / r0.tau - 1) < 1e-5
+    II = mech.II
+    _, res, _ = oracle.reactor_batch_pert(np.full(II, 900.0), np.full(II, P_ATM), np.tile(mix.Y, (II, 1)),
+                                          np.arange(II, dtype=np.int32), np.full(II, SENS_FACTOR),
+                                          V0=np.full(II, 10.0), **SENS_RUN)
+    so = (np.array([r.tau for r in res]) - r0.tau) * 1e3 / (SENS_FACTOR - 1.0)
+    assert np.all(np.abs(sens[idx] - so[idx]) < 0.02 * np.abs(so[idx]))
+
+
+def test_gfac_and_heat_loss_vs_oracle(dm, oracle, mech):
+    from pychemkin_amd import _native
+
+    Y0 = ch4_air_Y(mech, 1.0)
+    cases = [dict(gfac=2.0), dict(qloss=0.5), dict(htc=2e-3, areaq=5.0, tamb=400.0),
+             dict(profile2=([0.0, 0.02], [0.0, 1.0]), prof2_kind=1),
+             dict(htc=2e-3, areaq=5.0, tamb=400.0, profile2=([0.0, 0.01, 0.02], [2.0, 8.0, 8.0]), prof2_kind=2)]
+    for kw in cases:
+        cfg = dict(energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP", **kw)
+        res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1, 2], np.int32), [1250.0, 1250.0],
+                             [2 * P_ATM, 2 * P_ATM], [3.0, 3.0], np.vstack([Y0, Y0]))
+        for i, prob in enumerate((1, 2)):
+            r, Ye = oracle.reactor(1250.0, 2 * P_ATM, 3.0, Y0[0], problem=prob, **cfg)
+            assert r.status == 0 and int(res["stats"][i, 6]) == 0, kw
+            assert abs(res["tau"][i].item() / r.tau - 1) < 1e-4, kw
+            assert abs(res["T"][i].item() / r.T - 1) < 1e-5, kw
+    # heat loss lowers the final temperature, GFAC = 2 shortens the ignition delay
+    base = dm.reactor_run(_native.make_cfg(energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP"),
+                          np.array([1], np.int32), [1250.0], [2 * P_ATM], [3.0], Y0)
+    lossy = dm.reactor_run(_native.make_cfg(energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP", qloss=0.5),
+                           np.array([1], np.int32), [1250.0], [2 * P_ATM], [3.0], Y0)
+    fast = dm.reactor_run(_native.make_cfg(energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP", gfac=2.0),
+                          np.array([1], np.int32), [1250.0], [2 * P_ATM], [3.0], Y0)
+    assert lossy["T"][0].item() < base["T"][0].item() - 10.0
+    assert fast["tau"][0].item() < 0.7 * base["tau"][0].item()
+
+
+def test_temperature_profile_vs_oracle(dm, oracle, mech):
+    from pychemkin_amd import _native
+
+    Y0 = ch4_air_Y(mech, 1.0)
+    prof = ([0.0, 1e-3, 2e-3], [1000.0, 1600.0, 1600.0])
+    ts = np.linspace(0.0, 2e-3, 21)
+    cfg = dict(energy=2, t_end=2e-3, atol=1e-12, rtol=1e-8, profile=prof, prof_kind=1)
+    res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1], np.int32), [1234.0], [P_ATM], [1.0], Y0, t_save=ts)
+    _, Ye, (_, ys, _, _) = oracle.reactor(1234.0, P_ATM, 1.0, Y0[0], t_save=ts, **cfg)
+    got = res["y_save"][0].cpu().numpy()
+    assert np.max(np.abs(got[:, 0] - np.interp(ts, prof[0], prof[1]))) < 1e-6
+    assert np.max(np.abs(got[:, 1:] - ys[:, 1:])) < 1e-7
+    assert abs(res["T"][0].item() - 1600.0) < 1e-6
+
+
+def test_adaptive_points_vs_oracle_dense_output(dm, oracle, mech):
+    from pychemkin_amd import _native
+
+    Y0 = ch4_air_Y(mech, 1.0)
+    cfg = dict(energy=1, t_end=5e-3, atol=1e-12, rtol=1e-8, ign_mode="TIFP", asteps=20)
+    res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1], np.int32), [1500.0], [10 * P_ATM], [1.0], Y0,
+                         max_adap=4096)
+    nst = int(res["stats"][0, 0])
+    na = int(res["n_adap"][0])
+    assert na == nst // 20
+    ta = res["t_adap"][0, :na].cpu().numpy()
+    ya = res["y_adap"][0, :na].cpu().numpy()
+    assert np.all(np.diff(ta) > 0)
+    _, _, (_, ys, _, _) = oracle.reactor(1500.0, 10 * P_ATM, 1.0, Y0[0], t_save=ta, problem=1, **cfg)
+    assert np.max(np.abs(ya[:, 0] / ys[:, 0] - 1)) < 1e-5
+    # AVAR/AVALUE: a point whenever T moved >= 50 K since the last one
+    cfg = dict(energy=1, t_end=5e-3, atol=1e-12, rtol=1e-8, ign_mode="TIFP", avar=0, avalue=50.0)
+    res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1], np.int32), [1500.0], [10 * P_ATM], [1.0], Y0,
+                         max_adap=4096)
+    na = int(res["n_adap"][0])
+    Ta = res["y_adap"][0, :na, 0].cpu().numpy()
+    assert na >= int((res["T"][0].item() - 1500.0) // 50.0) - 1
+    assert np.all(np.abs(np.diff(np.concatenate([[1500.0], Ta]))) >= 50.0)
+
+
+def test_drop_in_api_heat_loss_and_adaptive(chem):
+    import pychemkin_amd as ck
+
+    m = ck.Mixture(chem)
+    m.X = [("H2", 2.0), ("O2", 1.0), ("N2", 3.76)]
+    m.temperature = 1000.0
+    m.pressure = P_ATM
+    r = ck.GivenPressureBatchReactor_EnergyConservation(m, label="tran")
+    r.time = 5e-4
+    r.tolerances = (1e-20, 1e-8)
+    r.heat_loss_rate = 0.01
+    r.adaptive_solution_saving(True, steps=20)
+    assert r.run() == 0
+    r.process_solution()
+    t = r.get_solution_variable_profile("time")
+    assert len(t) > 101 and np.all(np.diff(t) > 0)  # DTSV grid plus adaptive points
+    assert r.get_ignition_delay() > 0

@@ -2,7 +2,8 @@
 import numpy as np
 import pytest
 
-from conftest import P_ATM, ch4_air_Y, golden, h2_air_Y, within
+from conftest import (P_ATM, SENS_FACTOR, SENS_RUN, ch4_air_Y, golden, h2_air_Y, sensitivity_mixture, top5,
+                      within)
 
 R = 1.3806504e-16 * 6.02214179e23
 
@@ -94,3 +95,25 @@ def test_reaction_rates_1800K_ordering(oracle, mech):
     assert order.tolist() == g["state-order_1800"]
     ratio = net[order] / np.asarray(g["rate-net_reaction_rate_1800"])
     assert np.all((ratio > 0.5) & (ratio < 2.0))
+
+
+def test_afactor_sensitivity_golden(oracle, mech, chem):
+    """sensitivity.baseline: 325 brute-force A-factor perturbations of a C3H8/CH4/H2 ignition
+    (sensitivity.py:141-160).  The oracle reproduces Chemkin's top-5 positive and negative
+    reactions exactly and the coefficients (d tau [ms] / 0.001) within 3 % (most within 1 %);
+    this pins the kinetics, the integrator and the TIFP definition together."""
+    g = golden("sensitivity")
+    mix = sensitivity_mixture(chem)
+    II = mech.II
+    r0, _ = oracle.reactor(900.0, P_ATM, 10.0, mix.Y, **SENS_RUN)
+    nf, res, _ = oracle.reactor_batch_pert(np.full(II, 900.0), np.full(II, P_ATM), np.tile(mix.Y, (II, 1)),
+                                           np.arange(II, dtype=np.int32), np.full(II, SENS_FACTOR),
+                                           V0=np.full(II, 10.0), **SENS_RUN)
+    assert nf == 0 and r0.status == 0
+    sens = (np.array([r.tau for r in res]) - r0.tau) * 1e3 / (SENS_FACTOR - 1.0)
+    pos, neg = top5(sens)
+    assert pos == set(g["state-index_positive"]) and neg == set(g["state-index_negative"])
+    idx = g["state-index_positive"] + g["state-index_negative"]
+    ref = np.array(g["rate-sensitivity_positive"] + g["rate-sensitivity_negative"])
+    assert np.all(np.abs(sens[idx] / ref - 1) < 0.03)
+    assert np.median(np.abs(sens[idx] / ref - 1)) < 0.01

@@ -74,3 +74,51 @@ def test_oracle_ignition_converges_in_tolerance(oracle, mech):
                                 ign_mode="TIFP")
         taus.append(res.tau)
     assert abs(taus[0] / taus[1] - 1) < 1e-4
+
+
+def test_heat_loss_energy_balance_inert(oracle, mech):
+    """QLOS on a non-reacting N2 charge at constant pressure: h(T(t)) = h(T0) - Q t / m exactly."""
+    from scipy.optimize import brentq
+
+    R = 1.3806504e-16 * 6.02214179e23
+    k = mech.species.index("N2")
+    Y = np.zeros(mech.KK)
+    Y[k] = 1.0
+    T0, V0, Q, tend = 1200.0, 10.0, 2.0, 0.05  # Q [cal/s]
+    r, _ = oracle.reactor(T0, P_ATM, V0, Y, energy=1, t_end=tend, atol=1e-12, rtol=1e-10, qloss=Q)
+    assert r.status == 0
+
+    def h_mass(T):
+        return oracle.thermo(T)[1][k] * R * T / mech.wt[k]
+
+    mass = P_ATM * mech.wt[k] / (R * T0) * V0
+    T_exact = brentq(lambda T: h_mass(T) - (h_mass(T0) - Q * 4.184e7 * tend / mass), 300.0, T0)
+    assert abs(r.T / T_exact - 1) < 1e-8
+    # wall heat transfer towards a hotter ambient heats the charge
+    r2, _ = oracle.reactor(T0, P_ATM, V0, Y, energy=1, t_end=tend, atol=1e-12, rtol=1e-10, htc=1e-3, areaq=20.0,
+                           tamb=1500.0)
+    assert 1200.0 < r2.T < 1500.0
+    # QPRO ramp 0 -> 2Q over t_end removes the same heat as a constant Q
+    r3, _ = oracle.reactor(T0, P_ATM, V0, Y, energy=1, t_end=tend, atol=1e-12, rtol=1e-10,
+                           profile2=([0.0, tend], [0.0, 2 * Q]), prof2_kind=1)
+    assert abs(r3.T / T_exact - 1) < 1e-7
+
+
+def test_temperature_profile_given_T(oracle, mech):
+    """TPRO on a fixed-temperature reactor: T follows the piecewise-linear profile exactly."""
+    Y = ch4_air_Y(mech, 1.0)[0]
+    prof = ([0.0, 1e-3, 2e-3], [1000.0, 1600.0, 1600.0])
+    ts = np.linspace(0.0, 2e-3, 21)
+    r, _, (_, ys, _, _) = oracle.reactor(1234.0, P_ATM, 1.0, Y, t_save=ts, energy=2, t_end=2e-3, atol=1e-12,
+                                         rtol=1e-8, profile=prof, prof_kind=1)
+    assert r.status == 0
+    assert np.max(np.abs(ys[:, 0] - np.interp(ts, prof[0], prof[1]))) < 1e-6
+    assert abs(r.T - 1600.0) < 1e-6
+
+
+def test_gfac_scales_all_rates(oracle, mech):
+    Y = ch4_air_Y(mech, 1.0)[0]
+    y = np.concatenate([[1500.0], Y])
+    f1, _ = oracle.rhs_jac(y)
+    f2, _ = oracle.rhs_jac(y, gfac=2.0)
+    assert np.allclose(f2, 2.0 * f1, rtol=1e-13, atol=0)
