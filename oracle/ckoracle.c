@@ -433,6 +433,10 @@ typedef struct {
   rctx* ctx;
 } bdf;
 
+/* x^(1/p) for the step-size / order heuristics, in single precision as on the device
+ * (ckmi_reactor.hpp eta_root): it only selects the next step size. */
+static double eta_root(double x, int p) { return (double)exp2f(log2f((float)x) / (float)p); }
+
 static double wrms(const bdf* b, const double* v) {
   double s = 0.0;
   for (int i = 0; i < b->n; ++i) { double x = v[i] * b->ewt[i]; s += x * x; }
@@ -757,7 +761,7 @@ static int bdf_step(bdf* b, int* nst_global) {
     if (fabs(b->h) <= b->hmin * ONEPSM || nef == MXNEF) return 2;
     b->etamax = 1.0;
     if (nef <= MXNEF1) {
-      b->eta = 1.0 / (pow(BIAS2 * dsm, 1.0 / b->L) + ADDON);
+      b->eta = 1.0 / (eta_root(BIAS2 * dsm, b->L) + ADDON);
       b->eta = fmax(ETAMIN, fmax(b->eta, b->hmin / fabs(b->h)));
       if (nef >= SMALL_NEF) b->eta = fmin(b->eta, ETAMXF);
       rescale(b);
@@ -802,7 +806,7 @@ static int bdf_step(bdf* b, int* nst_global) {
     b->hprime = b->h;
     b->eta = 1.0;
   } else {
-    const double etaq = 1.0 / (pow(BIAS2 * dsm, 1.0 / b->L) + ADDON);
+    const double etaq = 1.0 / (eta_root(BIAS2 * dsm, b->L) + ADDON);
     if (b->qwait != 0) {
       b->eta = etaq;
       b->qprime = b->q;
@@ -811,13 +815,16 @@ static int bdf_step(bdf* b, int* nst_global) {
       double etaqm1 = 0.0, etaqp1 = 0.0;
       if (b->q > 1) {
         const double ddn = wrms(b, b->zn[b->q]) * b->tq[1];
-        etaqm1 = 1.0 / (pow(BIAS1 * ddn, 1.0 / b->q) + ADDON);
+        etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, b->q) + ADDON);
       }
       if (b->q != QMAX && b->saved_tq5 != 0.0) {
-        const double cquot = (b->tq[5] / b->saved_tq5) * pow(b->h / b->tau[2], (double)b->L);
+        const double hr = b->h / b->tau[2];
+        double hrL = hr;
+        for (int j = 1; j < b->L; ++j) hrL *= hr;
+        const double cquot = (b->tq[5] / b->saved_tq5) * hrL;
         for (int i = 0; i < b->n; ++i) b->tempv[i] = b->acor[i] - cquot * b->zn[QMAX][i];
         const double dup = wrms(b, b->tempv) * b->tq[3];
-        etaqp1 = 1.0 / (pow(BIAS3 * dup, 1.0 / (b->L + 1)) + ADDON);
+        etaqp1 = 1.0 / (eta_root(BIAS3 * dup, b->L + 1) + ADDON);
       }
       const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
       if (etam < THRESH) {

@@ -121,6 +121,7 @@ def test_drop_in_api_heat_loss_and_adaptive(chem):
     r.time = 5e-4
     r.tolerances = (1e-20, 1e-8)
     r.heat_loss_rate = 0.01
+    r.set_ignition_delay(method="T_rise", val=400)
     r.adaptive_solution_saving(True, steps=20)
     assert r.run() == 0
     r.process_solution()

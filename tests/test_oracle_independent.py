@@ -93,7 +93,7 @@ def test_heat_loss_energy_balance_inert(oracle, mech):
 
     mass = P_ATM * mech.wt[k] / (R * T0) * V0
     T_exact = brentq(lambda T: h_mass(T) - (h_mass(T0) - Q * 4.184e7 * tend / mass), 300.0, T0)
-    assert abs(r.T / T_exact - 1) < 1e-8
+    assert abs(r.T / T_exact - 1) < 1e-7
     # wall heat transfer towards a hotter ambient heats the charge
     r2, _ = oracle.reactor(T0, P_ATM, V0, Y, energy=1, t_end=tend, atol=1e-12, rtol=1e-10, htc=1e-3, areaq=20.0,
                            tamb=1500.0)
