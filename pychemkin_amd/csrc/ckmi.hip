@@ -34,7 +34,7 @@ enum { NF_FIRST = 0, NF_CONV_FAIL = 1, NF_ERR_FAIL = 2 };
 // Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py): per-reactor shader
 // cycles spent in each phase, written to a debug buffer no other code reads.
 // Slots 8..31 accumulate the cycles spent in each integrator state (RHS, LU, solve excluded).
-enum { PH_RHS = 0, PH_JAC = 1, PH_LU = 2, PH_SOLVE = 3, PH_TOTAL = 4, PH_STATE = 8, PH_N = 32 };
+enum { PH_RHS = 0, PH_JAC = 1, PH_LU = 2, PH_SOLVE = 3, PH_TOTAL = 4, PH_STATE = 8, PH_N = 48 };
 #ifdef CKMI_PHASE_TIMERS
 __device__ unsigned long long* g_phase_buf = nullptr;
 #define PH_T0() const unsigned long long _ph0 = __builtin_amdgcn_s_memtime()
@@ -150,7 +150,7 @@ struct Ctl {
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 __host__ __device__ constexpr int slice_vec_bytes(int G) { return align16(8 * (6 * VL + (G > 0 ? G : 1))); }
 #ifdef CKMI_PHASE_TIMERS
-constexpr int PH_SLICE = 8 * 32;  // per-state cycle counters of the wave
+constexpr int PH_SLICE = 8 * 40;  // per-state (0..19) and per-strip (24..29) cycle counters
 #else
 constexpr int PH_SLICE = 0;
 #endif
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
 #ifdef CKMI_PHASE_TIMERS
 #pragma unroll
           for (int k = 0; k < 8; ++k) ph[k] = 0;
-          if (lane < 32) phs[lane] = 0;
+          if (lane < 40) phs[lane] = 0;
           t_r0 = __builtin_amdgcn_s_memtime();
 #endif
           START_BEGIN(0.0, yl, crit_time(dcfg, c.tend, 0), cfg->h0);
@@ -894,13 +894,17 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
 #ifdef CKMI_PHASE_TIMERS
-    unsigned long long sub[3] = {0, 0, 0};
+    unsigned long long sub[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j, sub);
     ph[with_j ? PH_JAC : PH_RHS] += __builtin_amdgcn_s_memtime() - t0;
     if (!with_j) {
       ph[5] += sub[0];
       ph[6] += sub[1];
       ph[7] += sub[2];
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) phs[24 + k] += sub[3 + k];
+      }
     }
 #else
     fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j);
@@ -1050,7 +1054,7 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
                 const std::vector<double>& geff, const std::vector<double>& wt, const std::vector<double>& rwt) {
   const int KK = m->KK, IIp = m->IIpad, G = m->G;
   const int KKp = (KK + WAVE - 1) / WAVE * WAVE;
-  if (KK > 255) return fail(CKMI_ERR_UNSUPPORTED, "more than 255 species not supported by the mechanism image");
+  if (KK > SP_ONE) return fail(CKMI_ERR_UNSUPPORTED, "more than 63 species not supported by the mechanism image");
   std::vector<uint32_t> urs(IIp, 0), ups(IIp, 0), unu(IIp, 0), uinfo(IIp, 0);
   std::vector<double> aux;
   int naux = 0;
@@ -1059,24 +1063,30 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     uint32_t a = 0, b = 0, nu = 0;
     const int* r4 = &rsp[s].x;
     const int* p4 = &psp[s].x;
+    // unit-coefficient slots: a species with coefficient c occupies c slots
+    int ns_r = 0, ns_p = 0;
     for (int u = 0; u < nr; ++u) {
       const int c = (int)rnu[u * IIp + s];
-      if (c > 15) return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficient > 15");
-      a |= (uint32_t)r4[u] << (8 * u);
-      nu |= (uint32_t)c << (4 * u);
+      nu |= (uint32_t)std::min(c, 15) << (4 * u);
+      for (int k = 0; k < c; ++k, ++ns_r)
+        if (ns_r < 4) a |= (uint32_t)r4[u] << (8 * ns_r);
     }
     for (int u = 0; u < np; ++u) {
       const int c = (int)pnu[u * IIp + s];
-      if (c > 15) return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficient > 15");
-      b |= (uint32_t)p4[u] << (8 * u);
-      nu |= (uint32_t)c << (16 + 4 * u);
+      nu |= (uint32_t)std::min(c, 15) << (16 + 4 * u);
+      for (int k = 0; k < c; ++k, ++ns_p)
+        if (ns_p < 4) b |= (uint32_t)p4[u] << (8 * ns_p);
     }
+    if (ns_r > 4 || ns_p > 4)
+      return fail(CKMI_ERR_UNSUPPORTED, "more than 4 molecules (sum of coefficients) on a reaction side");
+    for (int u = ns_r; u < 4; ++u) a |= (uint32_t)SP_ONE << (8 * u);
+    for (int u = ns_p; u < 4; ++u) b |= (uint32_t)SP_ONE << (8 * u);
     urs[s] = a;
     ups[s] = b;
     unu[s] = nu;
     const int fl = flags[s];
     const int type = fl & 3;
-    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)nr << 7) | ((uint32_t)np << 10);
+    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10);
     if (slots[s] >= 0 && (type == 2 || (fl & 8))) {
       double rec[AUXW] = {lnA0[s], beta0[s], Ea0[s], fp[0 * IIp + s], fp[1 * IIp + s], fp[2 * IIp + s],
                           fp[3 * IIp + s], fp[4 * IIp + s], rlnA[s], rbeta[s], rEa[s], 0.0};
@@ -1139,6 +1149,11 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   for (int g = 0; g < G; ++g)
     for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)g * KKp + gsp[e]] = geff[e];
   I.o_geffd = put(geffd.data(), geffd.size() * 8);
+  {
+    double e2t[64];
+    for (int j = 0; j < 64; ++j) e2t[j] = (double)std::exp2((long double)j / 64.0L);
+    I.o_e2t = put(e2t, sizeof(e2t));
+  }
   I.bytes = (int)blob.size();
   {
     const int* so = nullptr;

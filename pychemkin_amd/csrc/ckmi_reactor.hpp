@@ -95,21 +95,21 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// J[1+k][1+j] += nu_k dq W_k / W_j for every participant k of one reaction (column-major
-// shared scratch Jsh[col * LDJ + row]).
+// J[1+k][1+j] += (+/-) dq W_k / W_j for every (unit-coefficient) slot k of one reaction
+// (column-major shared scratch Jsh[col * LDJ + row]).
 __device__ __forceinline__ void jac_scatter(const MechView& V, int oJ, int nr, int np, uint32_t rs, uint32_t ps,
-                                            uint32_t nuw, int j, double dq) {
+                                            int j, double dq) {
   double* col = lds_at<double>(oJ) + (1 + j) * LDJ + 1;
   const double dqw = dq * V.rwt()[j];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     if (u < nr) {
       const int k = sp_of(rs, u);
-      atomicAdd(&col[k], -nur_of(nuw, u) * dqw * V.wt()[k]);
+      atomicAdd(&col[k], -dqw * V.wt()[k]);
     }
     if (u < np) {
       const int k = sp_of(ps, u);
-      atomicAdd(&col[k], nup_of(nuw, u) * dqw * V.wt()[k]);
+      atomicAdd(&col[k], dqw * V.wt()[k]);
     }
   }
 }
@@ -122,7 +122,7 @@ __device__ __forceinline__ void jac_scatter(const MechView& V, int oJ, int nr, i
 __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R, double t, double yl,
                                               const WaveLds& L, int oJ, int lane, int ncol, bool with_j
 #ifdef CKMI_PHASE_TIMERS
-                                              , unsigned long long (&sub)[3]
+                                              , unsigned long long (&sub)[9]
 #endif
 ) {
 #ifdef CKMI_PHASE_TIMERS
@@ -144,7 +144,8 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const double Yk = isp ? yl : 0.0;
   const double rw = isp ? V.rwt()[s] : 0.0;
   const double Wk = isp ? V.wt()[s] : 0.0;
-  const double Wbar = 1.0 / wave_sum(Yk * rw);
+  const double sumYW = wave_sum(Yk * rw);
+  const double Wbar = 1.0 / sumYW;
   const int conp = R.conp;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
   if (conp) {
@@ -168,8 +169,12 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     L.wdot()[s] = 0.0;
     L.hRT()[s] = th.hRT;
     L.dwdT()[s] = 0.0;
+  } else if (lane == 0) {  // the dummy slot of the unit-coefficient reaction tables
+    C[SP_ONE] = 1.0;
+    L.gRT()[SP_ONE] = 0.0;
+    L.hRT()[SP_ONE] = 0.0;
   }
-  const double Ctot = wave_sum(Ck);
+  const double Ctot = rho * sumYW;  // = sum_k C_k, without a second reduction
   double* Jsh = lds_at<double>(oJ);
   if (with_j) {
     for (int idx = lane; idx < ncol * LDJ; idx += WAVE) Jsh[idx] = 0.0;
@@ -204,16 +209,24 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     const int i = base + lane;
     const uint32_t inf = V.info()[i];
     const int nr = rx_nr(inf), np = rx_np(inf);
-    if (nr + np == 0) continue;
-    const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
-    const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false,
-                               R.pslot, R.plnf, R.gfac);
-    const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
+    if (nr + np != 0) {
+      const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
+      const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false,
+                                 R.pslot, R.plnf, R.gfac);
+      const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (u < nr) atomicAdd(&L.wdot()[sp_of(rs, u)], -nur_of(nuw, u) * q);
-      if (u < np) atomicAdd(&L.wdot()[sp_of(ps, u)], nup_of(nuw, u) * q);
+      for (int u = 0; u < 4; ++u) {
+        if (u < nr) atomicAdd(&L.wdot()[sp_of(rs, u)], -q);
+        if (u < np) atomicAdd(&L.wdot()[sp_of(ps, u)], q);
+      }
     }
+#ifdef CKMI_PHASE_TIMERS
+    if (base / WAVE < 6) {
+      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+      sub[3 + base / WAVE] += t2 - tsub;
+      tsub = t2;
+    }
+#endif
   }
   if (with_j) {
     for (int base = 0; base < IIp; base += WAVE) {
@@ -227,39 +240,33 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
       double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
       if (conp) {
-        int ordf = 0, ordr = 0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (u < nr) ordf += nur_of(nuw, u);
-          if (u < np) ordr += nup_of(nuw, u);
-        }
+        const int ordf = nr, ordr = np;  // unit-coefficient slots
         dqdT -= e.mfac * (ordf * e.kf * e.pf - ordr * e.kr * e.pr) * invT;
         if (rx_type(inf) == 1) dqdT -= q * invT;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (u < nr) atomicAdd(&L.dwdT()[sp_of(rs, u)], -nur_of(nuw, u) * dqdT);
-        if (u < np) atomicAdd(&L.dwdT()[sp_of(ps, u)], nup_of(nuw, u) * dqdT);
+        if (u < nr) atomicAdd(&L.dwdT()[sp_of(rs, u)], -dqdT);
+        if (u < np) atomicAdd(&L.dwdT()[sp_of(ps, u)], dqdT);
       }
-      // dq/dC_j for every reactant slot (forward) and product slot (reverse)
+      // dq/dC_j for every reactant slot (forward) and product slot (reverse): the product of
+      // the other three slots' concentrations (a species in two slots contributes twice)
+      const int r0 = sp_of(rs, 0), r1 = sp_of(rs, 1), r2 = sp_of(rs, 2), r3 = sp_of(rs, 3);
+      const int p0 = sp_of(ps, 0), p1 = sp_of(ps, 1), p2 = sp_of(ps, 2), p3 = sp_of(ps, 3);
+      const double kf = e.mfac * e.kf, kr = -e.mfac * e.kr;
+      if (e.kf != 0.0) {
+        const double c0 = C[r0], c1 = C[r1], c2 = C[r2], c3 = C[r3];
+        const double d[4] = {c1 * c2 * c3, c0 * c2 * c3, c0 * c1 * c3, c0 * c1 * c2};
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl) {
-        if (sl < nr && e.kf != 0.0) {
-          const int nus = nur_of(nuw, sl);
-          double d = nus * powi(C[sp_of(rs, sl)], nus - 1);
+        for (int sl = 0; sl < 4; ++sl)
+          if (sl < nr) jac_scatter(V, oJ, nr, np, rs, ps, sp_of(rs, sl), kf * d[sl]);
+      }
+      if (e.kr != 0.0) {
+        const double c0 = C[p0], c1 = C[p1], c2 = C[p2], c3 = C[p3];
+        const double d[4] = {c1 * c2 * c3, c0 * c2 * c3, c0 * c1 * c3, c0 * c1 * c2};
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (u < nr && u != sl) d *= powi(C[sp_of(rs, u)], nur_of(nuw, u));
-          jac_scatter(V, oJ, nr, np, rs, ps, nuw, sp_of(rs, sl), e.mfac * e.kf * d);
-        }
-        if (sl < np && e.kr != 0.0) {
-          const int nus = nup_of(nuw, sl);
-          double d = nus * powi(C[sp_of(ps, sl)], nus - 1);
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-            if (u < np && u != sl) d *= powi(C[sp_of(ps, u)], nup_of(nuw, u));
-          jac_scatter(V, oJ, nr, np, rs, ps, nuw, sp_of(ps, sl), -e.mfac * e.kr * d);
-        }
+        for (int sl = 0; sl < 4; ++sl)
+          if (sl < np) jac_scatter(V, oJ, nr, np, rs, ps, sp_of(ps, sl), kr * d[sl]);
       }
     }
   }

@@ -32,7 +32,7 @@ def main():
     T0, P0, Y0 = bench.sweep(mech, 1, 0)
     prob, V0 = np.ones(len(T0), np.int32), np.ones(len(T0))
     idx = np.arange(0, len(T0), max(1, len(T0) // n))[:n]
-    buf = torch.zeros((len(idx), 32), dtype=torch.int64, device="cuda:0")
+    buf = torch.zeros((len(idx), 48), dtype=torch.int64, device="cuda:0")
     L = _native.lib()
     L.ckmi_debug_phase_buffer.argtypes = [ct.c_void_p]
     assert L.ckmi_debug_phase_buffer(buf.data_ptr()) == 0
@@ -55,6 +55,7 @@ def main():
               "STEP_COMPLETE", "STEP_END", "FINISH"]
     out["state_cycles_per_step"] = {nm: float(ph[:, 8 + k].mean() / out["mean_steps"]) for k, nm in enumerate(states)
                                     if ph[:, 8 + k].any()}
+    out["rhs_strip_cycles_per_call"] = [float(ph[:, 8 + 24 + k].sum() / max(counts["rhs"].sum(), 1)) for k in range(6)]
     acc = sum(out[nm + "_cycles"] for nm in names[:4])
     out["other_cycles"] = out["total_cycles"] - acc
     out["cycles_per_step"] = out["total_cycles"] / out["mean_steps"]
