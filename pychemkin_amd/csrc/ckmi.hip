@@ -915,87 +915,94 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
 }
 
 // ---------------------------------------------------------------- ROP kernels
-// One wave per state (lanes over reactions), SoA inputs [KK][n].
+// Persistent grid of ROP_WAVES-wave workgroups; the workgroup stages the mechanism image in LDS
+// once, each wave then takes tasks of ROP_CHUNK consecutive states and evaluates them one at a
+// time (lanes over species for thermo, over reactions for the rates).  Consecutive states of one
+// wave touch the same cache lines of the species-major inputs / outputs ([KK][n]), so each line
+// is fetched once by one XCD and partial-line writes merge in its L2 (one state per workgroup
+// spread consecutive states over all 8 XCDs: 4-8x HBM traffic, measured).
+constexpr int ROP_WAVES = 8;
+constexpr int ROP_CHUNK = 16;
+__host__ __device__ constexpr int rop_slice_bytes(int G) { return align16(8 * (3 * VL + (G > 0 ? G : 1))); }
+
 template <int MODE>  // 0: wdot + cp + h, 1: qf / qr
-__global__ __launch_bounds__(WAVE) void rop_kernel(MechDev M, int nstate, const double* __restrict__ Tv,
-                                                   const double* __restrict__ Pv, const double* __restrict__ Yv,
-                                                   double* __restrict__ o0, double* __restrict__ o1,
-                                                   double* __restrict__ o2) {
-  extern __shared__ double lds[];
-  const int st = blockIdx.x;
-  if (st >= nstate) return;
-  const int lane = threadIdx.x;
-  const int KK = M.KK;
-  const int VL = (KK + WAVE - 1) / WAVE * WAVE;
-  double* C = lds;
+__global__ __launch_bounds__(ROP_WAVES* WAVE) void rop_kernel(MechImage img, const int* __restrict__ orig, int nstate,
+                                                               const double* __restrict__ Tv,
+                                                               const double* __restrict__ Pv,
+                                                               const double* __restrict__ Yv, double* __restrict__ o0,
+                                                               double* __restrict__ o1, double* __restrict__ o2) {
+  stage_image(0, img);
+  const MechView V = make_view(0, img);
+  const int wid = threadIdx.x / WAVE;
+  const int lane = threadIdx.x % WAVE;
+  const int oC = img.bytes + wid * rop_slice_bytes(img.G);
+  double* C = lds_at<double>(oC);
   double* gRT = C + VL;
   double* wdot = gRT + VL;
   double* Mg = wdot + VL;
-  const double T = Tv[st], P = Pv[st];
-  double yk[2] = {0.0, 0.0};  // up to 128 species per state
-  double rwv[2] = {0.0, 0.0};
-  double s = 0.0;
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int k = lane + c * WAVE;
-    if (k < KK) {
-      yk[c] = Yv[(size_t)k * nstate + st];
-      rwv[c] = M.rwt[k];
-      s += yk[c] * rwv[c];
-    }
-  }
-  const double Wbar = 1.0 / wave_sum(s);
-  const double rho = P * Wbar / (RU * T);
-  const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
-  double cpm = 0.0, hm = 0.0, ctot = 0.0;
-  for (int k = lane; k < KK; k += WAVE) {
-    const int c = k / WAVE;
-    const SpThermo th = nasa7(M, k, T, lnT);
-    const double Ck = rho * yk[c] * rwv[c];
-    C[k] = Ck;
-    gRT[k] = th.hRT - th.sR;
-    wdot[k] = 0.0;
-    ctot += Ck;
-    cpm += yk[c] * th.cpR * RU * rwv[c];
-    hm += yk[c] * th.hRT * RU * T * rwv[c];
-  }
-  const double Ctot = wave_sum(ctot);
-  __syncthreads();
-  for (int g = lane; g < M.G; g += WAVE) {
-    double m = Ctot;
-    for (int p = M.gptr[g]; p < M.gptr[g + 1]; ++p) m += M.geff[p] * C[M.gsp[p]];
-    Mg[g] = m;
-  }
-  __syncthreads();
-  const int IIp = M.IIpad;
-  for (int base = 0; base < IIp; base += WAVE) {
-    const int i = base + lane;
-    const int nrp = M.nrp[i];
-    const int nr = nrp & 0xff, np = nrp >> 8;
-    if (nr + np == 0) continue;
-    const RxnEval e = eval_rxn(M, i, T, lnT, invT, lnPRT, C, gRT, nullptr, Mg, false);
-    const double qf = e.mfac * e.kf * e.pf, qr = e.mfac * e.kr * e.pr;
-    if (MODE == 1) {
-      const int oi = M.orig[i];
-      o0[(size_t)oi * nstate + st] = qf;
-      o1[(size_t)oi * nstate + st] = qr;
-    } else {
-      const double q = qf - qr;
-      const int4 rs = M.rsp[i], ps = M.psp[i];
-#pragma unroll
-      for (int u = 0; u < SLOTS; ++u) {
-        if (u < nr) atomicAdd(&wdot[slot(rs, u)], -M.rnu[u * IIp + i] * q);
-        if (u < np) atomicAdd(&wdot[slot(ps, u)], M.pnu[u * IIp + i] * q);
+  const int KK = V.KK;
+  const bool isp = lane < KK;
+  const double rw = isp ? V.rwt()[lane] : 0.0;
+  const int ntask = (nstate + ROP_CHUNK - 1) / ROP_CHUNK;
+  for (int task = blockIdx.x * ROP_WAVES + wid; task < ntask; task += gridDim.x * ROP_WAVES) {
+    const int s1 = min(nstate, (task + 1) * ROP_CHUNK);
+    for (int st = task * ROP_CHUNK; st < s1; ++st) {
+      const double T = Tv[st], P = Pv[st];
+      const double yk = isp ? Yv[(size_t)lane * nstate + st] : 0.0;
+      const double sumYW = wave_sum(yk * rw);
+      const double rho = P / (RU * T * sumYW);
+      const double lnT = log(T), invT = 1.0 / T, lnPRT = LN_PATM_RU - lnT;
+      double cpm = 0.0, hm = 0.0;
+      if (isp) {
+        const Thermo7 th = nasa7_img(V, lane, T, lnT, invT);
+        C[lane] = rho * yk * rw;
+        gRT[lane] = th.hRT - th.sR;
+        wdot[lane] = 0.0;
+        cpm = yk * th.cpR * RU * rw;
+        hm = yk * th.hRT * RU * T * rw;
+      } else if (lane == SP_ONE) {
+        C[SP_ONE] = 1.0;
+        gRT[SP_ONE] = 0.0;
       }
-    }
-  }
-  if (MODE == 0) {
-    __syncthreads();
-    for (int k = lane; k < KK; k += WAVE) o0[(size_t)k * nstate + st] = wdot[k];
-    const double cps = wave_sum(cpm), hs = wave_sum(hm);
-    if (lane == 0) {
-      if (o1) o1[st] = cps;
-      if (o2) o2[st] = hs;
+      const double Ctot = rho * sumYW;
+      wave_lds_sync();
+      for (int g = lane; g < V.G; g += WAVE) {
+        double m = Ctot;
+        for (int p = V.gptr()[g]; p < V.gptr()[g + 1]; ++p) m += V.geff()[p] * C[V.gsp()[p]];
+        Mg[g] = m;
+      }
+      wave_lds_sync();
+      for (int base = 0; base < V.IIp; base += WAVE) {
+        const int i = base + lane;
+        const uint32_t inf = V.info()[i];
+        const int nr = rx_nr(inf), np = rx_np(inf);
+        if (nr + np == 0) continue;
+        const uint32_t rs = V.rsp()[i], ps = V.psp()[i];
+        const Rxn e = eval_rxn_img(V, i, inf, rs, ps, 0u, T, lnT, invT, lnPRT, C, gRT, gRT, Mg, false);
+        const double qf = e.mfac * e.kf * e.pf, qr = e.mfac * e.kr * e.pr;
+        if (MODE == 1) {
+          const int oi = orig[i];
+          o0[(size_t)oi * nstate + st] = qf;
+          o1[(size_t)oi * nstate + st] = qr;
+        } else {
+          const double q = qf - qr;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (u < nr) atomicAdd(&wdot[sp_of(rs, u)], -q);
+            if (u < np) atomicAdd(&wdot[sp_of(ps, u)], q);
+          }
+        }
+      }
+      if (MODE == 0) {
+        wave_lds_sync();
+        if (isp) o0[(size_t)lane * nstate + st] = wdot[lane];
+        const double cps = wave_sum(cpm), hs = wave_sum(hm);
+        if (lane == 0) {
+          if (o1) o1[st] = cps;
+          if (o2) o2[st] = hs;
+        }
+      }
+      wave_lds_sync();  // the next state overwrites C / gRT / wdot
     }
   }
 }
@@ -1200,9 +1207,20 @@ int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t 
   return CKMI_OK;
 }
 
-size_t rop_lds_bytes(int KK, int G) {
-  const int VL = (KK + WAVE - 1) / WAVE * WAVE;
-  return sizeof(double) * (size_t)(3 * VL + std::max(G, 1));
+template <int MODE>
+int launch_rop(const ckmi_mech* m, int n, const double* T, const double* P, const double* Y, double* o0, double* o1,
+               double* o2, hipStream_t stream) {
+  const size_t lds = (size_t)m->img.bytes + (size_t)ROP_WAVES * rop_slice_bytes(m->G);
+  int ncu = 0, per_cu = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rop_kernel<MODE>, ROP_WAVES * WAVE, lds));
+  if (per_cu < 1) return fail(CKMI_ERR_SIZE, "ROP kernel does not fit on a CU");
+  const int tasks = (n + ROP_CHUNK - 1) / ROP_CHUNK;
+  const int grid = std::max(1, std::min(ncu * per_cu, (tasks + ROP_WAVES - 1) / ROP_WAVES));
+  hipLaunchKernelGGL(rop_kernel<MODE>, dim3(grid), dim3(ROP_WAVES * WAVE), lds, stream, m->img, m->d.orig, n, T, P, Y,
+                     o0, o1, o2);
+  HIP_CHECK(hipGetLastError());
+  return CKMI_OK;
 }
 
 }  // namespace
@@ -1452,20 +1470,14 @@ int ckmi_rop_thermo(const ckmi_mech* m, int32_t n, const double* T, const double
                     double* cp, double* h, void* stream) {
   if (!m || n < 0 || !wdot) return fail(CKMI_ERR_ARG, "bad argument");
   if (n == 0) return CKMI_OK;
-  hipLaunchKernelGGL(rop_kernel<0>, dim3(n), dim3(WAVE), rop_lds_bytes(m->KK, m->G), (hipStream_t)stream, m->d, n, T, P,
-                     Y, wdot, cp, h);
-  HIP_CHECK(hipGetLastError());
-  return CKMI_OK;
+  return launch_rop<0>(m, n, T, P, Y, wdot, cp, h, (hipStream_t)stream);
 }
 
 int ckmi_reaction_rates(const ckmi_mech* m, int32_t n, const double* T, const double* P, const double* Y, double* qf,
                         double* qr, void* stream) {
   if (!m || n < 0 || !qf || !qr) return fail(CKMI_ERR_ARG, "bad argument");
   if (n == 0) return CKMI_OK;
-  hipLaunchKernelGGL(rop_kernel<1>, dim3(n), dim3(WAVE), rop_lds_bytes(m->KK, m->G), (hipStream_t)stream, m->d, n, T, P,
-                     Y, qf, qr, (double*)nullptr);
-  HIP_CHECK(hipGetLastError());
-  return CKMI_OK;
+  return launch_rop<1>(m, n, T, P, Y, qf, qr, nullptr, (hipStream_t)stream);
 }
 
 int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t n, const int32_t* problem,

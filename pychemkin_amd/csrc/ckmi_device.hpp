@@ -1,9 +1,8 @@
 // ckmi_device.hpp -- device-side building blocks for gfx950 (CDNA4, wave64).
 //
-// Execution model: one 64-lane wavefront owns one reactor (or one state for the ROP
-// kernels).  Lane l holds component l of the ODE state y = (T, Y_1..Y_KK); the reaction
-// loop is strip-mined over the 64 lanes; species production and the analytic Jacobian are
-// assembled in LDS; the Newton iteration matrix is LU-factored row-per-lane in VGPRs.
+// Wave utilities (DPP reductions, broadcasts) and the global-memory mechanism tables (MechDev,
+// used by the thread-per-state species-thermo kernel and for the reaction-order map; the rate
+// kernels read the LDS image of ckmi_image.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -99,20 +98,6 @@ __device__ __forceinline__ double wave_max(double v) {
   return uni(fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48))));
 }
 
-// C^nu for the integral stoichiometric coefficients accepted by ckmi_mech_create
-__device__ __forceinline__ double powi_nu(double c, double nu) {
-  if (nu == 1.0) return c;
-  if (nu == 2.0) return c * c;
-  if (nu == 0.0) return 1.0;
-  double r = c * c * c;
-  for (int k = 3; k < (int)nu; ++k) r *= c;
-  return r;
-}
-
-__device__ __forceinline__ int slot(const int4& v, int s) {
-  return s == 0 ? v.x : (s == 1 ? v.y : (s == 2 ? v.z : v.w));
-}
-
 // ------------------------------------------------------------------ thermo (NASA-7)
 struct SpThermo {
   double cpR, hRT, sR;
@@ -130,96 +115,6 @@ __device__ __forceinline__ SpThermo nasa7(const MechDev& M, int k, double T, dou
   r.hRT = a0 + a1 * T / 2 + a2 * T2 / 3 + a3 * T3 / 4 + a4 * T4 / 5 + a5 / T;
   r.sR = a0 * lnT + a1 * T + a2 * T2 / 2 + a3 * T3 / 3 + a4 * T4 / 4 + a6;
   return r;
-}
-
-// ------------------------------------------------------------------ one reaction
-struct RxnEval {
-  double kf, kr, mfac, pf, pr, dlkf, dlkr;
-};
-
-// Rate coefficients and concentration products of device reaction slot i at (T, C).
-// C, gRT, hRT, Mg live in LDS.  Mirrors oracle/ckoracle.c eval_reaction().
-__device__ __forceinline__ RxnEval eval_rxn(const MechDev& M, int i, double T, double lnT, double invT,
-                                            double lnPRT, const double* C, const double* gRT, const double* hRT,
-                                            const double* Mg, bool need_h) {
-  const int fl = M.flags[i];
-  const int type = fl & 3;
-  const int nrp = M.nrp[i];
-  const int nr = nrp & 0xff, np = nrp >> 8;
-  const int4 rs = M.rsp[i], ps = M.psp[i];
-  const int IIp = M.IIpad;
-  const double lnA = M.lnA[i], b = M.beta[i], Ea = M.Ea[i];
-  double kf = exp(lnA + b * lnT - Ea * invT);
-  const double dlkf = (b + Ea * invT) * invT;
-  double mfac = 1.0;
-  if (type != 0) {
-    const int tb = M.tb[i];
-    const double Mc = tb >= 0 ? Mg[tb] : C[-tb - 2];
-    if (type == 1) {
-      mfac = Mc;
-    } else {
-      const double k0 = exp(M.lnA0[i] + M.beta0[i] * lnT - M.Ea0[i] * invT);
-      const double Pr = k0 * Mc / kf;
-      double F = 1.0;
-      const int ft = (fl >> 4) & 7;
-      if (ft == 2 || ft == 3) {
-        const double fa = M.fp[0 * IIp + i], T3s = M.fp[1 * IIp + i], T1s = M.fp[2 * IIp + i];
-        double Fcent = (1.0 - fa) * exp(-T / T3s) + fa * exp(-T / T1s);
-        if (ft == 3) Fcent += exp(-M.fp[3 * IIp + i] * invT);
-        const double lFc = log10(Fcent > 1e-300 ? Fcent : 1e-300);
-        const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
-        const double c = -0.4 - 0.67 * lFc, nn = 0.75 - 1.27 * lFc;
-        const double f1 = (lPr + c) / (nn - 0.14 * (lPr + c));
-        F = exp10(lFc / (1.0 + f1 * f1));
-      } else if (ft == 4) {
-        const double lPr = log10(Pr > 1e-300 ? Pr : 1e-300);
-        const double X = 1.0 / (1.0 + lPr * lPr);
-        F = M.fp[3 * IIp + i] * pow(M.fp[0 * IIp + i] * exp(-M.fp[1 * IIp + i] * invT) + exp(-T / M.fp[2 * IIp + i]), X) *
-            pow(T, M.fp[4 * IIp + i]);
-      }
-      kf = kf * (Pr / (1.0 + Pr)) * F;
-    }
-  }
-  double kr = 0.0, dlkr = 0.0;
-  if ((fl >> 2) & 1) {
-    if ((fl >> 3) & 1) {
-      kr = exp(M.rlnA[i] + M.rbeta[i] * lnT - M.rEa[i] * invT);
-      if (type == 2) kr *= kf / exp(lnA + b * lnT - Ea * invT);
-      dlkr = (M.rbeta[i] + M.rEa[i] * invT) * invT;
-    } else {
-      double dG = 0.0, dH = 0.0;
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        if (s < nr) {
-          const int k = slot(rs, s);
-          const double nu = M.rnu[s * IIp + i];
-          dG -= nu * gRT[k];
-          if (need_h) dH -= nu * hRT[k];
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        if (s < np) {
-          const int k = slot(ps, s);
-          const double nu = M.pnu[s * IIp + i];
-          dG += nu * gRT[k];
-          if (need_h) dH += nu * hRT[k];
-        }
-      }
-      const double dnu = M.dnu[i];
-      kr = kf * exp(dG - dnu * lnPRT);
-      dlkr = dlkf - (dH - dnu) * invT;
-    }
-  }
-  double pf = 1.0, pr = 1.0;
-#pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
-    if (s < nr) pf *= powi_nu(C[slot(rs, s)], M.rnu[s * IIp + i]);
-    if (s < np) pr *= powi_nu(C[slot(ps, s)], M.pnu[s * IIp + i]);
-  }
-  RxnEval e;
-  e.kf = kf; e.kr = kr; e.mfac = mfac; e.pf = pf; e.pr = pr; e.dlkf = dlkf; e.dlkr = dlkr;
-  return e;
 }
 
 }  // namespace ckmi

@@ -151,7 +151,7 @@ __device__ __forceinline__ double fexp(double x, const double* e2t) {
 struct Thermo7 {
   double cpR, hRT, sR;
 };
-__device__ __forceinline__ Thermo7 nasa7_img(const MechView& V, int k, double T, double lnT) {
+__device__ __forceinline__ Thermo7 nasa7_img(const MechView& V, int k, double T, double lnT, double invT) {
   const int KKp = V.KKp;
   const double* t = V.th() + k;
   // both ranges are loaded (independent LDS reads) and selected, instead of a load that waits
@@ -161,11 +161,11 @@ __device__ __forceinline__ Thermo7 nasa7_img(const MechView& V, int k, double T,
 #pragma unroll
   for (int c = 0; c < 7; ++c) a[c] = hi ? t[(8 + c) * KKp] : t[(1 + c) * KKp];
   const double a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3], a4 = a[4], a5 = a[5], a6 = a[6];
-  const double T2 = T * T, T3 = T2 * T, T4 = T3 * T;
+  // Horner forms with the 1/2 ... 1/5 factors as multiplications (no FP64 divisions)
   Thermo7 r;
-  r.cpR = a0 + a1 * T + a2 * T2 + a3 * T3 + a4 * T4;
-  r.hRT = a0 + a1 * T / 2 + a2 * T2 / 3 + a3 * T3 / 4 + a4 * T4 / 5 + a5 / T;
-  r.sR = a0 * lnT + a1 * T + a2 * T2 / 2 + a3 * T3 / 3 + a4 * T4 / 4 + a6;
+  r.cpR = fma(T, fma(T, fma(T, fma(T, a4, a3), a2), a1), a0);
+  r.hRT = fma(T, fma(T, fma(T, fma(T, a4 * 0.2, a3 * 0.25), a2 * (1.0 / 3.0)), a1 * 0.5), a0) + a5 * invT;
+  r.sR = fma(a0, lnT, fma(T, fma(T, fma(T, fma(T, a4 * 0.25, a3 * (1.0 / 3.0)), a2 * 0.5), a1), a6));
   return r;
 }
 

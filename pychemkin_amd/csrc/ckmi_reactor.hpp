@@ -163,7 +163,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   th.cpR = th.hRT = th.sR = 0.0;
   double* C = L.C();
   if (isp) {
-    th = nasa7_img(V, s, T, lnT);
+    th = nasa7_img(V, s, T, lnT, invT);
     C[s] = Ck;
     L.gRT()[s] = th.hRT - th.sR;
     L.wdot()[s] = 0.0;
