@@ -74,6 +74,19 @@ def ch4_air_Y(mech, phi):
     return Y / Y.sum(axis=1, keepdims=True)
 
 
+def sweep_c4(mech, world, rank):
+    """configs[3]: 128 T0 x 64 phi x 64 P x {CONP, CONV} = 2^20 reactors in total, strided over ranks
+    (strong scaling: the total is fixed).  problem = CONP for even, CONV for odd global index."""
+    T = 1100.0 + 600.0 * np.arange(128) / 127
+    phi = 0.5 + 1.5 * np.arange(64) / 63
+    P = P_ATM * 10.0 ** (2.0 * np.arange(64) / 63)
+    TT, FF, PP = np.meshgrid(T, phi, P, indexing="ij")
+    TT, FF, PP = np.repeat(TT.ravel(), 2), np.repeat(FF.ravel(), 2), np.repeat(PP.ravel(), 2)
+    prob = np.tile(np.array([1, 2], np.int32), TT.size // 2)
+    sel = slice(rank, None, world)
+    return TT[sel], PP[sel], ch4_air_Y(mech, FF[sel]), prob[sel]
+
+
 def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
     """Rank's shard of the (64*world) x 32 x 32 ignition sweep (configs[2] at world = 1)."""
     T_all = 1100.0 + 600.0 * np.arange(nT * world) / (nT * world - 1)
@@ -98,6 +111,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+                    help="c3: configs[2], 65,536 CONP reactors per GPU (weak scaling, the metric); "
+                         "c4: configs[3], 2^20 CONP+CONV reactors in total (strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,15 +129,19 @@ def main():
     ops = count_ops(tables)
     dm = _native.DeviceMechanism(tables, device=dev)
 
-    T0, P0, Y0 = sweep(mech, world, rank)
+    if args.workload == "c4":
+        T0, P0, Y0, prob = sweep_c4(mech, world, rank)
+    else:
+        T0, P0, Y0 = sweep(mech, world, rank)
+        prob = np.ones(len(T0), np.int32)
     if args.reactors:
-        T0, P0, Y0 = T0[: args.reactors], P0[: args.reactors], Y0[: args.reactors]
+        T0, P0, Y0, prob = T0[: args.reactors], P0[: args.reactors], Y0[: args.reactors], prob[: args.reactors]
     n = len(T0)
     T0_d = torch.as_tensor(T0, device=dev)
     P0_d = torch.as_tensor(P0, device=dev)
     V0_d = torch.ones(n, dtype=torch.float64, device=dev)
     Y0_d = torch.as_tensor(Y0, device=dev).contiguous()
-    prob_d = torch.ones(n, dtype=torch.int32, device=dev)
+    prob_d = torch.as_tensor(prob, device=dev)
     cfg = _native.make_cfg(**RUN)
     out = dict(tau=torch.empty(n, dtype=torch.float64, device=dev), T=torch.empty(n, dtype=torch.float64, device=dev),
                P=torch.empty(n, dtype=torch.float64, device=dev), V=torch.empty(n, dtype=torch.float64, device=dev),
@@ -212,7 +232,7 @@ def main():
         while done < order.size and tcpu < args.cpu_seconds:
             idx = order[done: done + chunk]
             tc = time.perf_counter()
-            nfail, cres, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=np.ones(len(idx), np.int32),
+            nfail, cres, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=prob[idx],
                                                V0=np.ones(len(idx)), nthreads=threads, **RUN)
             tcpu += time.perf_counter() - tc
             ctau = np.array([r.tau for r in cres])
@@ -234,11 +254,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": tmax / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "weak" if args.workload == "c3" else "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": "configs[2]: GRI-3.0 CONP CH4/air ignition sweep 64 T0 x 32 phi x 32 P per GPU",
+            "config": {"workload": ("configs[2]: GRI-3.0 CONP CH4/air ignition sweep 64 T0 x 32 phi x 32 P per GPU"
+                                    if args.workload == "c3" else
+                                    "configs[3]: GRI-3.0 CH4/air 128 T0 x 64 phi x 64 P x {CONP, CONV} = 2^20 "
+                                    "reactors in total"),
                        "reactors_per_gpu": n, "t_end_s": 1.0, "atol": 1e-10, "rtol": 1e-8, "ignition": "TIFP",
                        "parallelism": f"shard-by-condition x{world}"},
             "reactors_per_min": value * 60.0,

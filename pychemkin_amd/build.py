@@ -7,7 +7,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "ckmi.hip")
-DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp")] + [
+DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp", "ckmi_image.hpp")] + [
     os.path.join(HERE, "..", "include", "ckmi.h")]
 OUT = os.path.join(HERE, "_lib", "libckmi.so")
 ARCH = "gfx950"  # MI355X only
