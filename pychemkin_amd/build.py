@@ -17,7 +17,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # constants and addresses out of the integrator loop, keep them live across the RHS and then
 # spill them to scratch (284 -> 16 B/lane of scratch, +29 % reactors/s measured A/B on MI355X).
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics", "-mcode-object-version=5",
-         f"--offload-arch={ARCH}", "-mllvm", "-disable-machine-licm", "-mllvm", "-disable-machine-sink"]
+         f"--offload-arch={ARCH}", "-mllvm", "-disable-machine-licm", "-mllvm", "-disable-machine-sink",
+         # the Gauss-Jordan factorisation is a fully unrolled 54 x 54 loop nest (a[] must stay in VGPRs)
+         "-mllvm", "-pragma-unroll-threshold=2000000"]
 
 
 def needs_build() -> bool:

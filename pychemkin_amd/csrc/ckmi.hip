@@ -156,7 +156,7 @@ constexpr int PH_SLICE = 0;
 #endif
 __host__ __device__ constexpr int slice_bytes(int G) {
   return slice_vec_bytes(G) + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)) +
-         PH_SLICE;
+         align16((int)sizeof(RunCtx)) + ZN_BYTES + PH_SLICE;
 }
 template <int N>
 __host__ __device__ constexpr int jscratch_bytes() {
@@ -225,17 +225,21 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
   const int n = KK + 1;
   const bool isp = lane >= 1 && lane <= KK;
   const bool act = lane < n;
-  RunCtx R;
+  // per-reactor constants of the RHS: in LDS, not registers (the Newton matrix owns those)
+  RunCtx& R = *lds_at<RunCtx>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)));
   R.cfg = cfg;
   NewtonMatrix<N> M;
   Bdf b;
+  b.zn.base = oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)) +
+              align16((int)sizeof(RunCtx)) + lane * 8;
   double fe = 0.0, y_e = 0.0, t_e = 0.0;
   bool with_j = false;
 #ifdef CKMI_PHASE_TIMERS
   unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long t_r0 = 0;
   unsigned long long* phs = lds_at<unsigned long long>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) +
-                                                     align16((int)sizeof(Ign)));
+                                                     align16((int)sizeof(Ign)) + align16((int)sizeof(RunCtx)) +
+                                                     ZN_BYTES);
 #endif
   int st = ST_NEXT;
 
@@ -541,7 +545,21 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
 #endif
           // each lane reads back only the J entries it wrote itself (same-address order)
           M.build(Jg, WAVE, S.gamma, lane, n);
+#ifdef CKMI_PHASE_TIMERS
+          {
+            // build (J reload from HBM) timed separately; s_memtime waits for the loads
+            double chk = 0.0;
+#pragma unroll
+            for (int j = 0; j < N; ++j) chk += M.a[j];
+            if (lane == 0 && chk == 12345.678) phs[21] += 1;
+            if (lane == 0) phs[20] += __builtin_amdgcn_s_memtime() - t0;
+          }
+#endif
+#ifdef CKMI_NEWTON_LU
           const bool ok = M.factor(lane, n);
+#else
+          const bool ok = M.factor(lane, n, L.base + 32 * VL);  // the dwdT row of the slice (free here)
+#endif
 #ifdef CKMI_PHASE_TIMERS
           ph[PH_LU] += __builtin_amdgcn_s_memtime() - t0;
 #endif
@@ -986,11 +1004,19 @@ __global__ __launch_bounds__(ROP_WAVES* WAVE) void rop_kernel(MechImage img, con
           o1[(size_t)oi * nstate + st] = qr;
         } else {
           const double q = qf - qr;
+#ifdef CKMI_EXPT_NOATOM
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (u < nr) wdot[sp_of(rs, u)] = -q;
+            if (u < np) wdot[sp_of(ps, u)] = q;
+          }
+#else
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             if (u < nr) atomicAdd(&wdot[sp_of(rs, u)], -q);
             if (u < np) atomicAdd(&wdot[sp_of(ps, u)], q);
           }
+#endif
         }
       }
       if (MODE == 0) {

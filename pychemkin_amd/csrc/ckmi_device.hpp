@@ -98,6 +98,27 @@ __device__ __forceinline__ double wave_max(double v) {
   return uni(fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48))));
 }
 
+// max of a u32 over the wave (DPP inside rows, readlanes across them); the pivot search
+// compares |a| as fp32 bit patterns: 1 VALU op per stage instead of 3 for an FP64 fmax
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_QUAD_1032, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_QUAD_2301, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_ROW_MIRROR, 0xf, 0xf, false));
+  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
+  return max(max(a, b), max(c, d));
+}
+
+// 1 / x from the hardware reciprocal and two Newton steps (no IEEE division sequence)
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
 // ------------------------------------------------------------------ thermo (NASA-7)
 struct SpThermo {
   double cpR, hRT, sR;

@@ -214,11 +214,19 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false,
                                  R.pslot, R.plnf, R.gfac);
       const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
+#ifdef CKMI_EXPT_NOATOM  // timing experiment only: plain stores instead of LDS atomics (wrong wdot)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u < nr) L.wdot()[sp_of(rs, u)] = -q;
+        if (u < np) L.wdot()[sp_of(ps, u)] = q;
+      }
+#else
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         if (u < nr) atomicAdd(&L.wdot()[sp_of(rs, u)], -q);
         if (u < np) atomicAdd(&L.wdot()[sp_of(ps, u)], q);
       }
+#endif
     }
 #ifdef CKMI_PHASE_TIMERS
     if (base / WAVE < 6) {
@@ -345,6 +353,113 @@ __device__ __forceinline__ double bpermute(int src_lane, double v) {
   return __hiloint2double(hi, lo);
 }
 
+#ifndef CKMI_NEWTON_LU
+#ifndef CKMI_GJ_BATCH
+#define CKMI_GJ_BATCH 4  // row pairs read per batch in the elimination
+#endif
+// Gauss-Jordan form: factor() overwrites a with the explicit inverse of the row-permuted
+// matrix (same partial pivoting sequence as LU: the pivot of step k is the largest |a[k]|
+// among the rows not yet used).  Lane p_k (permv on lane k) ends up holding row k of
+// (P M)^-1, so a solve is one matrix-vector product whose 54 broadcasts are independent of
+// each other -- instead of two dependent 54-step triangular sweeps.  n^3 instead of n^3/3
+// FMAs at factor time, paid back within one solve (1.5 solves per factorisation on average
+// is the minimum; the bench workload does 11).
+template <int N>
+struct NewtonMatrix {
+  double a[N];
+  int permv;  // lane k: the lane whose row was the pivot of step k
+
+  __device__ __forceinline__ void build(const double* J, int ldj, double gamma, int lane_in, int n) {
+    const int lane = opaque_lane(lane_in);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+      a[j] = (j == lane ? 1.0 : 0.0) - gamma * J[j * ldj + lane];  // J rows / columns >= n are zero
+  }
+
+  // orow: LDS byte offset of an N-double scratch row of the calling wave (16-byte aligned).
+  // The pivot row is broadcast through it: the pivot lane writes its row with ds_write_b128,
+  // every lane reads it back with broadcast ds_read_b128 -- 1 LDS instruction per element
+  // instead of 2 v_readlane + the SGPR-forwarding wait of a register broadcast.
+  __device__ __forceinline__ bool factor(int lane_in, int n, int orow) {
+    const int lane = opaque_lane(lane_in);
+    bool pivoted = lane >= N;
+    permv = lane;
+    bool ok = true;
+    // laundered like the lane index: otherwise the 27 row addresses are hoisted out of the
+    // reactor loop and held in VGPRs for its whole life
+    double2* row = lds_at<double2>(__builtin_amdgcn_readfirstlane(opaque_lane(orow)));
+    constexpr int NP = N / 2;  // row pairs (ds_read_b128)
+    // partial pivoting on |a| rounded to fp32 (ties within fp32 rounding go to the lowest lane;
+    // any of them is an equally good pivot).  The search for column k+1 is software-pipelined
+    // into the elimination of step k: column k+1 is updated first, and the DPP stages of its
+    // wave max are spread between the remaining row pairs, so their latency overlaps FMAs.
+    uint32_t v0 = pivoted ? 0u : __float_as_uint((float)fabs(a[0]));
+    uint32_t vmax = wave_max_u32(v0);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (vmax == 0u) ok = false;
+      const uint64_t mask = __ballot(!pivoted && v0 == vmax);
+      const int p = uni(mask ? (int)__ffsll((unsigned long long)mask) - 1 : 0);
+      const bool me = lane == p;
+      if (me) {
+#pragma unroll
+        for (int j = 0; j < N; j += 2) row[j / 2] = make_double2(a[j], a[j + 1]);
+      }
+      wave_lds_sync();  // other lanes' reads must follow the pivot lane's writes
+      const double piv = bcast(a[k], p);
+      const double rp = rcp_nr(piv);
+      if (me) pivoted = true;
+      if (lane == k) permv = p;
+      // row p becomes row p / piv; every other row i loses (a_i[k] / piv) x row p.  One FMA
+      // form for both: g = (piv - 1) / piv on the pivot lane gives a_p - g a_p = a_p / piv.
+      const double g = me ? (piv - 1.0) * rp : a[k] * rp;
+      const double ak = me ? rp : -g;
+      const int P0 = (k + 1 < N ? k + 1 : k) / 2;  // the pair holding column k+1 goes first
+      uint32_t w = 0u;
+#pragma unroll
+      for (int t = 0; t < NP; ++t) {
+        const int P = (P0 + t) % NP;
+        const double2 r = row[P];
+        if (2 * P != k) a[2 * P] = fma(-g, r.x, a[2 * P]);
+        if (2 * P + 1 != k) a[2 * P + 1] = fma(-g, r.y, a[2 * P + 1]);
+        if (k + 1 < N) {
+          if (t == 0) {
+            v0 = pivoted ? 0u : __float_as_uint((float)fabs(a[k + 1]));
+            w = v0;
+          }
+          if (t == 2) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_QUAD_1032, 0xf, 0xf, false));
+          if (t == 5) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_QUAD_2301, 0xf, 0xf, false));
+          if (t == 8) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false));
+          if (t == 11) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_ROW_MIRROR, 0xf, 0xf, false));
+          if (t == 14) {
+            const uint32_t r0 = __builtin_amdgcn_readlane(w, 0), r1 = __builtin_amdgcn_readlane(w, 16);
+            const uint32_t r2 = __builtin_amdgcn_readlane(w, 32), r3 = __builtin_amdgcn_readlane(w, 48);
+            vmax = max(max(r0, r1), max(r2, r3));
+          }
+        }
+        if (t % CKMI_GJ_BATCH == CKMI_GJ_BATCH - 1) asm volatile("" ::: "memory");  // row reads in flight (VGPR peak)
+      }
+      a[k] = ak;
+    }
+    return ok;
+  }
+
+  // x = M^-1 b (lane k: component k)
+  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
+    const int lane = opaque_lane(lane_in);
+    if (lane >= n) b = 0.0;
+    const double bp = bpermute(permv, b);  // lane j: b[p_j]
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      s0 = fma(a[j], bcast(bp, j), s0);
+      if (j + 1 < N) s1 = fma(a[j + 1], bcast(bp, j + 1), s1);
+    }
+    // lane p_k holds x_k; bring it to lane k
+    return bpermute(permv, s0 + s1);
+  }
+};
+#else
 template <int N>
 struct NewtonMatrix {
   double a[N];
@@ -412,6 +527,8 @@ struct NewtonMatrix {
   }
 };
 
+#endif
+
 // uniform small-array access with runtime index (keeps the arrays in SGPRs)
 template <int S>
 __device__ __forceinline__ double pick(const double (&v)[S], int i) {
@@ -441,8 +558,17 @@ struct BdfS {
 };
 
 // per-lane vectors (VGPRs)
+// The Nordsieck history lives in the wave's LDS slice (zn[j] of lane l at base_l + j * 512):
+// it is touched a few times per step, and its 12 VGPRs are worth more to the register-resident
+// Newton matrix.
+struct ZnLds {
+  int base;  // LDS byte offset of this lane's zn[0]
+  __device__ __forceinline__ double& operator[](int j) const { return *lds_at<double>(base + j * WAVE * 8); }
+};
+constexpr int ZN_BYTES = (QMAX + 1) * WAVE * 8;
+
 struct Bdf {
-  double zn[QMAX + 1];
+  ZnLds zn;
   double ewt, acor, tempv, ftemp, y;
 };
 
@@ -464,22 +590,35 @@ __device__ __forceinline__ void bdf_rescale(Bdf& b, BdfS& S) {
   S.hscale = S.h;
 }
 
+// zn_{j-1} += zn_j for k = 1..q, j = q..k (Pascal-triangle prediction), in registers
 __device__ __forceinline__ void bdf_predict(Bdf& b, BdfS& S) {
   S.tn += S.h;
+  const int q = S.q;
+  double z[QMAX + 1];
+#pragma unroll
+  for (int j = 0; j <= QMAX; ++j) z[j] = b.zn[j];
 #pragma unroll
   for (int k = 1; k <= QMAX; ++k)
 #pragma unroll
     for (int j = QMAX; j >= 1; --j)
-      if (k <= S.q && j >= k && j <= S.q) b.zn[j - 1] += b.zn[j];
+      if (j >= k) z[j - 1] = (k <= q && j <= q) ? z[j - 1] + z[j] : z[j - 1];
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
 __device__ __forceinline__ void bdf_restore(Bdf& b, BdfS& S, double saved_t) {
   S.tn = saved_t;
+  const int q = S.q;
+  double z[QMAX + 1];
+#pragma unroll
+  for (int j = 0; j <= QMAX; ++j) z[j] = b.zn[j];
 #pragma unroll
   for (int k = 1; k <= QMAX; ++k)
 #pragma unroll
     for (int j = QMAX; j >= 1; --j)
-      if (k <= S.q && j >= k && j <= S.q) b.zn[j - 1] -= b.zn[j];
+      if (j >= k) z[j - 1] = (k <= q && j <= q) ? z[j - 1] - z[j] : z[j - 1];
+#pragma unroll
+  for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
 __device__ __forceinline__ void bdf_set(Bdf& b, BdfS& S) {

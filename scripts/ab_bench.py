@@ -1,6 +1,6 @@
 """A/B timing of libckmi variants on the same GPU (alternating processes, same workload).
 
-    python scripts/ab_bench.py pychemkin_amd/_lib/libA.so pychemkin_amd/_lib/libB.so [--reps 3] [--n 16384]
+    python scripts/ab_bench.py pychemkin_amd/_lib/libA.so pychemkin_amd/_lib/libB.so [--reps 3] [--n 16384] [--rop]
 
 Each rep runs every library in its own process (CKMI_LIB=...) on a strided subsample of the
 bench sweep and reports the kernel time from HIP events; prints the per-library median.
@@ -32,16 +32,42 @@ print(json.dumps({"ms": e0.elapsed_time(e1), "steps": float(st[:, 0].mean()), "f
                   "tau0": float(res["tau"][0].item())}))
 """
 
+ROP_CHILD = r"""
+import os, sys, json, numpy as np
+sys.path.insert(0, %r)
+import torch, bench
+from pychemkin_amd import _native
+ns = %d
+mech = bench.mechanism()
+dm = _native.DeviceMechanism(mech.to_tables(), device=0)
+rng = np.random.default_rng(0)
+dev = "cuda:0"
+Ts = torch.as_tensor(rng.uniform(300.0, 3000.0, ns), device=dev)
+Ps = torch.as_tensor(bench.P_ATM * 10.0 ** rng.uniform(-1.0, 2.0, ns), device=dev)
+Ys = torch.as_tensor(rng.dirichlet(0.5 * np.ones(mech.KK), ns).T.copy(), device=dev)
+wdot = torch.empty((mech.KK, ns), dtype=torch.float64, device=dev)
+cp = torch.empty(ns, dtype=torch.float64, device=dev)
+hh = torch.empty(ns, dtype=torch.float64, device=dev)
+dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh); torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for _ in range(3):
+    dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
+e1.record(); torch.cuda.synchronize()
+print(json.dumps({"ms": e0.elapsed_time(e1) / 3, "wsum": float(wdot[:, :1000].abs().sum().item())}))
+"""
+
 
 def main():
     libs = [a for a in sys.argv[1:] if a.endswith(".so")]
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
-    n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 16384
+    rop = "--rop" in sys.argv
+    n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else (4_000_000 if rop else 16384)
     out = {lib: [] for lib in libs}
     for _ in range(reps):
         for lib in libs:
             env = dict(os.environ, CKMI_LIB=os.path.abspath(lib))
-            r = subprocess.run([sys.executable, "-c", CHILD % (ROOT, n)], env=env, capture_output=True, text=True,
+            r = subprocess.run([sys.executable, "-c", (ROP_CHILD if rop else CHILD) % (ROOT, n)], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
                 print(r.stderr[-2000:], file=sys.stderr)
@@ -50,7 +76,7 @@ def main():
             out[lib].append(d)
             print(os.path.basename(lib), d, flush=True)
     summary = {os.path.basename(k): {"median_ms": sorted(x["ms"] for x in v)[len(v) // 2],
-                                     "reactors_per_s": n / (sorted(x["ms"] for x in v)[len(v) // 2] / 1e3)}
+                                     ("states_per_s" if rop else "reactors_per_s"): n / (sorted(x["ms"] for x in v)[len(v) // 2] / 1e3)}
                for k, v in out.items()}
     print(json.dumps(summary, indent=1))
 

@@ -55,6 +55,7 @@ def main():
               "STEP_COMPLETE", "STEP_END", "FINISH"]
     out["state_cycles_per_step"] = {nm: float(ph[:, 8 + k].mean() / out["mean_steps"]) for k, nm in enumerate(states)
                                     if ph[:, 8 + k].any()}
+    out["newton_build_cycles_per_call"] = float(ph[:, 8 + 20].sum() / max(counts["lu"].sum(), 1))
     out["rhs_strip_cycles_per_call"] = [float(ph[:, 8 + 24 + k].sum() / max(counts["rhs"].sum(), 1)) for k in range(6)]
     acc = sum(out[nm + "_cycles"] for nm in names[:4])
     out["other_cycles"] = out["total_cycles"] - acc
