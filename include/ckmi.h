@@ -195,6 +195,20 @@ int ckmi_reactor_run_ex(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int3
                         double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
                         void* stream);
 
+/* Batched dense LU of Newton iteration matrices too large for one wave (mechanisms with more
+ * than 63 species).  Replaces the factorisation inside the reference's
+ * KINAll0D_Calculate (batchreactor.py:1158), which has no public entry point of its own.
+ *   A     [nsys][n][n] row-major FP64 (device), overwritten by L (unit lower) and U
+ *   ipiv  [nsys][n] 0-based pivot rows, LAPACK dgetrf order (row i was swapped with ipiv[i])
+ *   info  [nsys] 0, or k + 1 if U(k, k) is exactly zero (dgetrf convention)
+ * One workgroup per matrix; the trailing updates run on v_mfma_f64_16x16x4_f64.  n <= 192. */
+#define CKMI_LU_NMAX 192
+int ckmi_lu_factor_batched(int32_t nsys, int32_t n, double* A, int32_t* ipiv, int32_t* info, void* stream);
+/* B[nsys][n] <- A^-1 B from the factors of ckmi_lu_factor_batched (dgetrs, one right-hand side). */
+int ckmi_lu_solve_batched(int32_t nsys, int32_t n, const double* LU, const int32_t* ipiv, double* B,
+                          void* stream);
+const char* ckmi_lu_last_error(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,7 +77,11 @@ PROTOTYPES = {
                                      _P, ct.c_int32, _P, _P, _P]),
     "ckmi_reactor_run_ex": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P,
                                         ct.POINTER(ReactorExt), _P, _P, _P, _P, _P, _P, ct.c_int32, _P, _P, _P]),
+    "ckmi_lu_factor_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
+    "ckmi_lu_solve_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
+    "ckmi_lu_last_error": (ct.c_char_p, []),
 }
+LU_NMAX = 192
 
 
 def lib() -> ct.CDLL:
@@ -309,3 +313,46 @@ class DeviceMechanism:
             res["t_save"] = ts
             res["y_save"] = ys
         return res
+
+
+# ------------------------------------------------------------------ batched dense LU (n <= 192)
+def _lu_check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().ckmi_lu_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (code {rc}): {msg}")
+
+
+def lu_factor_batched(A: torch.Tensor):
+    """In-place batched LU with partial pivoting of A[nsys, n, n] (FP64, row-major, on the GPU).
+
+    Returns (A, ipiv[nsys, n] int32 0-based, info[nsys] int32) with LAPACK dgetrf semantics:
+    the Newton-matrix factorisation of the reactor integrator for mechanisms with more than 63
+    species (trailing updates on FP64 MFMA)."""
+    if not isinstance(A, torch.Tensor) or not A.is_cuda:
+        raise NativeError("lu_factor_batched needs a device tensor (no CPU path)")
+    if A.dtype != torch.float64 or A.dim() != 3 or A.shape[1] != A.shape[2] or not A.is_contiguous():
+        raise ValueError("A must be a contiguous float64 tensor [nsys, n, n]")
+    nsys, n = int(A.shape[0]), int(A.shape[1])
+    if not 1 <= n <= LU_NMAX:
+        raise ValueError(f"n must be in [1, {LU_NMAX}]")
+    ipiv = torch.empty((nsys, n), dtype=torch.int32, device=A.device)
+    info = torch.empty(nsys, dtype=torch.int32, device=A.device)
+    with torch.cuda.device(A.device):
+        _lu_check(lib().ckmi_lu_factor_batched(nsys, n, _ptr(A), _ptr(ipiv), _ptr(info), _stream_ptr(A.device)),
+                  "ckmi_lu_factor_batched")
+    return A, ipiv, info
+
+
+def lu_solve_batched(LU: torch.Tensor, ipiv: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """B[nsys, n] <- A^-1 B in place, from the factors of lu_factor_batched."""
+    if not (LU.is_cuda and ipiv.is_cuda and B.is_cuda):
+        raise NativeError("lu_solve_batched needs device tensors (no CPU path)")
+    nsys, n = int(LU.shape[0]), int(LU.shape[1])
+    if tuple(B.shape) != (nsys, n) or B.dtype != torch.float64 or not B.is_contiguous():
+        raise ValueError("B must be a contiguous float64 tensor [nsys, n]")
+    if tuple(ipiv.shape) != (nsys, n) or ipiv.dtype != torch.int32:
+        raise ValueError("ipiv must be int32 [nsys, n]")
+    with torch.cuda.device(LU.device):
+        _lu_check(lib().ckmi_lu_solve_batched(nsys, n, _ptr(LU), _ptr(ipiv), _ptr(B), _stream_ptr(LU.device)),
+                  "ckmi_lu_solve_batched")
+    return B

@@ -6,40 +6,64 @@ import subprocess
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "csrc", "ckmi.hip")
+SRC = os.path.join(HERE, "csrc", "ckmi.hip")        # kinetics, thermo and reactor kernels + C ABI
+LU_SRC = os.path.join(HERE, "csrc", "ckmi_lu.hip")  # batched MFMA LU (large mechanisms)
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp", "ckmi_image.hpp")] + [
     os.path.join(HERE, "..", "include", "ckmi.h")]
 OUT = os.path.join(HERE, "_lib", "libckmi.so")
+OBJ_DIR = os.path.join(HERE, "_lib", "obj")
 ARCH = "gfx950"  # MI355X only
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # MachineLICM / MachineSink are off: in the persistent reactor kernel they hoist FP64
 # constants and addresses out of the integrator loop, keep them live across the RHS and then
 # spill them to scratch (284 -> 16 B/lane of scratch, +29 % reactors/s measured A/B on MI355X).
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-munsafe-fp-atomics", "-mcode-object-version=5",
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-mcode-object-version=5",
          f"--offload-arch={ARCH}", "-mllvm", "-disable-machine-licm", "-mllvm", "-disable-machine-sink",
          # the Gauss-Jordan factorisation is a fully unrolled 54 x 54 loop nest (a[] must stay in VGPRs)
          "-mllvm", "-pragma-unroll-threshold=2000000"]
+LU_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", f"--offload-arch={ARCH}"]
+
+
+def _stale(target: str, sources) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(p) > t for p in sources)
 
 
 def needs_build() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in [SRC] + DEPS)
+    return _stale(OUT, [SRC, LU_SRC] + DEPS)
 
 
 PROF_OUT = os.path.join(HERE, "_lib", "libckmi_prof.so")  # diagnostic phase-timer build
 
 
+def _compile(src: str, obj: str, flags, verbose: bool) -> None:
+    cmd = [HIPCC] + list(flags) + ["-c", "-o", obj, src]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+
+
 def build(force: bool = False, verbose: bool = False, prof: bool = False, out: str = None, extra=()) -> str:
-    """Build libckmi.so (or the phase-timer build, or an A/B variant at `out` with `extra` flags)."""
+    """Build libckmi.so (or the phase-timer build, or an A/B variant at `out` with `extra` flags).
+
+    Two translation units, compiled separately (the reactor kernel alone takes ~2 min) and linked
+    into one shared library: ckmi.hip and ckmi_lu.hip."""
     default = out is None and not prof and not extra
     out = out or (PROF_OUT if prof else OUT)
     if not force and default and not needs_build():
         return OUT
-    os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [HIPCC] + FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(extra) + ["-o", out, SRC]
+    os.makedirs(OBJ_DIR, exist_ok=True)
+    lu_obj = os.path.join(OBJ_DIR, "ckmi_lu.o")
+    if force or _stale(lu_obj, [LU_SRC, DEPS[-1]]):
+        _compile(LU_SRC, lu_obj, LU_FLAGS, verbose)
+    tag = "main" if default else os.path.splitext(os.path.basename(out))[0]
+    main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
+    if force or not default or _stale(main_obj, [SRC] + DEPS):
+        _compile(SRC, main_obj, FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(extra), verbose)
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

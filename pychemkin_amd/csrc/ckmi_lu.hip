@@ -1,0 +1,426 @@
+// ckmi_lu.hip -- batched dense LU factorisation with FP64 MFMA trailing updates (gfx950).
+//
+// The Newton iteration matrix of a batch reactor is n x n with n = KK + 1.  For GRI-3.0 (n = 54)
+// the reactor kernel keeps it in one wave's VGPRs (ckmi_reactor.hpp, NewtonMatrix).  Mechanisms
+// with more than 63 species (n-heptane class, n ~ 161) do not fit a
+// wave; their factorisation is the right-looking blocked LU below, one workgroup of 8 waves per
+// matrix, the matrix held in the workgroup's registers as 16 x 16 FP64 tiles in the
+// v_mfma_f64_16x16x4_f64 C/D layout (lane l, component r: row (l >> 4) + 4 r, column l & 15):
+//
+//   for each 16-column panel K:
+//     1. the owners of the panel tiles write them to LDS (P);
+//     2. wave 0 factors the panel with partial pivoting (LAPACK dgetf2 rule: first row of
+//        maximal |a|), records the swaps, reduces them to a net row permutation of at most 32
+//        rows, and forms L11^-1 (unit lower, 16 x 16);
+//     3. every wave applies the permutation to its tiles of the other block columns (rows
+//        exchanged through LDS) and reads back its factored panel tiles;
+//     4. U12 = L11^-1 A12: 4 MFMAs per tile of block row K (the tile's own C registers are the
+//        B operand), written to LDS;
+//     5. A22 -= L21 U12: 4 MFMAs per trailing tile, A from the panel in LDS, B from U12 in LDS.
+//
+// The result has LAPACK dgetrf semantics (A = P L U, unit-lower L below the diagonal, U on and
+// above, row interchanges applied to the whole rows) with 0-based pivot rows.  This is the
+// factorisation inside the reference's closed KINAll0D_Calculate (batchreactor.py:1158) for a
+// mechanism of that size; ckmi_lu_solve_batched is the matching substitution.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/ckmi.h"
+
+namespace {
+
+constexpr int WAVE = 64;
+constexpr int LU_WAVES = 8;  // waves per workgroup (one matrix per workgroup)
+constexpr int TB = 16;       // tile edge = the 16x16x4 MFMA shape
+constexpr int LU_NB_MAX = CKMI_LU_NMAX / TB;
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ d4 mfma16(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+// runtime-indexed component of a C tile, as selects (a runtime vector index would go to scratch)
+__device__ __forceinline__ double comp(const d4& v, int r) { return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w; }
+__device__ __forceinline__ void set_comp(d4& v, int r, double x) {
+  v.x = r == 0 ? x : v.x;
+  v.y = r == 1 ? x : v.y;
+  v.z = r == 2 ? x : v.z;
+  v.w = r == 3 ? x : v.w;
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// exact FP64 max over the wave (DPP inside rows, readlanes across them)
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp_mov<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmax(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmax(v, dpp_mov<0x141>(v));  // row_half_mirror
+  v = fmax(v, dpp_mov<0x140>(v));  // row_mirror
+  return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
+}
+
+template <int NB>
+struct LuSmem {
+  static constexpr int NP = NB * TB;
+  static constexpr int PLD = TB + 1;  // odd row stride: lanes on different rows hit different banks
+  double P[NP * PLD];                 // panel block column, indexed by global row
+  double X[32 * NP];                  // row-exchange buffer, then the U12 block row [16][NP]
+  double Linv[TB * PLD];
+  int src[32], dst[32];     // slot q < 32: row dst[q] receives the old row src[q]
+  uint32_t smask[NB], dmask[NB];  // per tile row: the slots whose source / destination it holds
+  int piv[TB];
+  int info;
+};
+
+// Step 2: wave 0 factors panel K in LDS.  Rows K*16 .. NP-1, columns 0..15 of S.P.
+template <int NB>
+__device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int n) {
+  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
+  const int r0 = K * TB;
+#pragma unroll
+  for (int c = 0; c < TB; ++c) {
+    const int col = r0 + c;
+    // pivot: first row of maximal |a| among rows >= col (idamax; exact FP64 comparison)
+    double best = -1.0;
+    int bq = 0;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int r = r0 + lane + WAVE * q;
+      if (r >= col && r < NP) {
+        const double v = fabs(S.P[r * PLD + c]);
+        if (v > best) {
+          best = v;
+          bq = q;
+        }
+      }
+    }
+    const double maxv = wave_max(best);
+    // the smallest row among the maxima: lowest q level first (rows r0 + l + 64 q), then lowest lane
+    int p = col;
+#pragma unroll
+    for (int q = NQ - 1; q >= 0; --q) {
+      const uint64_t mq = __ballot(best == maxv && bq == q);
+      if (mq) p = r0 + (int)__ffsll((unsigned long long)mq) - 1 + WAVE * q;
+    }
+    p = __builtin_amdgcn_readfirstlane(p);
+    if (lane == 0) S.piv[c] = p;
+    if (maxv != 0.0) {
+      if (p != col && lane < TB) {
+        const double a = S.P[col * PLD + lane], b = S.P[p * PLD + lane];
+        S.P[col * PLD + lane] = b;
+        S.P[p * PLD + lane] = a;
+      }
+      wave_lds_sync();
+      double prow[TB];
+#pragma unroll
+      for (int cc = c; cc < TB; ++cc) prow[cc] = S.P[col * PLD + cc];
+      const double rp = 1.0 / prow[c];
+#pragma unroll 1
+      for (int q = 0; q < NQ; ++q) {
+        const int r = r0 + lane + WAVE * q;
+        if (r > col && r < NP) {
+          double* row = &S.P[r * PLD];
+          const double l = row[c] * rp;
+          row[c] = l;
+#pragma unroll
+          for (int cc = c + 1; cc < TB; ++cc) row[cc] = fma(-l, prow[cc], row[cc]);
+        }
+      }
+    } else if (lane == 0 && S.info == 0 && col < n) {
+      S.info = col + 1;  // LAPACK: U(col, col) is exactly zero
+    }
+    wave_lds_sync();
+  }
+  // L11^-1 (unit lower) by forward substitution on the identity, right-looking over columns m
+  // of L11: lane (i, g) holds X[i][g + 4k], k = 0..3; row m is read from lane m + 16 g
+  {
+    const int i = lane & 15, g = lane >> 4;
+    double x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = (i == g + 4 * k) ? 1.0 : 0.0;
+#pragma unroll 1
+    for (int mm = 0; mm < TB - 1; ++mm) {
+      const double lm = i > mm ? S.P[(r0 + i) * PLD + mm] : 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[k] = fma(-lm, __shfl(x[k], mm + 16 * g), x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) S.Linv[i * PLD + g + 4 * k] = x[k];
+  }
+  // Net row permutation of the 16 interchanges.  Lanes 0..15 track rows r0 + l, lanes 16..31 the
+  // pivot rows; each lane's `val` is the original row whose content its row holds now.
+  const int key = lane < TB ? r0 + lane : (lane < 2 * TB ? S.piv[lane - TB] : -1);
+  int val = key;
+#pragma unroll
+  for (int c = 0; c < TB; ++c) {
+    const int a = r0 + c, b = S.piv[c];
+    if (a != b) {
+      const uint64_t ma = __ballot(key == a), mb = __ballot(key == b);
+      const int va = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)ma) - 1);
+      const int vb = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)mb) - 1);
+      if (key == a) val = vb;
+      if (key == b) val = va;
+    }
+  }
+  // keep the first lane of each key whose row actually changed; slot = lane
+  bool rep = key >= 0 && val != key;
+#pragma unroll
+  for (int j = 0; j < 2 * TB; ++j) {
+    const int kj = __builtin_amdgcn_readlane(key, j);
+    if (j < lane && kj == key) rep = false;
+  }
+  if (lane < 2 * TB) {
+    S.dst[lane] = key;
+    S.src[lane] = val;
+  }
+#pragma unroll
+  for (int I = 0; I < NB; ++I) {
+    const uint32_t sm = (uint32_t)__ballot(rep && val / TB == I);
+    const uint32_t dm = (uint32_t)__ballot(rep && key / TB == I);
+    if (lane == 0) {
+      S.smask[I] = sm;
+      S.dmask[I] = dm;
+    }
+  }
+}
+
+template <int NB>
+__global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int n, double* __restrict__ A,
+                                                                   int* __restrict__ ipiv, int* __restrict__ info) {
+  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NT = (NB * NB + LU_WAVES - 1) / LU_WAVES;
+  __shared__ LuSmem<NB> S;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const int lc0 = lane & 15, lg0 = lane >> 4;
+
+  for (int sys = blockIdx.x; sys < nsys; sys += gridDim.x) {
+    double* As = A + (size_t)sys * n * n;
+    d4 t[NT];
+    {
+      // laundered per matrix (the load offsets would otherwise be hoisted out of the sys loop)
+      int w = w0, lc = lc0, lg = lg0, nl = n;
+      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg), "+s"(nl));
+      // tile s of wave w is tile index w + 8 s = (I, J) in row-major tile order
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w + LU_WAVES * s;
+        const int I = ti / NB, J = ti % NB;
+        const int col = J * TB + lc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = I * TB + lg + 4 * r;
+          double v = row == col ? 1.0 : 0.0;  // identity padding up to a multiple of 16
+          if (ti < NB * NB && row < nl && col < nl) v = As[(size_t)row * nl + col];
+          t[s][r] = v;
+        }
+      }
+    }
+    if (threadIdx.x == 0) S.info = 0;
+
+    for (int K = 0; K < NB; ++K) {
+      // laundered per panel: keeps the per-tile indices and LDS addresses from being hoisted
+      // out of the K loop and held in registers for the whole factorisation
+      int w = w0, lc = lc0, lg = lg0;
+      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg));
+      // 1. panel tiles (I >= K, K) to LDS
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w + LU_WAVES * s;
+        const int I = ti / NB, J = ti % NB;
+        if (ti < NB * NB && J == K && I >= K) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S.P[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+        }
+      }
+      __syncthreads();
+      // 2. factor the panel
+      if (w == 0) panel_factor<NB>(S, K, lane, n);
+      __syncthreads();
+      // 3. row interchanges in the other block columns (sources out), factored panel back in
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w + LU_WAVES * s;
+        const int I = ti / NB, J = ti % NB;
+        if (ti < NB * NB && J != K) {
+          for (uint32_t mk = I >= K ? S.smask[I] : 0u; mk; mk &= mk - 1) {
+            const int q = __builtin_ctz(mk);
+            const int sr = S.src[q];
+            if (lg == (sr & 3)) S.X[q * NP + J * TB + lc] = comp(t[s], (sr % TB) >> 2);
+          }
+        } else if (ti < NB * NB && J == K && I >= K) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[s][r] = S.P[(I * TB + lg + 4 * r) * PLD + lc];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w + LU_WAVES * s;
+        const int I = ti / NB, J = ti % NB;
+        if (ti < NB * NB && J != K) {
+          for (uint32_t mk = I >= K ? S.dmask[I] : 0u; mk; mk &= mk - 1) {
+            const int q = __builtin_ctz(mk);
+            const int dr = S.dst[q];
+            if (lg == (dr & 3)) set_comp(t[s], (dr % TB) >> 2, S.X[q * NP + J * TB + lc]);
+          }
+        }
+      }
+      __syncthreads();
+      // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (X reused as [16][NP])
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w + LU_WAVES * s;
+        const int I = ti / NB, J = ti % NB;
+        if (ti < NB * NB && I == K && J > K) {
+          d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) u = mfma16(S.Linv[lc * PLD + 4 * kk + lg], t[s][kk], u);
+          t[s] = u;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S.X[(lg + 4 * r) * NP + J * TB + lc] = u[r];
+        }
+      }
+      __syncthreads();
+      // 5. trailing update A22 -= L21 U12
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w + LU_WAVES * s;
+        const int I = ti / NB, J = ti % NB;
+        if (ti < NB * NB && I > K && J > K) {
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk)
+            t[s] = mfma16(-S.P[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
+        }
+      }
+      if (threadIdx.x < TB && K * TB + threadIdx.x < n) ipiv[(size_t)sys * n + K * TB + threadIdx.x] = S.piv[threadIdx.x];
+      __syncthreads();  // P, X and piv are rewritten by the next panel
+    }
+    // opaque copies: otherwise the 4 NT store addresses are CSE'd with the load addresses and
+    // held in VGPRs through the whole factorisation
+    int n_st = n, lc_st = lc0, lg = lg0, w = w0;
+    double* Ast = As;
+    asm volatile("" : "+s"(n_st), "+v"(lc_st), "+s"(Ast), "+v"(lg), "+s"(w));
+#pragma unroll
+    for (int s = 0; s < NT; ++s) {
+      const int ti = w + LU_WAVES * s;
+      const int I = ti / NB, J = ti % NB;
+      const int col = J * TB + lc_st;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = I * TB + lg + 4 * r;
+        if (ti < NB * NB && row < n_st && col < n_st) Ast[(size_t)row * n_st + col] = t[s][r];
+      }
+    }
+    if (threadIdx.x == 0) info[sys] = S.info;
+    __syncthreads();  // S.info
+  }
+}
+
+// One wave per right-hand side: x = U^-1 L^-1 P b, in place in B[sys][n].
+constexpr int SOLVE_WAVES = 4;
+__global__ __launch_bounds__(SOLVE_WAVES* WAVE) void lu_solve_kernel(int nsys, int n, const double* __restrict__ LU,
+                                                                     const int* __restrict__ ipiv,
+                                                                     double* __restrict__ B) {
+  __shared__ double xs[SOLVE_WAVES][CKMI_LU_NMAX];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w = threadIdx.x / WAVE;
+  const int sys = blockIdx.x * SOLVE_WAVES + w;
+  if (sys >= nsys) return;  // whole wave leaves
+  const double* L = LU + (size_t)sys * n * n;
+  double* b = B + (size_t)sys * n;
+  double* x = xs[w];
+  for (int i = lane; i < n; i += WAVE) x[i] = b[i];
+  wave_lds_sync();
+  if (lane == 0) {
+    for (int i = 0; i < n; ++i) {  // interchanges in order (dgetrs / dlaswp)
+      const int p = ipiv[(size_t)sys * n + i];
+      if (p != i) {
+        const double tmp = x[i];
+        x[i] = x[p];
+        x[p] = tmp;
+      }
+    }
+  }
+  wave_lds_sync();
+  for (int j = 0; j < n; ++j) {  // L y = P b (unit diagonal)
+    const double yj = x[j];
+    for (int i = j + 1 + lane; i < n; i += WAVE) x[i] = fma(-L[(size_t)i * n + j], yj, x[i]);
+    wave_lds_sync();
+  }
+  for (int j = n - 1; j >= 0; --j) {  // U x = y
+    const double xj = x[j] / L[(size_t)j * n + j];
+    wave_lds_sync();
+    if (lane == 0) x[j] = xj;
+    for (int i = lane; i < j; i += WAVE) x[i] = fma(-L[(size_t)i * n + j], xj, x[i]);
+    wave_lds_sync();
+  }
+  for (int i = lane; i < n; i += WAVE) b[i] = x[i];
+}
+
+thread_local std::string g_lu_err;
+
+template <int NB>
+hipError_t launch_factor(int nsys, int n, double* A, int* ipiv, int* info, hipStream_t st) {
+  const int grid = nsys < 8192 ? nsys : 8192;
+  hipLaunchKernelGGL(lu_factor_kernel<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
+  return hipGetLastError();
+}
+
+typedef hipError_t (*factor_fn)(int, int, double*, int*, int*, hipStream_t);
+const factor_fn kFactor[LU_NB_MAX] = {launch_factor<1>, launch_factor<2>, launch_factor<3>,  launch_factor<4>,
+                                      launch_factor<5>, launch_factor<6>, launch_factor<7>,  launch_factor<8>,
+                                      launch_factor<9>, launch_factor<10>, launch_factor<11>, launch_factor<12>};
+
+}  // namespace
+
+extern "C" {
+
+const char* ckmi_lu_last_error(void) { return g_lu_err.c_str(); }
+
+int ckmi_lu_factor_batched(int32_t nsys, int32_t n, double* A, int32_t* ipiv, int32_t* info, void* stream) {
+  if (nsys < 0 || n < 1 || n > CKMI_LU_NMAX || (nsys > 0 && (!A || !ipiv || !info))) {
+    g_lu_err = "ckmi_lu_factor_batched: need 1 <= n <= " + std::to_string(CKMI_LU_NMAX) + " and device pointers";
+    return CKMI_ERR_ARG;
+  }
+  if (nsys == 0) return CKMI_OK;
+  const hipError_t e = kFactor[(n + TB - 1) / TB - 1](nsys, n, A, ipiv, info, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    g_lu_err = std::string("lu_factor_kernel launch: ") + hipGetErrorString(e);
+    return CKMI_ERR_HIP;
+  }
+  return CKMI_OK;
+}
+
+int ckmi_lu_solve_batched(int32_t nsys, int32_t n, const double* LU, const int32_t* ipiv, double* B, void* stream) {
+  if (nsys < 0 || n < 1 || n > CKMI_LU_NMAX || (nsys > 0 && (!LU || !ipiv || !B))) {
+    g_lu_err = "ckmi_lu_solve_batched: need 1 <= n <= " + std::to_string(CKMI_LU_NMAX) + " and device pointers";
+    return CKMI_ERR_ARG;
+  }
+  if (nsys == 0) return CKMI_OK;
+  hipLaunchKernelGGL(lu_solve_kernel, dim3((nsys + SOLVE_WAVES - 1) / SOLVE_WAVES), dim3(SOLVE_WAVES * WAVE), 0,
+                     (hipStream_t)stream, nsys, n, LU, ipiv, B);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    g_lu_err = std::string("lu_solve_kernel launch: ") + hipGetErrorString(e);
+    return CKMI_ERR_HIP;
+  }
+  return CKMI_OK;
+}
+
+}  // extern "C"
