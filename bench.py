@@ -98,6 +98,36 @@ def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
     return TT, PP, ch4_air_Y(mech, FF)
 
 
+def lu_bench(dev, nsys, n):
+    """Batched LU (ckmi_lu_factor_batched) on nsys Newton-like matrices I - gamma J of size n, timed with HIP
+    events on the stream it is launched on; algorithmic work (2/3) n^3 per matrix."""
+    g = torch.Generator(device=dev).manual_seed(0)
+    A0 = torch.eye(n, dtype=torch.float64, device=dev) - 1e-6 * torch.randn(
+        (nsys, n, n), dtype=torch.float64, device=dev, generator=g) * 10.0 ** (6.0 * torch.rand(
+            (nsys, n, n), dtype=torch.float64, device=dev, generator=g))
+    A = torch.empty_like(A0)
+    times = []
+    for it in range(4):
+        A.copy_(A0)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        _, _, info = _native.lu_factor_batched(A)
+        e1.record()
+        torch.cuda.synchronize()
+        if it:
+            times.append(e0.elapsed_time(e1) / 1e3)
+    sec = float(np.median(times))
+    flops = nsys * 2.0 / 3.0 * n ** 3
+    nbytes = nsys * 2.0 * n * n * 8
+    del A, A0
+    return {"kernel": "lu_factor_kernel<11>", "systems": nsys, "n": n, "ms_per_launch": sec * 1e3,
+            "systems_per_s": nsys / sec, "singular": int((info != 0).sum().item()),
+            "roofline": {"bound": "mfma", "pipe": "fp64-mfma", "achieved": flops / sec / 1e12,
+                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": flops / sec / 1e12 / FP64_PEAK_TFLOPS,
+                         "hbm_GBs": nbytes / sec / 1e9, "traffic": None}}
+
+
 RUN = dict(energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
 
 
@@ -108,6 +138,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reactors", type=int, default=0, help="override reactors per GPU (0 = full 65,536 shard)")
     ap.add_argument("--rop-states", type=int, default=10_000_000)
+    ap.add_argument("--lu-systems", type=int, default=16384,
+                    help="configs[4] component: batched n = 161 Newton-matrix LU on MFMA (0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -218,6 +250,11 @@ def main():
         }
         del Ts, Ps, Ys, wdot, cp, hh
 
+    # ---- configs[4] component: batched FP64 LU of n = 161 Newton matrices (MFMA trailing updates)
+    lu = None
+    if rank == 0 and args.lu_systems > 0:
+        lu = lu_bench(dev, args.lu_systems, 161)
+
     # ---- CPU baseline (rank 0, N = 1): oracle C restatement on a strided sample
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -276,6 +313,7 @@ def main():
                          "flops_per_launch": flops, "kernel_ms": kern_s * 1e3},
             "cpu_baseline": cpu,
             "rop": rop,
+            "lu": lu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
