@@ -217,6 +217,19 @@ def main():
     total_reactors = n * world * args.steps
     value = total_reactors / tmax
 
+    # PCIe-inclusive rate (reported beside value, never as value): host numpy inputs -> H2D ->
+    # one launch -> D2H of tau, T, P, V, Y, stats, on this rank
+    torch.cuda.synchronize()
+    tp = time.perf_counter()
+    rp = dm.reactor_run(cfg, prob, T0, P0, np.ones(n), Y0)
+    host_out = {k: v.cpu().numpy() for k, v in rp.items()}
+    torch.cuda.synchronize()
+    pcie_s = time.perf_counter() - tp
+    pcie = {"reactors_per_s": n / pcie_s, "seconds": pcie_s,
+            "bytes_h2d": int(T0.nbytes + P0.nbytes + Y0.nbytes + prob.nbytes + 8 * n),
+            "bytes_d2h": int(sum(a.nbytes for a in host_out.values()))}
+    del rp, host_out
+
     # ---- ROP + thermo (configs[1]) : secondary metric
     rop = None
     if args.rop_states > 0:
@@ -275,7 +288,13 @@ def main():
             ctau = np.array([r.tau for r in cres])
             dmax = max(dmax, float(np.max(np.abs(tau[idx] / ctau - 1))))
             done += len(idx)
+        # the same oracle on one core, over the first chunk of the sample (~3 s)
+        idx1 = order[: max(8, min(64, order.size))]
+        tc = time.perf_counter()
+        orc.reactor_batch(T0[idx1], P0[idx1], Y0[idx1], problem=prob[idx1], V0=np.ones(len(idx1)), nthreads=1, **RUN)
+        one_core = len(idx1) / (time.perf_counter() - tc)
         cpu = {"value": done / tcpu, "unit": "reactors/s", "cores": threads, "kind": "port",
+               "single_core_value": one_core, "single_core_sample": f"{len(idx1)} reactors of the same sample",
                "sample": f"{done} reactors (random subset of every {stride}th of this GPU's sweep), oracle C restatement, "
                          f"OpenMP over reactors",
                "tau_max_rel_diff_vs_gpu": dmax,
@@ -314,6 +333,7 @@ def main():
             "cpu_baseline": cpu,
             "rop": rop,
             "lu": lu,
+            "pcie_inclusive": pcie,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

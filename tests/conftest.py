@@ -118,3 +118,43 @@ def within(a, b, atol, rtol):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return np.abs(a - b) <= atol + rtol * np.abs(b)
+
+
+def _h_mass(tables, Y, T):
+    """Mixture enthalpy per mass [erg/g] from the NASA-7 tables (numpy; [KK][17] layout of ckmi_mech_desc)."""
+    th = np.asarray(tables["thermo"])
+    a = np.where((T > th[:, 1])[:, None], th[:, 10:17], th[:, 3:10])
+    hRT = a[:, 0] + T * (a[:, 1] / 2 + T * (a[:, 2] / 3 + T * (a[:, 3] / 4 + T * a[:, 4] / 5))) + a[:, 5] / T
+    return float(np.sum(Y * hRT * 8.314462618e7 * T / np.asarray(tables["wt"])))
+
+
+def hp_equilibrium_start(mech, tables, phi, T_reac=295.15):
+    """Start state for the HP-equilibrium golden (adiabaticflametemperature.py:54-91: CH4/O2,
+    products CO2/H2O, 295.15 K, 1 atm): the same elements burned to {CO, CO2, H2O, H2, O2} and
+    heated to the temperature with the reactants' enthalpy per mass.  An adiabatic constant-pressure
+    reactor started there keeps H and P, so its long-time state is the HP equilibrium of the
+    reactant mixture (no ignition wait at 295 K).  Returns (T*, Y*)."""
+    def Y_of(moles):
+        X = np.zeros(mech.KK)
+        for k, v in moles.items():
+            X[mech.species.index(k)] = v
+        Y = X * mech.wt
+        return Y / Y.sum()
+
+    h_r = _h_mass(tables, Y_of({"CH4": phi, "O2": 2.0}), T_reac)   # X = phi X_fuel + 2 X_oxid
+    n_co, o_left = phi, 4.0 - phi
+    n_h2o = min(2.0 * phi, o_left)
+    o_left -= n_h2o
+    n_h2 = (4.0 * phi - 2.0 * n_h2o) / 2.0
+    conv = min(n_co, o_left)
+    n_co -= conv
+    o_left -= conv
+    Yp = Y_of({"CO": n_co, "CO2": conv, "H2O": n_h2o, "H2": n_h2, "O2": o_left / 2.0})
+    lo, hi = 300.0, 8000.0
+    for _ in range(100):
+        mid = 0.5 * (lo + hi)
+        if _h_mass(tables, Yp, mid) > h_r:
+            hi = mid
+        else:
+            lo = mid
+    return 0.5 * (lo + hi), Yp

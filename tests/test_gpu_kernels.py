@@ -46,7 +46,7 @@ def test_species_cv_matches_speciesproperties_golden(chem):
     assert np.max(np.abs(cv / np.asarray(g["state-Cv"]) - 1)) < 1e-12
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 4097])
+@pytest.mark.parametrize("n", [1, 5, 8, 23, 63, 64, 4097])
 def test_rop_thermo_matches_oracle(dm, oracle, mech, n):
     T, P, Y = _random_states(mech.KK, n, seed=n)
     w, cp, h = (x.cpu().numpy() for x in dm.rop_thermo(T, P, Y))

@@ -240,3 +240,24 @@ def test_invalid_config_fails_loudly(dm, mech):
         dm.reactor_run(_native.make_cfg(t_end=-1.0), np.array([1], np.int32), [1200.0], [P_ATM], [1.0], Y0)
     with pytest.raises(_native.NativeError):
         dm.reactor_run(_native.make_cfg(t_end=1.0), np.array([3], np.int32), [1200.0], [P_ATM], [1.0], Y0)
+
+
+def test_hp_equilibrium_golden_on_gpu(dm, mech, tables):
+    """adiabaticflametemperature.baseline through the kernel: 12 adiabatic CONP reactors (one per
+    phi = 0.5..1.6) started at the reactants' H and P relax to Chemkin's HP-equilibrium
+    temperature (the oracle reproduces it to ~1e-8, test_oracle_golden.py)."""
+    from conftest import hp_equilibrium_start
+    from pychemkin_amd import _native
+
+    g = golden("adiabaticflametemperature")
+    starts = [hp_equilibrium_start(mech, tables, phi) for phi in g["state-equivalence_ratio"]]
+    n = len(starts)
+    T0 = np.array([s[0] for s in starts])
+    Y0 = np.stack([s[1] for s in starts])
+    cfg = _native.make_cfg(energy=1, t_end=1.0, atol=1e-14, rtol=1e-9)
+    res = dm.reactor_run(cfg, np.ones(n, np.int32), T0, np.full(n, P_ATM), np.ones(n), Y0)
+    Tend = res["T"].cpu().numpy()
+    assert np.all(res["stats"].cpu().numpy()[:, 6] == 0)
+    Tg = np.asarray(g["state-temperature"])
+    assert np.all(within(Tend, Tg, *g["tolerance-var"]))
+    assert np.max(np.abs(Tend / Tg - 1)) < 1e-7

@@ -117,3 +117,19 @@ def test_afactor_sensitivity_golden(oracle, mech, chem):
     ref = np.array(g["rate-sensitivity_positive"] + g["rate-sensitivity_negative"])
     assert np.all(np.abs(sens[idx] / ref - 1) < 0.03)
     assert np.median(np.abs(sens[idx] / ref - 1)) < 0.01
+
+
+def test_hp_equilibrium_adiabatic_flame_temperature(oracle, mech, tables):
+    """adiabaticflametemperature.baseline (Chemkin HP equilibrium of CH4/O2 at 295.15 K, 1 atm,
+    phi = 0.5..1.6): an adiabatic CONP reactor holding the reactants' H and P relaxes to the same
+    state.  Reproduced to ~1e-8: pins NASA-7 (h, s), K_c of every reversible reaction and the
+    CONP energy equation at 2900-3100 K together."""
+    from conftest import hp_equilibrium_start
+
+    g = golden("adiabaticflametemperature")
+    for phi, Tg in zip(g["state-equivalence_ratio"], g["state-temperature"]):
+        Ts, Yp = hp_equilibrium_start(mech, tables, phi)
+        res, _ = oracle.reactor(Ts, P_ATM, 1.0, Yp, problem=1, energy=1, t_end=1.0, atol=1e-14, rtol=1e-9)
+        assert res.status == 0
+        assert within(np.array([res.T]), np.array([Tg]), *g["tolerance-var"]).all()
+        assert abs(res.T / Tg - 1) < 1e-7, (phi, res.T, Tg)
