@@ -35,6 +35,11 @@ constexpr int WAVE = 64;
 constexpr int LU_WAVES = 8;  // waves per workgroup (one matrix per workgroup)
 constexpr int TB = 16;       // tile edge = the 16x16x4 MFMA shape
 constexpr int LU_NB_MAX = CKMI_LU_NMAX / TB;
+#ifdef CKMI_LU_EXPT_NOSWAP  // timing experiment only (wrong factors): skip the row interchanges
+constexpr bool LU_EXPT_NOSWAP = true;
+#else
+constexpr bool LU_EXPT_NOSWAP = false;
+#endif
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -83,7 +88,7 @@ struct LuSmem {
   double X[32 * NP];                  // row-exchange buffer, then the U12 block row [16][NP]
   double Linv[TB * PLD];
   int src[32], dst[32];     // slot q < 32: row dst[q] receives the old row src[q]
-  uint32_t smask[NB], dmask[NB];  // per tile row: the slots whose source / destination it holds
+  int sslot[NP], dslot[NP]; // per row: the slot it is the source / destination of, or -1
   int piv[TB];
   int info;
 };
@@ -131,7 +136,7 @@ __device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int
 #pragma unroll
       for (int cc = c; cc < TB; ++cc) prow[cc] = S.P[col * PLD + cc];
       const double rp = 1.0 / prow[c];
-#pragma unroll 1
+#pragma unroll 1  // a full unroll spills (wave 0 also holds its 16 tiles): 41 VGPRs measured
       for (int q = 0; q < NQ; ++q) {
         const int r = r0 + lane + WAVE * q;
         if (r > col && r < NP) {
@@ -189,14 +194,16 @@ __device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int
     S.dst[lane] = key;
     S.src[lane] = val;
   }
-#pragma unroll
-  for (int I = 0; I < NB; ++I) {
-    const uint32_t sm = (uint32_t)__ballot(rep && val / TB == I);
-    const uint32_t dm = (uint32_t)__ballot(rep && key / TB == I);
-    if (lane == 0) {
-      S.smask[I] = sm;
-      S.dmask[I] = dm;
-    }
+  // row -> slot tables: every tile lane then finds its rows' slots with independent LDS reads
+  // (no serial walk over the slots)
+  for (int i = lane; i < NP; i += WAVE) {
+    S.sslot[i] = -1;
+    S.dslot[i] = -1;
+  }
+  wave_lds_sync();
+  if (rep) {
+    S.sslot[val] = lane;
+    S.dslot[key] = lane;
   }
 }
 
@@ -257,11 +264,11 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       for (int s = 0; s < NT; ++s) {
         const int ti = w + LU_WAVES * s;
         const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J != K) {
-          for (uint32_t mk = I >= K ? S.smask[I] : 0u; mk; mk &= mk - 1) {
-            const int q = __builtin_ctz(mk);
-            const int sr = S.src[q];
-            if (lg == (sr & 3)) S.X[q * NP + J * TB + lc] = comp(t[s], (sr % TB) >> 2);
+        if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = S.sslot[I * TB + lg + 4 * r];
+            if (q >= 0) S.X[q * NP + J * TB + lc] = t[s][r];
           }
         } else if (ti < NB * NB && J == K && I >= K) {
 #pragma unroll
@@ -273,11 +280,11 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       for (int s = 0; s < NT; ++s) {
         const int ti = w + LU_WAVES * s;
         const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J != K) {
-          for (uint32_t mk = I >= K ? S.dmask[I] : 0u; mk; mk &= mk - 1) {
-            const int q = __builtin_ctz(mk);
-            const int dr = S.dst[q];
-            if (lg == (dr & 3)) set_comp(t[s], (dr % TB) >> 2, S.X[q * NP + J * TB + lc]);
+        if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int q = S.dslot[I * TB + lg + 4 * r];
+            if (q >= 0) t[s][r] = S.X[q * NP + J * TB + lc];
           }
         }
       }

@@ -1,0 +1,9 @@
+#!/bin/bash
+# Standalone LU builds for scripts/lu_ab.py: base and no-swap (timing experiment).
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p pychemkin_amd/_lib/ab
+F="-O3 -std=c++17 -fPIC -shared -mcode-object-version=5 --offload-arch=gfx950"
+/opt/rocm/bin/hipcc $F -o pychemkin_amd/_lib/ab/lu_base.so pychemkin_amd/csrc/ckmi_lu.hip &
+/opt/rocm/bin/hipcc $F -DCKMI_LU_EXPT_NOSWAP -o pychemkin_amd/_lib/ab/lu_noswap.so pychemkin_amd/csrc/ckmi_lu.hip &
+wait
