@@ -98,6 +98,32 @@ def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
     return TT, PP, ch4_air_Y(mech, FF)
 
 
+def rop_bench(dev, mech, ns, reps=3):
+    """ROP + thermo over ns random (T, P, Y) states of `mech` (ckmi_rop_thermo), HIP-event timed."""
+    tables = mech.to_tables()
+    ops = count_ops(tables)
+    dm = _native.DeviceMechanism(tables, device=dev)
+    rng = np.random.default_rng(0)
+    Ts = torch.as_tensor(rng.uniform(300.0, 3000.0, ns), device=dev)
+    Ps = torch.as_tensor(P_ATM * 10.0 ** rng.uniform(-1.0, 2.0, ns), device=dev)
+    Ys = torch.as_tensor(rng.dirichlet(0.5 * np.ones(mech.KK), ns).T.copy(), device=dev)
+    dm.rop_thermo(Ts, Ps, Ys)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        dm.rop_thermo(Ts, Ps, Ys)
+    e1.record()
+    torch.cuda.synchronize()
+    sec = e0.elapsed_time(e1) / 1e3 / reps
+    tf = ops["F_rop"] * ns / sec / 1e12
+    return {"mechanism": f"synthetic GRI-3.0 + tracers, KK = {mech.KK}, II = {mech.II}", "states": ns,
+            "value": ns / sec, "unit": "states/s", "ms_per_launch": sec * 1e3,
+            "roofline": {"bound": "mfma", "pipe": "fp64-valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                         "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "traffic": None}}
+
+
 def lu_bench(dev, nsys, n):
     """Batched LU (ckmi_lu_factor_batched) on nsys Newton-like matrices I - gamma J of size n, timed with HIP
     events on the stream it is launched on; algorithmic work (2/3) n^3 per matrix."""
@@ -140,6 +166,8 @@ def main():
     ap.add_argument("--rop-states", type=int, default=10_000_000)
     ap.add_argument("--lu-systems", type=int, default=16384,
                     help="configs[4] component: batched n = 161 Newton-matrix LU on MFMA (0 = skip)")
+    ap.add_argument("--big-states", type=int, default=1_000_000,
+                    help="configs[4] component: ROP+thermo on the synthetic 161-species mechanism (0 = skip)")
     ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -268,6 +296,12 @@ def main():
     if rank == 0 and args.lu_systems > 0:
         lu = lu_bench(dev, args.lu_systems, 161)
 
+    rop_big = None
+    if rank == 0 and args.big_states > 0:
+        rop_big = rop_bench(dev, Mechanism.from_files(os.path.join(ROOT, "data", "gri30_tracer161_chem.inp"),
+                                                      os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat")),
+                            args.big_states)
+
     # ---- CPU baseline (rank 0, N = 1): oracle C restatement on a strided sample
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
@@ -333,6 +367,7 @@ def main():
             "cpu_baseline": cpu,
             "rop": rop,
             "lu": lu,
+            "rop_161sp": rop_big,
             "pcie_inclusive": pcie,
         }
         print(json.dumps(line), flush=True)

@@ -945,39 +945,50 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
 // half-chunk's wdot_1..wdot_KK, cp, h go back the same way, so every HBM request covers whole
 // 64-B halves of 128-B lines (one state at a time, lane = species, touched 53 lines with 8 B
 // each: 8.8x the algorithmic traffic, measured).
+//
+// Mechanisms with more than 63 species (up to 255) run the same kernel with NCH = KKp / 64
+// species per lane (lane + 64 j) and half as many waves per workgroup (the image, the species
+// arrays and the staging rows grow with KK).
 constexpr int ROP_WAVES = 8;
 constexpr int ROP_CHUNK = 16;
 constexpr int ROP_SUB = 8;
 constexpr int ROP_LD = ROP_SUB + 1;  // odd row stride: lane = species reads of one state spread over the banks
+__host__ __device__ constexpr int rop_waves(int nch) { return nch == 1 ? ROP_WAVES : 4; }
 __host__ __device__ constexpr int rop_io_bytes(int KK) { return align16(8 * ROP_LD * (KK + 2)); }
-__host__ __device__ constexpr int rop_slice_bytes(int G, int KK) {
-  return align16(8 * (3 * VL + (G > 0 ? G : 1))) + rop_io_bytes(KK);
+__host__ __device__ constexpr int rop_slice_bytes(int G, int KK, int KKp) {
+  return align16(8 * (3 * KKp + (G > 0 ? G : 1))) + rop_io_bytes(KK);
 }
 
-template <int MODE>  // 0: wdot + cp + h, 1: qf / qr
-__global__ __launch_bounds__(ROP_WAVES* WAVE) void rop_kernel(MechImage img, const int* __restrict__ orig, int nstate,
-                                                               const double* __restrict__ Tv,
-                                                               const double* __restrict__ Pv,
-                                                               const double* __restrict__ Yv, double* __restrict__ o0,
-                                                               double* __restrict__ o1, double* __restrict__ o2) {
+template <int MODE, int NCH>  // MODE 0: wdot + cp + h, 1: qf / qr; NCH species per lane
+__global__ __launch_bounds__(rop_waves(NCH)* WAVE) void rop_kernel(MechImage img, const int* __restrict__ orig,
+                                                                  int nstate, const double* __restrict__ Tv,
+                                                                  const double* __restrict__ Pv,
+                                                                  const double* __restrict__ Yv,
+                                                                  double* __restrict__ o0, double* __restrict__ o1,
+                                                                  double* __restrict__ o2) {
+  constexpr int NW = rop_waves(NCH);
   stage_image(0, img);
   const MechView V = make_view(0, img);
   const int wid = threadIdx.x / WAVE;
   const int lane = threadIdx.x % WAVE;
-  const int oC = img.bytes + wid * rop_slice_bytes(img.G, img.KK);
+  const int KKp = img.KKp;
+  const int slice = rop_slice_bytes(img.G, img.KK, KKp);
+  const int oC = img.bytes + wid * slice;
   double* C = lds_at<double>(oC);
-  double* gRT = C + VL;
-  double* wdot = gRT + VL;
-  double* Mg = wdot + VL;
+  double* gRT = C + KKp;
+  double* wdot = gRT + KKp;
+  double* Mg = wdot + KKp;
   const int KK = V.KK;
+  const int sp_one = img.sp_one;
   // half-chunk staging rows [KK + 2][ROP_SUB]: T, P, Y_k in; cp, h, wdot_k out (same slots)
-  double* io = lds_at<double>(oC + rop_slice_bytes(img.G, img.KK) - rop_io_bytes(img.KK));
+  double* io = lds_at<double>(oC + slice - rop_io_bytes(img.KK));
   const int nrow = KK + 2;
   const int io_c = lane & (ROP_SUB - 1), io_r = lane / ROP_SUB;
-  const bool isp = lane < KK;
-  const double rw = isp ? V.rwt()[lane] : 0.0;
+  double rw[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) rw[j] = lane + WAVE * j < KK ? V.rwt()[lane + WAVE * j] : 0.0;
   const int ntask = (nstate + ROP_CHUNK - 1) / ROP_CHUNK;
-  for (int task = blockIdx.x * ROP_WAVES + wid; task < ntask; task += gridDim.x * ROP_WAVES) {
+  for (int task = blockIdx.x * NW + wid; task < ntask; task += gridDim.x * NW) {
     const int s1 = min(nstate, (task + 1) * ROP_CHUNK);
     for (int st = task * ROP_CHUNK; st < s1; ++st) {
       const int c = st & (ROP_SUB - 1);
@@ -992,21 +1003,32 @@ __global__ __launch_bounds__(ROP_WAVES* WAVE) void rop_kernel(MechImage img, con
         wave_lds_sync();
       }
       const double T = io[c], P = io[ROP_LD + c];
-      const double yk = isp ? io[(2 + lane) * ROP_LD + c] : 0.0;
-      const double sumYW = wave_sum(yk * rw);
+      double yk[NCH];
+      double syw = 0.0;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int k = lane + WAVE * j;
+        yk[j] = k < KK ? io[(2 + k) * ROP_LD + c] : 0.0;
+        syw = fma(yk[j], rw[j], syw);
+      }
+      const double sumYW = wave_sum(syw);
       const double rho = P / (RU * T * sumYW);
       const double lnT = log(T), invT = 1.0 / T, lnPRT = LN_PATM_RU - lnT;
       double cpm = 0.0, hm = 0.0;
-      if (isp) {
-        const Thermo7 th = nasa7_img(V, lane, T, lnT, invT);
-        C[lane] = rho * yk * rw;
-        gRT[lane] = th.hRT - th.sR;
-        wdot[lane] = 0.0;
-        cpm = yk * th.cpR * RU * rw;
-        hm = yk * th.hRT * RU * T * rw;
-      } else if (lane == SP_ONE) {
-        C[SP_ONE] = 1.0;
-        gRT[SP_ONE] = 0.0;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int k = lane + WAVE * j;
+        if (k < KK) {
+          const Thermo7 th = nasa7_img(V, k, T, lnT, invT);
+          C[k] = rho * yk[j] * rw[j];
+          gRT[k] = th.hRT - th.sR;
+          wdot[k] = 0.0;
+          cpm += yk[j] * th.cpR * RU * rw[j];
+          hm += yk[j] * th.hRT * RU * T * rw[j];
+        } else if (k == sp_one) {
+          C[sp_one] = 1.0;
+          gRT[sp_one] = 0.0;
+        }
       }
       const double Ctot = rho * sumYW;
       wave_lds_sync();
@@ -1030,24 +1052,20 @@ __global__ __launch_bounds__(ROP_WAVES* WAVE) void rop_kernel(MechImage img, con
           o1[(size_t)oi * nstate + st] = qr;
         } else {
           const double q = qf - qr;
-#ifdef CKMI_EXPT_NOATOM
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (u < nr) wdot[sp_of(rs, u)] = -q;
-            if (u < np) wdot[sp_of(ps, u)] = q;
-          }
-#else
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             if (u < nr) atomicAdd(&wdot[sp_of(rs, u)], -q);
             if (u < np) atomicAdd(&wdot[sp_of(ps, u)], q);
           }
-#endif
         }
       }
       if (MODE == 0) {
         wave_lds_sync();
-        if (isp) io[(2 + lane) * ROP_LD + c] = wdot[lane];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+          const int k = lane + WAVE * j;
+          if (k < KK) io[(2 + k) * ROP_LD + c] = wdot[k];
+        }
         const double cps = wave_sum(cpm), hs = wave_sum(hm);
         if (lane == 0) {
           io[c] = cps;
@@ -1123,8 +1141,10 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
                 const std::vector<int>& tb, const std::vector<int>& gptr, const std::vector<int>& gsp,
                 const std::vector<double>& geff, const std::vector<double>& wt, const std::vector<double>& rwt) {
   const int KK = m->KK, IIp = m->IIpad, G = m->G;
-  const int KKp = (KK + WAVE - 1) / WAVE * WAVE;
-  if (KK > SP_ONE) return fail(CKMI_ERR_UNSUPPORTED, "more than 63 species not supported by the mechanism image");
+  const int KKp = (KK + 1 + WAVE - 1) / WAVE * WAVE;  // room for the dummy species slot
+  const int sp_one = KKp - 1;                          // = SP_ONE (63) whenever KK <= 63
+  if (KK > KK_IMAGE_MAX)
+    return fail(CKMI_ERR_UNSUPPORTED, "more than 255 species not supported by the mechanism image");
   std::vector<uint32_t> urs(IIp, 0), ups(IIp, 0), unu(IIp, 0), uinfo(IIp, 0);
   std::vector<double> aux;
   int naux = 0;
@@ -1149,8 +1169,8 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     }
     if (ns_r > 4 || ns_p > 4)
       return fail(CKMI_ERR_UNSUPPORTED, "more than 4 molecules (sum of coefficients) on a reaction side");
-    for (int u = ns_r; u < 4; ++u) a |= (uint32_t)SP_ONE << (8 * u);
-    for (int u = ns_p; u < 4; ++u) b |= (uint32_t)SP_ONE << (8 * u);
+    for (int u = ns_r; u < 4; ++u) a |= (uint32_t)sp_one << (8 * u);
+    for (int u = ns_p; u < 4; ++u) b |= (uint32_t)sp_one << (8 * u);
     urs[s] = a;
     ups[s] = b;
     unu[s] = nu;
@@ -1194,6 +1214,7 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   MechImage& I = m->img;
   I.KK = KK;
   I.KKp = KKp;
+  I.sp_one = sp_one;
   I.II = m->II;
   I.IIp = IIp;
   I.G = G;
@@ -1215,8 +1236,11 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   const double dzero = 0.0;
   I.o_gsp = gsp.empty() ? put(&zero, 4) : put(gsp.data(), gsp.size() * 4);
   I.o_geff = geff.empty() ? put(&dzero, 8) : put(geff.data(), geff.size() * 8);
-  std::vector<double> geffd((size_t)std::max(G, 1) * KKp, 0.0);
-  for (int g = 0; g < G; ++g)
+  // dense efficiency rows: only the reactor kernel's CKMI_MG_DENSE variant reads them, and only for
+  // KK <= 63; larger mechanisms get a one-row stub so that the image fits in LDS (G x KKp grows fast)
+  const bool dense = KK <= SP_ONE;
+  std::vector<double> geffd(dense ? (size_t)std::max(G, 1) * KKp : (size_t)2, 0.0);
+  for (int g = 0; dense && g < G; ++g)
     for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)g * KKp + gsp[e]] = geff[e];
   I.o_geffd = put(geffd.data(), geffd.size() * 8);
   {
@@ -1270,20 +1294,37 @@ int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t 
   return CKMI_OK;
 }
 
+template <int MODE, int NCH>
+int launch_rop_n(const ckmi_mech* m, int n, const double* T, const double* P, const double* Y, double* o0,
+                 double* o1, double* o2, hipStream_t stream) {
+  constexpr int NW = rop_waves(NCH);
+  const size_t lds = (size_t)m->img.bytes + (size_t)NW * rop_slice_bytes(m->G, m->img.KK, m->img.KKp);
+  int ncu = 0, per_cu = 0, lds_max = 0;
+  HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
+  HIP_CHECK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, m->device));
+  if (lds > (size_t)lds_max) return fail(CKMI_ERR_SIZE, "mechanism image + ROP work space exceed the LDS of a CU");
+  HIP_CHECK(hipFuncSetAttribute((const void*)rop_kernel<MODE, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rop_kernel<MODE, NCH>, NW * WAVE, lds));
+  if (per_cu < 1) return fail(CKMI_ERR_SIZE, "ROP kernel does not fit on a CU");
+  const int tasks = (n + ROP_CHUNK - 1) / ROP_CHUNK;
+  const int grid = std::max(1, std::min(ncu * per_cu, (tasks + NW - 1) / NW));
+  hipLaunchKernelGGL((rop_kernel<MODE, NCH>), dim3(grid), dim3(NW * WAVE), lds, stream, m->img, m->d.orig, n, T, P,
+                     Y, o0, o1, o2);
+  HIP_CHECK(hipGetLastError());
+  return CKMI_OK;
+}
+
 template <int MODE>
 int launch_rop(const ckmi_mech* m, int n, const double* T, const double* P, const double* Y, double* o0, double* o1,
                double* o2, hipStream_t stream) {
-  const size_t lds = (size_t)m->img.bytes + (size_t)ROP_WAVES * rop_slice_bytes(m->G, m->img.KK);
-  int ncu = 0, per_cu = 0;
-  HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rop_kernel<MODE>, ROP_WAVES * WAVE, lds));
-  if (per_cu < 1) return fail(CKMI_ERR_SIZE, "ROP kernel does not fit on a CU");
-  const int tasks = (n + ROP_CHUNK - 1) / ROP_CHUNK;
-  const int grid = std::max(1, std::min(ncu * per_cu, (tasks + ROP_WAVES - 1) / ROP_WAVES));
-  hipLaunchKernelGGL(rop_kernel<MODE>, dim3(grid), dim3(ROP_WAVES * WAVE), lds, stream, m->img, m->d.orig, n, T, P, Y,
-                     o0, o1, o2);
-  HIP_CHECK(hipGetLastError());
-  return CKMI_OK;
+  switch (m->img.KKp / WAVE) {
+    case 1: return launch_rop_n<MODE, 1>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 2: return launch_rop_n<MODE, 2>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 3: return launch_rop_n<MODE, 3>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 4: return launch_rop_n<MODE, 4>(m, n, T, P, Y, o0, o1, o2, stream);
+    default: return fail(CKMI_ERR_UNSUPPORTED, "mechanism image with more than 255 species");
+  }
 }
 
 }  // namespace
@@ -1305,7 +1346,7 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   if (!d || !out) return fail(CKMI_ERR_ARG, "null argument");
   const int KK = d->KK, II = d->II;
   if (KK <= 0 || II < 0) return fail(CKMI_ERR_SIZE, "bad sizes");
-  if (KK + 1 > 64) return fail(CKMI_ERR_UNSUPPORTED, "more than 63 species not supported by this build");
+  if (KK > KK_IMAGE_MAX) return fail(CKMI_ERR_UNSUPPORTED, "more than 255 species not supported by this build");
   auto* m = new ckmi_mech();
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
@@ -1549,6 +1590,9 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
                         double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
                         void* stream) {
   if (!m || !cfg || n < 0) return fail(CKMI_ERR_ARG, "bad argument");
+  if (m->KK + 1 > 64)  // the wave-per-reactor integrator: lane = state component
+    return fail(CKMI_ERR_UNSUPPORTED, "batch reactors with more than 63 species are not supported yet "
+                                      "(the ROP/thermo kernels and ckmi_lu_factor_batched are)");
   if (cfg->nprof < 0 || cfg->nprof > 64) return fail(CKMI_ERR_ARG, "nprof must be in [0, 64]");
   if (!(cfg->t_end > 0.0) || !(cfg->rtol > 0.0) || !(cfg->atol > 0.0)) return fail(CKMI_ERR_ARG, "t_end, rtol, atol must be > 0");
   if (cfg->energy != 1 && cfg->energy != 2) return fail(CKMI_ERR_ARG, "energy must be 1 or 2");

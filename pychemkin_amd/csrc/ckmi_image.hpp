@@ -11,9 +11,10 @@
 //   wt    double [KKp], rwt double [KKp]
 //   lnA, beta, Ea  double [IIp]
 //   rsp, psp  u32 [IIp]   four unit-coefficient species slots per side, one byte each: a species
-//                         with coefficient 2 occupies two slots; unused slots hold SP_ONE (63),
-//                         whose per-wave C is 1 and g/RT, h/RT are 0, so products and sums over
-//                         the four slots need no guards
+//                         with coefficient 2 occupies two slots; unused slots hold the dummy
+//                         species sp_one = KKp - 1 (63 for KK <= 63; KKp = KK + 1 rounded up to
+//                         64), whose per-wave C is 1 and g/RT, h/RT are 0, so products and sums
+//                         over the four slots need no guards
 //   nu        u32 [IIp]   (unused by the device kernels; kept for layout stability)
 //   info      u32 [IIp]   type:2 rev:1 hasrev:1 ftype:3 nr:3 np:3 | aux index << 16
 //   tb        i32 [IIp]   >= 0 third-body group, <= -2 single collider species -(tb+2), -1 none
@@ -29,13 +30,15 @@
 namespace ckmi {
 
 constexpr int AUXW = 12;
-constexpr int SP_ONE = 63;  // dummy species slot: C = 1, g/RT = h/RT = 0 (KK <= 63)
+constexpr int SP_ONE = 63;  // dummy species slot of the reactor kernel's images (KK <= 63)
+constexpr int KK_IMAGE_MAX = 255;  // species bytes: the dummy slot KKp - 1 must fit in 8 bits
 
 struct MechImage {
   const uint4* blob;  // device copy of the image
   const int* slot_of; // device: original reaction index -> device slot
   int bytes;          // multiple of 16
   int KK, KKp, II, IIp, G, naux;
+  int sp_one;         // dummy species slot (KKp - 1)
   int o_th, o_wt, o_rwt, o_lnA, o_beta, o_Ea, o_rsp, o_psp, o_nu, o_info, o_tb, o_aux, o_gptr, o_gsp, o_geff, o_geffd, o_e2t;
 };
 

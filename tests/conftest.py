@@ -158,3 +158,15 @@ def hp_equilibrium_start(mech, tables, phi, T_reac=295.15):
         else:
             lo = mid
     return 0.5 * (lo + hi), Yp
+
+
+BIG_CHEM = os.path.join(ROOT, "data", "gri30_tracer161_chem.inp")
+BIG_THERM = os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat")
+
+
+@pytest.fixture(scope="session")
+def big_mech():
+    """Synthetic 161-species mechanism (data/make_tracer_mechanism.py)."""
+    from pychemkin_amd.mechanism import Mechanism
+
+    return Mechanism.from_files(BIG_CHEM, BIG_THERM)

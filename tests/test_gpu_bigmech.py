@@ -1,0 +1,98 @@
+"""Large-mechanism kernels (configs[4] size) on the synthetic 161-species mechanism.
+
+No ~160-species mechanism exists offline, so these results are checked against the oracle
+(itself checked against the numpy restatement on the same mechanism, test_oracle_independent.py)
+and LAPACK, not against the reference: parity with Chemkin is unpinned for this size.
+Tolerances as for GRI-3.0 (test_gpu_kernels.py): 1e-11 of the largest |wdot| of a state.
+"""
+import numpy as np
+import pytest
+import scipy.linalg as sla
+
+from conftest import P_ATM
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def big(big_mech):
+    from oracle.oracle import Oracle
+    from pychemkin_amd import _native
+
+    return big_mech, Oracle(big_mech), _native.DeviceMechanism(big_mech.to_tables())
+
+
+def _states(KK, n, seed):
+    rng = np.random.default_rng(seed)
+    T = rng.uniform(300.0, 3000.0, n)
+    P = P_ATM * 10.0 ** rng.uniform(-1.0, 2.0, n)
+    Y = rng.dirichlet(0.5 * np.ones(KK), n).T.copy()
+    return T, P, Y
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 17, 1000])
+def test_rop_thermo_161_species(big, n):
+    mech, orc, dm = big
+    T, P, Y = _states(mech.KK, n, seed=n)
+    w, cp, h = (x.cpu().numpy() for x in dm.rop_thermo(T, P, Y))
+    wo, cpo, ho = orc.rop_batch(T, P, Y)
+    scale = np.max(np.abs(wo), axis=0, keepdims=True)
+    assert np.max(np.abs(w - wo) / scale) < 1e-11
+    assert np.max(np.abs(cp / cpo - 1)) < 1e-12
+    assert np.max(np.abs(h - ho) / np.max(np.abs(ho))) < 1e-12
+    # the tracer block (species 53..160) is active, not all zero
+    assert np.max(np.abs(w[53:])) > 0
+
+
+def test_reaction_rates_and_thermo_161_species(big):
+    mech, orc, dm = big
+    T, P, Y = _states(mech.KK, 19, seed=3)
+    qf, qr = (x.cpu().numpy() for x in dm.reaction_rates(T, P, Y))
+    for j in range(T.size):
+        qfo, qro, _ = orc.rates(T[j], P[j], Y[:, j])
+        sc = max(np.max(np.abs(qfo)), np.max(np.abs(qro)))
+        assert np.max(np.abs(qf[:, j] - qfo)) < 1e-11 * sc
+        assert np.max(np.abs(qr[:, j] - qro)) < 1e-11 * sc
+    cp, hh, s = (x.cpu().numpy() for x in dm.species_thermo(T))
+    for j in range(T.size):
+        cpo, ho, so = orc.thermo(T[j])
+        assert np.allclose(cp[:, j], cpo, rtol=1e-13, atol=0)
+        assert np.allclose(hh[:, j], ho, rtol=1e-12, atol=1e-12)
+
+
+def test_newton_matrices_161_species_lu(big):
+    """Newton matrices I - gamma J of the 161-species mechanism (n = 162, J from the oracle's
+    analytic Jacobian at burning states) through ckmi_lu_factor_batched: LAPACK pivots exactly,
+    factors to rounding."""
+    import torch
+    from pychemkin_amd import _native
+
+    mech, orc, _ = big
+    rng = np.random.default_rng(11)
+    mats = []
+    for i in range(12):
+        T = rng.uniform(1200.0, 2800.0)
+        Y = rng.dirichlet(0.5 * np.ones(mech.KK))
+        y = np.concatenate([[T], Y])
+        _, J = orc.rhs_jac(y, problem=1 + i % 2, P0=P_ATM * 10.0 ** rng.uniform(0, 2))
+        gamma = 10.0 ** rng.uniform(-9, -6)
+        mats.append(np.eye(y.size) - gamma * J)
+    A = np.stack(mats)
+    At = torch.as_tensor(A.copy(), device="cuda:0")
+    _, piv, info = _native.lu_factor_batched(At)
+    LU, piv, info = At.cpu().numpy(), piv.cpu().numpy(), info.cpu().numpy()
+    assert np.all(info == 0)
+    for s in range(A.shape[0]):
+        lu_ref, piv_ref = sla.lu_factor(A[s])
+        np.testing.assert_array_equal(piv[s], piv_ref)
+        np.testing.assert_allclose(LU[s], lu_ref, rtol=0, atol=1e-12 * np.abs(lu_ref).max())
+
+
+def test_reactor_run_rejects_161_species_loudly(big):
+    from pychemkin_amd import _native
+
+    mech, _, dm = big
+    Y0 = np.zeros((1, mech.KK))
+    Y0[0, mech.species.index("N2")] = 1.0
+    with pytest.raises(_native.NativeError, match="63 species"):
+        dm.reactor_run(_native.make_cfg(energy=1, t_end=1e-3), np.ones(1, np.int32), [1000.0], [P_ATM], [1.0], Y0)

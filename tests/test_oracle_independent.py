@@ -122,3 +122,25 @@ def test_gfac_scales_all_rates(oracle, mech):
     f1, _ = oracle.rhs_jac(y)
     f2, _ = oracle.rhs_jac(y, gfac=2.0)
     assert np.allclose(f2, 2.0 * f1, rtol=1e-13, atol=0)
+
+
+def test_c_oracle_matches_numpy_on_161_species_mechanism(big_mech):
+    """The synthetic configs[4]-sized mechanism (GRI-3.0 + 108 tracer species, conftest.
+    write_big_mechanism): the C oracle and the dense-matrix numpy restatement agree, so the oracle
+    can check the > 63-species kernels."""
+    from oracle.oracle import Oracle
+
+    tables = big_mech.to_tables()
+    orc = Oracle(big_mech)
+    nk = NumpyKinetics(tables)
+    rng = np.random.default_rng(5)
+    for _ in range(10):
+        T = rng.uniform(300, 3000)
+        P = P_ATM * 10 ** rng.uniform(-1, 2)
+        Y = rng.dirichlet(0.5 * np.ones(big_mech.KK))
+        qf, qr, w = orc.rates(T, P, Y)
+        qf2, qr2, w2 = nk.rates(T, P, Y)
+        assert np.allclose(qf, qf2, rtol=1e-11, atol=1e-300)
+        assert np.allclose(qr, qr2, rtol=1e-10, atol=1e-300)
+        assert np.max(np.abs(w - w2)) <= 1e-10 * np.max(np.abs(w2))
+    assert big_mech.KK == 161 and np.any(tables["rsp"] > 63) and np.any(tables["eff_sp"] > 63)
