@@ -93,9 +93,6 @@ struct LuSmem {
   int info;
 };
 
-template <int NB>
-__device__ __forceinline__ void panel_finish(LuSmem<NB>& S, int K, int lane);
-
 // Step 2: wave 0 factors panel K in LDS.  Rows K*16 .. NP-1, columns 0..15 of S.P.
 template <int NB>
 __device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int n) {
@@ -155,102 +152,6 @@ __device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int
     }
     wave_lds_sync();
   }
-  panel_finish<NB>(S, K, lane);
-}
-
-// Step 2 with the panel in registers (the dedicated panel wave of lu_factor_kernel_pw, which owns
-// no tiles): lane l holds rows r0 + l + 64 q, q < NQ, all 16 columns.  The pivot search, the row
-// interchange (v_readlane of the two rows) and the rank-1 update need no LDS round trip; the
-// panel goes back to S.P once at the end.  Same pivot rule (first row of maximal |a|) and the
-// same arithmetic per element as panel_factor.
-template <int NB>
-__device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, int K, int lane, int n) {
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
-  const int r0 = K * TB;
-  double pv[NQ][TB];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int r = r0 + lane + WAVE * q;
-#pragma unroll
-    for (int cc = 0; cc < TB; ++cc) pv[q][cc] = r < NP ? S.P[r * PLD + cc] : 0.0;
-  }
-#pragma unroll
-  for (int c = 0; c < TB; ++c) {
-    const int col = r0 + c;
-    double best = -1.0;
-    int bq = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int r = r0 + lane + WAVE * q;
-      if (r >= col && r < NP) {
-        const double v = fabs(pv[q][c]);
-        if (v > best) {
-          best = v;
-          bq = q;
-        }
-      }
-    }
-    const double maxv = wave_max(best);
-    int p = col;
-#pragma unroll
-    for (int q = NQ - 1; q >= 0; --q) {
-      const uint64_t mq = __ballot(best == maxv && bq == q);
-      if (mq) p = r0 + (int)__ffsll((unsigned long long)mq) - 1 + WAVE * q;
-    }
-    p = __builtin_amdgcn_readfirstlane(p);
-    if (lane == 0) S.piv[c] = p;
-    if (maxv != 0.0) {
-      const int qp = __builtin_amdgcn_readfirstlane((p - r0) / WAVE), lp = __builtin_amdgcn_readfirstlane((p - r0) % WAVE);
-      double prow[TB];
-      if (p != col) {
-        // row col is lane c of level 0; swap it with row p (lane lp of level qp), all 16 columns
-#pragma unroll
-        for (int cc = 0; cc < TB; ++cc) {
-          double src = pv[0][cc];
-#pragma unroll
-          for (int q = 1; q < NQ; ++q) src = qp == q ? pv[q][cc] : src;
-          prow[cc] = bcast(src, lp);
-          const double crow = bcast(pv[0][cc], c);
-          if (lane == c) pv[0][cc] = prow[cc];
-#pragma unroll
-          for (int q = 0; q < NQ; ++q)
-            if (q == qp && lane == lp) pv[q][cc] = crow;
-        }
-      } else {
-#pragma unroll
-        for (int cc = 0; cc < TB; ++cc) prow[cc] = bcast(pv[0][cc], c);
-      }
-      const double rp = 1.0 / prow[c];
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int r = r0 + lane + WAVE * q;
-        if (r > col && r < NP) {
-          const double l = pv[q][c] * rp;
-          pv[q][c] = l;
-#pragma unroll
-          for (int cc = c + 1; cc < TB; ++cc) pv[q][cc] = fma(-l, prow[cc], pv[q][cc]);
-        }
-      }
-    } else if (lane == 0 && S.info == 0 && col < n) {
-      S.info = col + 1;  // LAPACK: U(col, col) is exactly zero
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int r = r0 + lane + WAVE * q;
-#pragma unroll
-    for (int cc = 0; cc < TB; ++cc)
-      if (r < NP) S.P[r * PLD + cc] = pv[q][cc];
-  }
-  wave_lds_sync();
-  panel_finish<NB>(S, K, lane);
-}
-
-// L11^-1, the net row permutation of the panel's interchanges and the row -> slot tables
-template <int NB>
-__device__ __forceinline__ void panel_finish(LuSmem<NB>& S, int K, int lane) {
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD;
-  const int r0 = K * TB;
   // L11^-1 (unit lower) by forward substitution on the identity, right-looking over columns m
   // of L11: lane (i, g) holds X[i][g + 4k], k = 0..3; row m is read from lane m + 16 g
   {
@@ -438,155 +339,6 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
   }
 }
 
-// Panel-wave variant (default): wave 0 owns no tiles and factors every panel with the panel in
-// its registers (panel_factor_reg); waves 1..7 own the tiles (7 per tile row sweep, NT = 18 for
-// n = 161).  The panel is the serial part of the factorisation (58 % of the shared-wave kernel's
-// time, measured by skipping it), and keeping it out of LDS removes its round trips.
-template <int NB>
-__global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel_pw(int nsys, int n, double* __restrict__ A,
-                                                                   int* __restrict__ ipiv, int* __restrict__ info) {
-  constexpr int TW = LU_WAVES - 1;  // tile waves 1..7; wave 0 is the panel wave
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NT = (NB * NB + TW - 1) / TW;
-  __shared__ LuSmem<NB> S;
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const int lc0 = lane & 15, lg0 = lane >> 4;
-
-  for (int sys = blockIdx.x; sys < nsys; sys += gridDim.x) {
-    if (w0 == 0) {
-      // panel wave: the same six barriers per panel as the tile waves
-      if (lane == 0) S.info = 0;
-      for (int K = 0; K < NB; ++K) {
-        __syncthreads();  // 1. panel tiles are in S.P
-        panel_factor_reg<NB>(S, K, lane, n);
-        if (lane < TB && K * TB + lane < n) ipiv[(size_t)sys * n + K * TB + lane] = S.piv[lane];
-        __syncthreads();  // 2. factored panel, Linv, slots
-        __syncthreads();  // 3. interchange sources in X
-        __syncthreads();  // 4. interchanges applied
-        __syncthreads();  // 5. U12 in X
-        __syncthreads();  // 6. trailing update done: P, X, piv may be rewritten
-      }
-      if (lane == 0) info[sys] = S.info;
-      __syncthreads();  // S.info
-      continue;
-    }
-    double* As = A + (size_t)sys * n * n;
-    d4 t[NT];
-    {
-      // laundered per matrix (the load offsets would otherwise be hoisted out of the sys loop)
-      int w = w0 - 1, lc = lc0, lg = lg0, nl = n;
-      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg), "+s"(nl));
-      // tile s of tile wave w (= wave w + 1) is tile index w + 7 s = (I, J) in row-major tile order
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        const int col = J * TB + lc;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = I * TB + lg + 4 * r;
-          double v = row == col ? 1.0 : 0.0;  // identity padding up to a multiple of 16
-          if (ti < NB * NB && row < nl && col < nl) v = As[(size_t)row * nl + col];
-          t[s][r] = v;
-        }
-      }
-    }
-    for (int K = 0; K < NB; ++K) {
-      // laundered per panel: keeps the per-tile indices and LDS addresses from being hoisted
-      // out of the K loop and held in registers for the whole factorisation
-      int w = w0 - 1, lc = lc0, lg = lg0;
-      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg));
-      // 1. panel tiles (I >= K, K) to LDS
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J == K && I >= K) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) S.P[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
-        }
-      }
-      __syncthreads();
-      // 2. the panel wave factors the panel
-      __syncthreads();
-      // 3. row interchanges in the other block columns (sources out), factored panel back in
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = S.sslot[I * TB + lg + 4 * r];
-            if (q >= 0) S.X[q * NP + J * TB + lc] = t[s][r];
-          }
-        } else if (ti < NB * NB && J == K && I >= K) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) t[s][r] = S.P[(I * TB + lg + 4 * r) * PLD + lc];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = S.dslot[I * TB + lg + 4 * r];
-            if (q >= 0) t[s][r] = S.X[q * NP + J * TB + lc];
-          }
-        }
-      }
-      __syncthreads();
-      // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (X reused as [16][NP])
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && I == K && J > K) {
-          d4 u = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk) u = mfma16(S.Linv[lc * PLD + 4 * kk + lg], t[s][kk], u);
-          t[s] = u;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) S.X[(lg + 4 * r) * NP + J * TB + lc] = u[r];
-        }
-      }
-      __syncthreads();
-      // 5. trailing update A22 -= L21 U12
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && I > K && J > K) {
-#pragma unroll
-          for (int kk = 0; kk < 4; ++kk)
-            t[s] = mfma16(-S.P[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
-        }
-      }
-      __syncthreads();  // P, X and piv are rewritten by the next panel
-    }
-    // opaque copies: otherwise the 4 NT store addresses are CSE'd with the load addresses and
-    // held in VGPRs through the whole factorisation
-    int n_st = n, lc_st = lc0, lg = lg0, w = w0 - 1;
-    double* Ast = As;
-    asm volatile("" : "+s"(n_st), "+v"(lc_st), "+s"(Ast), "+v"(lg), "+s"(w));
-#pragma unroll
-    for (int s = 0; s < NT; ++s) {
-      const int ti = w + TW * s;
-      const int I = ti / NB, J = ti % NB;
-      const int col = J * TB + lc_st;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = I * TB + lg + 4 * r;
-        if (ti < NB * NB && row < n_st && col < n_st) Ast[(size_t)row * n_st + col] = t[s][r];
-      }
-    }
-    __syncthreads();  // S.info
-  }
-}
-
 // One wave per right-hand side: x = U^-1 L^-1 P b, in place in B[sys][n].
 constexpr int SOLVE_WAVES = 4;
 __global__ __launch_bounds__(SOLVE_WAVES* WAVE) void lu_solve_kernel(int nsys, int n, const double* __restrict__ LU,
@@ -633,11 +385,7 @@ thread_local std::string g_lu_err;
 template <int NB>
 hipError_t launch_factor(int nsys, int n, double* A, int* ipiv, int* info, hipStream_t st) {
   const int grid = nsys < 8192 ? nsys : 8192;
-#ifndef CKMI_LU_PANEL_WAVE  // default: the panel factored in LDS by wave 0, which also owns tiles
   hipLaunchKernelGGL(lu_factor_kernel<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
-#else
-  hipLaunchKernelGGL(lu_factor_kernel_pw<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
-#endif
   return hipGetLastError();
 }
 

@@ -8,11 +8,14 @@ import sys
 import torch
 
 
-def time_lib(path, nsys=16384, n=161, reps=4):
+def time_lib(path, nsys=16384, n=161, reps=4, newton=False):
     lib = ct.CDLL(path)
     lib.ckmi_lu_factor_batched.argtypes = [ct.c_int32, ct.c_int32, ct.c_void_p, ct.c_void_p, ct.c_void_p, ct.c_void_p]
     g = torch.Generator(device="cuda:0").manual_seed(0)
     A0 = torch.randn((nsys, n, n), dtype=torch.float64, device="cuda:0", generator=g)
+    if newton:  # I - gamma J with J entries spread over 6 decades (bench.py lu_bench)
+        A0 = torch.eye(n, dtype=torch.float64, device="cuda:0") - 1e-6 * A0 * 10.0 ** (6.0 * torch.rand(
+            (nsys, n, n), dtype=torch.float64, device="cuda:0", generator=g))
     A = torch.empty_like(A0)
     ipiv = torch.empty((nsys, n), dtype=torch.int32, device="cuda:0")
     info = torch.empty(nsys, dtype=torch.int32, device="cuda:0")
@@ -29,9 +32,18 @@ def time_lib(path, nsys=16384, n=161, reps=4):
         assert rc == 0
         if it:
             ts.append(e0.elapsed_time(e1))
-    return sorted(ts)[len(ts) // 2]
+    return sorted(ts)[len(ts) // 2], A.cpu(), ipiv.cpu(), info.cpu()
 
 
 if __name__ == "__main__":
-    for p in sys.argv[1:]:
-        print(json.dumps({"lib": p, "ms": time_lib(p)}), flush=True)
+    for newton in (False, True):
+        ref = None
+        for p in sys.argv[1:]:
+            ms, A, ipiv, info = time_lib(p, newton=newton)
+            same = None
+            if ref is None:
+                ref = (A, ipiv, info)
+            else:
+                same = bool(torch.equal(A, ref[0]) and torch.equal(ipiv, ref[1]) and torch.equal(info, ref[2]))
+            print(json.dumps({"lib": p, "matrices": "newton" if newton else "randn", "ms": ms,
+                              "bitwise_equal_to_first": same}), flush=True)
