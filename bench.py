@@ -121,7 +121,7 @@ def rop_bench(dev, mech, ns, reps=3):
             "value": ns / sec, "unit": "states/s", "ms_per_launch": sec * 1e3,
             "roofline": {"bound": "mfma", "pipe": "fp64-valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                         "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "traffic": None}}
+                         "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "traffic": load_traffic("rop_161sp", ns)}}
 
 
 def lu_bench(dev, nsys, n):
@@ -151,7 +151,7 @@ def lu_bench(dev, nsys, n):
             "systems_per_s": nsys / sec, "singular": int((info != 0).sum().item()),
             "roofline": {"bound": "mfma", "pipe": "fp64-mfma", "achieved": flops / sec / 1e12,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": flops / sec / 1e12 / FP64_PEAK_TFLOPS,
-                         "hbm_GBs": nbytes / sec / 1e9, "traffic": None}}
+                         "hbm_GBs": nbytes / sec / 1e9, "traffic": load_traffic("lu", nsys)}}
 
 
 RUN = dict(energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")

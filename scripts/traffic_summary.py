@@ -20,7 +20,10 @@ def main():
         per = collections.defaultdict(float)
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            kind = "reactor" if "reactor_kernel" in k else ("rop" if "rop_kernel<0>" in k or "rop_kernel<0" in k else None)
+            kind = ("reactor" if "reactor_kernel" in k else
+                    "rop" if "rop_kernel<0, 1>" in k else           # GRI-3.0 (KK <= 63)
+                    "rop_161sp" if "rop_kernel<0, 3>" in k else     # synthetic 161-species mechanism
+                    "lu" if "lu_factor_kernel" in k else None)
             if kind is None:
                 continue
             per[(kind, row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
@@ -37,6 +40,10 @@ def main():
         out["reactor"]["units"] = 65536
     if "rop" in out:
         out["rop"]["units"] = 10_000_000
+    if "rop_161sp" in out:
+        out["rop_161sp"]["units"] = 1_000_000
+    if "lu" in out:
+        out["lu"]["units"] = 16384
     print(json.dumps(out, indent=1))
 
 
