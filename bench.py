@@ -288,7 +288,30 @@ def main():
                 "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "hbm_frac": ops["bytes_rop"] * ns / sec / 1e9 / HBM_PEAK_GBS,
                 "traffic": load_traffic("rop", ns),
             },
+            "cpu_baseline": None,
         }
+        if rank == 0 and world == 1 and args.cpu_sample > 0:
+            # oracle C restatement over the first 200k of the same states (OpenMP over states), and
+            # over the first 20k on one core; the GPU result of the same states is the checker
+            from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
+            orc_r = Oracle(mech)
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            m = min(ns, 200_000)
+            Th, Ph, Yh = Ts[:m].cpu().numpy(), Ps[:m].cpu().numpy(), Ys[:, :m].cpu().numpy()
+            tc = time.perf_counter()
+            wc, _, _ = orc_r.rop_batch(Th, Ph, Yh, nthreads=threads)
+            t_all = time.perf_counter() - tc
+            m1 = min(m, 20_000)
+            tc = time.perf_counter()
+            orc_r.rop_batch(Th[:m1], Ph[:m1], np.ascontiguousarray(Yh[:, :m1]), nthreads=1)
+            t_one = time.perf_counter() - tc
+            wg = wdot[:, :m].cpu().numpy()
+            rop["cpu_baseline"] = {
+                "value": m / t_all, "unit": "states/s", "cores": threads, "kind": "port",
+                "single_core_value": m1 / t_one,
+                "sample": f"first {m} of the same 10M states ({m1} on one core), oracle C restatement, OpenMP over states",
+                "wdot_max_rel_diff_vs_gpu": float(np.max(np.abs(wg - wc) / np.max(np.abs(wc), axis=0, keepdims=True))),
+            }
         del Ts, Ps, Ys, wdot, cp, hh
 
     # ---- configs[4] component: batched FP64 LU of n = 161 Newton matrices (MFMA trailing updates)
