@@ -96,3 +96,28 @@ def test_reactor_run_rejects_161_species_loudly(big):
     Y0[0, mech.species.index("N2")] = 1.0
     with pytest.raises(_native.NativeError, match="63 species"):
         dm.reactor_run(_native.make_cfg(energy=1, t_end=1e-3), np.ones(1, np.int32), [1000.0], [P_ATM], [1.0], Y0)
+
+
+def test_drop_in_api_on_161_species_mechanism(big):
+    """Chemistry.preprocess / Mixture.ROP / RxnRates / HML / CPBL (the reference's public names,
+    mixture.py:1693-1808) on the 161-species mechanism, through the GPU kernels."""
+    import pychemkin_amd as ck
+    from conftest import BIG_CHEM, BIG_THERM
+
+    mech, orc, _ = big
+    chem = ck.Chemistry(label="tracer161")
+    chem.chemfile = BIG_CHEM
+    chem.thermfile = BIG_THERM
+    chem.preprocess()
+    assert chem.KK == 161 and chem.IIGas == 505
+    m = ck.Mixture(chem)
+    m.temperature = 1700.0
+    m.pressure = 3 * P_ATM
+    m.X = [("CH4", 0.05), ("O2", 0.15), ("N2", 0.6), ("OH", 0.01), ("AX1", 0.1), ("AX60", 0.05), ("AX108", 0.04)]
+    qfo, qro, wo = orc.rates(1700.0, 3 * P_ATM, m.Y)
+    assert np.max(np.abs(m.ROP() - wo)) < 1e-11 * np.max(np.abs(wo))
+    qf, qr = m.RxnRates()
+    assert np.max(np.abs(qf - qfo)) < 1e-11 * np.max(np.abs(qfo))
+    assert np.max(np.abs(qr - qro)) < 1e-11 * np.max(np.abs(qro))
+    # tracer exchange AX1 + H <=> AX2 + H carries a nonzero rate
+    assert np.abs(m.ROP()[chem.get_specindex("AX2")]) > 0
