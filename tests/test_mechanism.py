@@ -101,3 +101,23 @@ def test_thermo_parser_roundtrip(mech):
     text = open(__import__("conftest").THERM).read()
     d = parse_thermo_text(text)
     assert len(d) == 53 and d["N2"].composition == {"N": 2}
+
+
+def test_tracer_mechanism_files_match_generator(tmp_path):
+    """data/gri30_tracer161_* (the configs[4]-sized stand-in) are exactly what
+    data/make_tracer_mechanism.py writes, and parse to KK = 161, II = 505."""
+    import importlib.util
+    import os
+
+    from conftest import BIG_CHEM, BIG_THERM, ROOT
+    from pychemkin_amd.mechanism import Mechanism
+
+    spec = importlib.util.spec_from_file_location("mtm", os.path.join(ROOT, "data", "make_tracer_mechanism.py"))
+    mtm = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mtm)
+    cp, tp = mtm.write_big_mechanism(str(tmp_path))
+    assert open(cp).read() == open(BIG_CHEM).read()
+    assert open(tp).read() == open(BIG_THERM).read()
+    m = Mechanism.from_files(BIG_CHEM, BIG_THERM)
+    assert (m.KK, m.II) == (161, 505)
+    assert m.species[53] == "AX1" and m.species[-1] == "AX108"
