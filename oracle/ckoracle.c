@@ -576,7 +576,9 @@ static int nls(bdf* b, int nflag) {
       } else {
         b->jcur = 0;
       }
-      for (int i = 0; i < n * n; ++i) b->M[i] = -b->gamma * b->J[i];
+      /* the device parks J in FP32 between setups (ckmi.hip reactor_kernel): M is built from
+         the same rounded J, so both take the same Newton iterations */
+      for (int i = 0; i < n * n; ++i) b->M[i] = -b->gamma * (double)(float)b->J[i];
       for (int i = 0; i < n; ++i) b->M[i * n + i] += 1.0;
       const int sing = lu_factor(n, b->M, b->piv);
       b->nlu++;

@@ -220,7 +220,10 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
   BdfS& S = *lds_at<BdfS>(oS);
   Ctl& c = *lds_at<Ctl>(oS + align16((int)sizeof(BdfS)));
   Ign& g = *lds_at<Ign>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)));
-  double* Jg = jws + ((size_t)blockIdx.x * RWAVES + wid) * N * WAVE;
+  // the wave's parked Jacobian, rounded to FP32: M = I - gamma J is rebuilt from it at every
+  // setup (5.6 per J); the modified Newton iteration only needs an approximate M, and half
+  // the bytes keep the slots of an XCD's 256 waves (3.5 MB) within its 4 MB L2
+  float* Jg = reinterpret_cast<float*>(jws) + ((size_t)blockIdx.x * RWAVES + wid) * N * WAVE;
   const int KK = V.KK;
   const int n = KK + 1;
   const bool isp = lane >= 1 && lane <= KK;
@@ -528,7 +531,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           {
             const double* Jsh = lds_at<const double>(oJ);
 #pragma unroll 2
-            for (int j = 0; j < N; ++j) Jg[j * WAVE + lane] = Jsh[j * LDJ + lane];
+            for (int j = 0; j < N; ++j) Jg[j * WAVE + lane] = (float)Jsh[j * LDJ + lane];
           }
           wave_lds_sync();
           if (lane == 0) atomicExch(lds_at<int>(olock), 0);

@@ -369,7 +369,8 @@ struct NewtonMatrix {
   double a[N];
   int permv;  // lane k: the lane whose row was the pivot of step k
 
-  __device__ __forceinline__ void build(const double* J, int ldj, double gamma, int lane_in, int n) {
+  template <typename TJ>
+  __device__ __forceinline__ void build(const TJ* J, int ldj, double gamma, int lane_in, int n) {
     const int lane = opaque_lane(lane_in);
 #pragma unroll
     for (int j = 0; j < N; ++j)
@@ -468,7 +469,8 @@ struct NewtonMatrix {
 
   // a = I - gamma J, J column-major with leading dimension ldj >= 64 (every lane reads its own
   // row; rows >= n are zero)
-  __device__ __forceinline__ void build(const double* J, int ldj, double gamma, int lane_in, int n) {
+  template <typename TJ>
+  __device__ __forceinline__ void build(const TJ* J, int ldj, double gamma, int lane_in, int n) {
     const int lane = opaque_lane(lane_in);
 #pragma unroll
     for (int j = 0; j < N; ++j) a[j] = (j == lane ? 1.0 : 0.0) - gamma * J[j * ldj + lane];
