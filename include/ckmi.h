@@ -43,6 +43,7 @@ extern "C" {
 #define CKMI_RXN_ELEMENTARY 0
 #define CKMI_RXN_THIRDBODY 1
 #define CKMI_RXN_FALLOFF 2
+#define CKMI_RXN_PLOG 3 /* elementary with a PLOG table: ln k linear in ln P, clamped outside */
 /* falloff forms */
 #define CKMI_FALL_NONE 0
 #define CKMI_FALL_LINDEMANN 1
@@ -80,6 +81,8 @@ typedef struct {
   const int32_t* eff_ptr; /* [II+1] CSR into eff_sp / eff_val */
   const int32_t* eff_sp;
   const double* eff_val;  /* third-body efficiencies (absolute) */
+  const int32_t* plog_ptr; /* [II+1] CSR into plog_par for CKMI_RXN_PLOG reactions (may be NULL if none) */
+  const double* plog_par;  /* [npl][4] ln P (dyn/cm2), ln A (cgs), b, E/R (K); ascending, distinct P */
 } ckmi_mech_desc;
 
 typedef struct ckmi_mech ckmi_mech; /* opaque: tables resident in HBM of one device */

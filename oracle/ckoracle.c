@@ -48,13 +48,44 @@ typedef struct {
   double kf, kr, mfac, pf, pr, dlkf, dlkr;
 } rxn_eval;
 
-static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, double lnPRT, const double* C,
-                          double Ctot, const double* g_RT, const double* h_RT, double dlnA, double gfac, rxn_eval* e) {
+/* PLOG (Chemkin "PLOG /P A b E/"): ln k interpolated linearly in ln P between the two bracketing
+ * pressures, clamped to the end points outside the table; d ln k / dT interpolated alike. */
+static void plog_rate(const cko_mech* m, int i, double lnP, double lnT, double invT, double* lnk, double* dlk) {
+  const int p0 = m->plog_ptr[i], n = m->plog_ptr[i + 1] - p0;
+  const double* t = m->plog_par + 4 * p0;
+  int j = 0;
+  while (j < n - 2 && lnP > t[4 * (j + 1)]) ++j;
+  const double lk0 = t[4 * j + 1] + t[4 * j + 2] * lnT - t[4 * j + 3] * invT;
+  const double dk0 = (t[4 * j + 2] + t[4 * j + 3] * invT) * invT;
+  if (n == 1) {
+    *lnk = lk0;
+    *dlk = dk0;
+    return;
+  }
+  const double* u = t + 4 * (j + 1);
+  const double lk1 = u[1] + u[2] * lnT - u[3] * invT;
+  const double dk1 = (u[2] + u[3] * invT) * invT;
+  double w = (lnP - t[4 * j]) / (u[0] - t[4 * j]);
+  w = w < 0.0 ? 0.0 : (w > 1.0 ? 1.0 : w);
+  *lnk = lk0 + w * (lk1 - lk0);
+  *dlk = dk0 + w * (dk1 - dk0);
+}
+
+static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, double lnPRT, double P,
+                          const double* C, double Ctot, const double* g_RT, const double* h_RT, double dlnA,
+                          double gfac, rxn_eval* e) {
   const double* a = m->arr + 3 * i;
-  double kf = exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
-  double dlkf = (a[1] + a[2] * invT) * invT;
+  double kf, dlkf;
   double mfac = 1.0;
   const int type = m->rtype[i];
+  if (type == 3) {
+    double lnk;
+    plog_rate(m, i, log(P), lnT, invT, &lnk, &dlkf);
+    kf = exp(lnk + dlnA);
+  } else {
+    kf = exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
+    dlkf = (a[1] + a[2] * invT) * invT;
+  }
   if (type == 1 || type == 2) {
     double M;
     if (m->tbsp[i] >= 0) {
@@ -147,7 +178,7 @@ void cko_rates(const cko_mech* m, double T, double P, const double* Y, double* q
   const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   for (int i = 0; i < m->II; ++i) {
     rxn_eval e;
-    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, 0.0, 1.0, &e);
+    eval_reaction(m, i, T, lnT, invT, lnPRT, P, C, Ctot, g_RT, h_RT, 0.0, 1.0, &e);
     double f = e.mfac * e.kf * e.pf, r = e.mfac * e.kr * e.pr;
     if (qf) qf[i] = f;
     if (qr) qr[i] = r;
@@ -256,7 +287,7 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
   const double lnT = log(T), invT = 1.0 / T, lnPRT = log(PATM / (RU * T));
   for (int i = 0; i < m->II; ++i) {
     rxn_eval e;
-    eval_reaction(m, i, T, lnT, invT, lnPRT, C, Ctot, g_RT, h_RT, i == c->cfg->pert_rxn ? dlnA_p : 0.0,
+    eval_reaction(m, i, T, lnT, invT, lnPRT, P, C, Ctot, g_RT, h_RT, i == c->cfg->pert_rxn ? dlnA_p : 0.0,
                   c->cfg->gfac, &e);
     const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
     const int* rs = m->rsp + CKO_SLOTS * i;

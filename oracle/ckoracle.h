@@ -24,7 +24,7 @@ typedef struct {
   int KK, II;
   const double* wt;      /* [KK] g/mol */
   const double* thermo;  /* [KK][17]: tlow, tmid, thigh, low a1..a7, high a1..a7 */
-  const int* rtype;      /* 0 elementary, 1 third body, 2 falloff */
+  const int* rtype;      /* 0 elementary, 1 third body, 2 falloff, 3 PLOG */
   const int* rev;        /* reversible flag */
   const int* nr; const int* np;
   const int* rsp; const int* psp;      /* [II][4] */
@@ -37,6 +37,8 @@ typedef struct {
   const double* fpar;    /* [II][5] */
   const int* tbsp;       /* -1 mixture, else species index */
   const int* eff_ptr; const int* eff_sp; const double* eff_val;
+  const int* plog_ptr;   /* [II+1] CSR into plog_par (rtype 3) */
+  const double* plog_par;/* [npl][4]: ln P (dyn/cm2), ln A (cgs), b, E/R; ascending P per reaction */
 } cko_mech;
 
 typedef struct {

@@ -40,6 +40,8 @@ class NumpyKinetics:
         self.ftype = t["ftype"]
         self.fpar = t["fpar"]
         self.tbsp = t["tbsp"]
+        self.plog_ptr = t["plog_ptr"]
+        self.plog_par = t["plog_par"]
         self.eff = np.ones((II, KK))
         for i in range(II):
             for p in range(t["eff_ptr"][i], t["eff_ptr"][i + 1]):
@@ -54,6 +56,12 @@ class NumpyKinetics:
         s = a[:, 0] * np.log(T) + T * (a[:, 1] + T * (a[:, 2] / 2 + T * (a[:, 3] / 3 + T * a[:, 4] / 4))) + a[:, 6]
         return cp, h, s
 
+    def _plog_k(self, i, P, T):
+        # PLOG: ln k linear in ln P between the bracketing table pressures, end values outside
+        tab = self.plog_par[self.plog_ptr[i]:self.plog_ptr[i + 1]]
+        lnk = tab[:, 1] + tab[:, 2] * np.log(T) - tab[:, 3] / T
+        return float(np.exp(np.interp(np.log(P), tab[:, 0], lnk)))
+
     def rates(self, T, P, Y):
         Y = np.asarray(Y, dtype=np.float64)
         rho = P / (RU * T) / np.sum(Y / self.wt)
@@ -61,6 +69,8 @@ class NumpyKinetics:
         cp, h, s = self.thermo(T)
         g = h - s
         kf = np.exp(self.arr[:, 0] + self.arr[:, 1] * np.log(T) - self.arr[:, 2] / T)
+        for i in np.nonzero(self.rtype == 3)[0]:
+            kf[i] = self._plog_k(i, P, T)
         M = self.eff @ C
         tbc = self.tbsp >= 0
         M = np.where(tbc, C[np.maximum(self.tbsp, 0)], M)

@@ -37,7 +37,8 @@ _P = ct.c_void_p
 class MechDesc(ct.Structure):
     _fields_ = [("KK", ct.c_int32), ("II", ct.c_int32)] + [
         (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
-                          "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val")
+                          "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val",
+                          "plog_ptr", "plog_par")
     ]
 
 

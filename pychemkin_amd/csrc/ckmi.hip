@@ -201,7 +201,7 @@ enum {
 #define CKMI_RWAVES 8
 #endif
 constexpr int RWAVES = CKMI_RWAVES;
-template <int N>
+template <int N, bool PL = false>  // PL: the mechanism has PLOG reactions
 __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, const DevCfg* __restrict__ dcfg,
                                                                int nreact, int* __restrict__ queue,
                                                                double* __restrict__ jws, ReactorIO io) {
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
 #endif
 #ifdef CKMI_PHASE_TIMERS
     unsigned long long sub[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j, sub);
+    fe = reactor_rhs<PL>(V, R, t_e, y_e, L, oJ, lane, N, with_j, sub);
     ph[with_j ? PH_JAC : PH_RHS] += __builtin_amdgcn_s_memtime() - t0;
     if (!with_j) {
       ph[5] += sub[0];
@@ -928,7 +928,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
       }
     }
 #else
-    fe = reactor_rhs(V, R, t_e, y_e, L, oJ, lane, N, with_j);
+    fe = reactor_rhs<PL>(V, R, t_e, y_e, L, oJ, lane, N, with_j);
 #endif
   }
 #undef REQUEST_F
@@ -962,7 +962,7 @@ __host__ __device__ constexpr int rop_slice_bytes(int G, int KK, int KKp) {
   return align16(8 * (3 * KKp + (G > 0 ? G : 1))) + rop_io_bytes(KK);
 }
 
-template <int MODE, int NCH>  // MODE 0: wdot + cp + h, 1: qf / qr; NCH species per lane
+template <int MODE, int NCH, bool PL = false>  // MODE 0: wdot + cp + h, 1: qf / qr; NCH species per lane; PL: PLOG
 __global__ __launch_bounds__(rop_waves(NCH)* WAVE) void rop_kernel(MechImage img, const int* __restrict__ orig,
                                                                   int nstate, const double* __restrict__ Tv,
                                                                   const double* __restrict__ Pv,
@@ -1047,7 +1047,7 @@ __global__ __launch_bounds__(rop_waves(NCH)* WAVE) void rop_kernel(MechImage img
         const int nr = rx_nr(inf), np = rx_np(inf);
         if (nr + np == 0) continue;
         const uint32_t rs = V.rsp()[i], ps = V.psp()[i];
-        const Rxn e = eval_rxn_img(V, i, inf, rs, ps, 0u, T, lnT, invT, lnPRT, C, gRT, gRT, Mg, false);
+        const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, 0u, T, lnT, invT, lnPRT, P, C, gRT, gRT, Mg, false);
         const double qf = e.mfac * e.kf * e.pf, qr = e.mfac * e.kr * e.pr;
         if (MODE == 1) {
           const int oi = orig[i];
@@ -1116,6 +1116,8 @@ struct ckmi_mech {
   std::vector<void*> allocs;
   // host copies of the forward Arrhenius (original order) for get/set
   std::vector<double> lnA_orig, b_orig, E_orig;
+  std::vector<int> rtype_orig;
+  bool has_plog = false;
   std::vector<int> slot_of;  // original reaction -> device slot
   DevCfg* cfg_dev;
   mutable DevCfg cfg_host;  // host staging of the per-call configuration
@@ -1180,7 +1182,16 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     const int fl = flags[s];
     const int type = fl & 3;
     uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10);
-    if (slots[s] >= 0 && (type == 2 || (fl & 8))) {
+    if (slots[s] >= 0 && type == CKMI_RXN_PLOG) {
+      // PLOG stream: npts, then (ln P, ln A, b, E/R) per point, over ceil((1 + 4 npts) / AUXW) records
+      const int i = slots[s], p0 = d->plog_ptr[i], n = d->plog_ptr[i + 1] - p0;
+      std::vector<double> rec{(double)n};
+      rec.insert(rec.end(), d->plog_par + 4 * p0, d->plog_par + 4 * (p0 + n));
+      rec.resize((rec.size() + AUXW - 1) / AUXW * AUXW, 0.0);
+      aux.insert(aux.end(), rec.begin(), rec.end());
+      inf |= (uint32_t)naux << 16;
+      naux += (int)rec.size() / AUXW;
+    } else if (slots[s] >= 0 && (type == 2 || (fl & 8))) {
       double rec[AUXW] = {lnA0[s], beta0[s], Ea0[s], fp[0 * IIp + s], fp[1 * IIp + s], fp[2 * IIp + s],
                           fp[3 * IIp + s], fp[4 * IIp + s], rlnA[s], rbeta[s], rEa[s], 0.0};
       const int ft = (fl >> 4) & 7;
@@ -1271,17 +1282,17 @@ size_t reactor_lds_bytes(const ckmi_mech* m) {
 }
 // Grid = (CUs x resident workgroups per CU), capped by the batch; J workspace = one
 // column-major N x 64 matrix per wave slot, allocated stream-ordered (~55 MB for GRI-3.0).
-template <int N>
+template <int N, bool PL = false>
 int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t stream) {
   const size_t lds = reactor_lds_bytes<N>(m);
   static thread_local std::map<int, int> max_lds_set;
   if (lds > 64 * 1024 && max_lds_set[m->device] < (int)lds) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)reactor_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIP_CHECK(hipFuncSetAttribute((const void*)reactor_kernel<N, PL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     max_lds_set[m->device] = (int)lds;
   }
   int ncu = 0, per_cu = 0;
   HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reactor_kernel<N>, RWAVES * WAVE, lds));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reactor_kernel<N, PL>, RWAVES * WAVE, lds));
   if (per_cu < 1) return fail(CKMI_ERR_SIZE, "reactor kernel does not fit on a CU (LDS " + std::to_string(lds) + " B)");
   const int want = (n + RWAVES - 1) / RWAVES;
   const int grid = std::max(1, std::min(ncu * per_cu, want));
@@ -1290,14 +1301,14 @@ int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t 
   HIP_CHECK(hipMallocAsync(&ws, jbytes + 256, stream));
   int* queue = (int*)((char*)ws + jbytes);
   HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(int), stream));
-  hipLaunchKernelGGL(reactor_kernel<N>, dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, m->cfg_dev, n, queue,
+  hipLaunchKernelGGL((reactor_kernel<N, PL>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, m->cfg_dev, n, queue,
                      (double*)ws, io);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipFreeAsync(ws, stream));
   return CKMI_OK;
 }
 
-template <int MODE, int NCH>
+template <int MODE, int NCH, bool PL>
 int launch_rop_n(const ckmi_mech* m, int n, const double* T, const double* P, const double* Y, double* o0,
                  double* o1, double* o2, hipStream_t stream) {
   constexpr int NW = rop_waves(NCH);
@@ -1306,13 +1317,13 @@ int launch_rop_n(const ckmi_mech* m, int n, const double* T, const double* P, co
   HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
   HIP_CHECK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, m->device));
   if (lds > (size_t)lds_max) return fail(CKMI_ERR_SIZE, "mechanism image + ROP work space exceed the LDS of a CU");
-  HIP_CHECK(hipFuncSetAttribute((const void*)rop_kernel<MODE, NCH>, hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIP_CHECK(hipFuncSetAttribute((const void*)rop_kernel<MODE, NCH, PL>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rop_kernel<MODE, NCH>, NW * WAVE, lds));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rop_kernel<MODE, NCH, PL>, NW * WAVE, lds));
   if (per_cu < 1) return fail(CKMI_ERR_SIZE, "ROP kernel does not fit on a CU");
   const int tasks = (n + ROP_CHUNK - 1) / ROP_CHUNK;
   const int grid = std::max(1, std::min(ncu * per_cu, (tasks + NW - 1) / NW));
-  hipLaunchKernelGGL((rop_kernel<MODE, NCH>), dim3(grid), dim3(NW * WAVE), lds, stream, m->img, m->d.orig, n, T, P,
+  hipLaunchKernelGGL((rop_kernel<MODE, NCH, PL>), dim3(grid), dim3(NW * WAVE), lds, stream, m->img, m->d.orig, n, T, P,
                      Y, o0, o1, o2);
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;
@@ -1321,11 +1332,16 @@ int launch_rop_n(const ckmi_mech* m, int n, const double* T, const double* P, co
 template <int MODE>
 int launch_rop(const ckmi_mech* m, int n, const double* T, const double* P, const double* Y, double* o0, double* o1,
                double* o2, hipStream_t stream) {
+  const bool pl = m->has_plog;
   switch (m->img.KKp / WAVE) {
-    case 1: return launch_rop_n<MODE, 1>(m, n, T, P, Y, o0, o1, o2, stream);
-    case 2: return launch_rop_n<MODE, 2>(m, n, T, P, Y, o0, o1, o2, stream);
-    case 3: return launch_rop_n<MODE, 3>(m, n, T, P, Y, o0, o1, o2, stream);
-    case 4: return launch_rop_n<MODE, 4>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 1: return pl ? launch_rop_n<MODE, 1, true>(m, n, T, P, Y, o0, o1, o2, stream)
+                      : launch_rop_n<MODE, 1, false>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 2: return pl ? launch_rop_n<MODE, 2, true>(m, n, T, P, Y, o0, o1, o2, stream)
+                      : launch_rop_n<MODE, 2, false>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 3: return pl ? launch_rop_n<MODE, 3, true>(m, n, T, P, Y, o0, o1, o2, stream)
+                      : launch_rop_n<MODE, 3, false>(m, n, T, P, Y, o0, o1, o2, stream);
+    case 4: return pl ? launch_rop_n<MODE, 4, true>(m, n, T, P, Y, o0, o1, o2, stream)
+                      : launch_rop_n<MODE, 4, false>(m, n, T, P, Y, o0, o1, o2, stream);
     default: return fail(CKMI_ERR_UNSUPPORTED, "mechanism image with more than 255 species");
   }
 }
@@ -1361,14 +1377,24 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   m->II = II;
   // ---- order reactions: elementary, then third-body, then falloff
   std::vector<int> ordr;
-  for (int t = 0; t < 3; ++t)
+  for (int t = 0; t < 4; ++t)
     for (int i = 0; i < II; ++i)
       if (d->rtype[i] == t) ordr.push_back(i);
-  for (int i = 0; i < II; ++i)
-    if (d->rtype[i] < 0 || d->rtype[i] > 2) {
+  for (int i = 0; i < II; ++i) {
+    if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_PLOG) {
       delete m;
       return fail(CKMI_ERR_UNSUPPORTED, "unsupported reaction type");
     }
+    if (d->rtype[i] == CKMI_RXN_PLOG) {
+      const int p0 = d->plog_ptr ? d->plog_ptr[i] : 0, n = d->plog_ptr ? d->plog_ptr[i + 1] - p0 : 0;
+      bool ok = d->plog_par && n >= 1 && n <= 64 && !d->has_rev[i];
+      for (int j = 0; ok && j + 1 < n; ++j) ok = d->plog_par[4 * (p0 + j)] < d->plog_par[4 * (p0 + j + 1)];
+      if (!ok) {
+        delete m;
+        return fail(CKMI_ERR_UNSUPPORTED, "PLOG table must hold 1..64 points with ascending pressures and no REV");
+      }
+    }
+  }
   // pad the elementary block to a 64 multiple when it does not add a strip
   int nelem = 0;
   for (int i = 0; i < II; ++i) nelem += d->rtype[i] == 0;
@@ -1454,9 +1480,10 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     dnu[s] = sr - sf;
     ordf[s] = sf;
     ordrr[s] = sr;
-    lnA[s] = d->arr[3 * i];
-    beta[s] = d->arr[3 * i + 1];
-    Ea[s] = d->arr[3 * i + 2];
+    const bool plog = type == CKMI_RXN_PLOG;  // rate from the aux stream; the slot holds ln 1, 0, 0
+    lnA[s] = plog ? 0.0 : d->arr[3 * i];
+    beta[s] = plog ? 0.0 : d->arr[3 * i + 1];
+    Ea[s] = plog ? 0.0 : d->arr[3 * i + 2];
     lnA0[s] = d->low[3 * i];
     beta0[s] = d->low[3 * i + 1];
     Ea0[s] = d->low[3 * i + 2];
@@ -1464,9 +1491,11 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     rlnA[s] = d->revp[3 * i];
     rbeta[s] = d->revp[3 * i + 1];
     rEa[s] = d->revp[3 * i + 2];
-    if (type != 0) tb[s] = d->tbsp[i] >= 0 ? -(d->tbsp[i] + 2) : group_of(i);
+    if (type == 1 || type == 2) tb[s] = d->tbsp[i] >= 0 ? -(d->tbsp[i] + 2) : group_of(i);
   }
   m->G = (int)gmap.size();
+  m->rtype_orig.assign(d->rtype, d->rtype + II);
+  m->has_plog = std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_PLOG) > 0;
   m->lnA_orig.resize(II);
   m->b_orig.resize(II);
   m->E_orig.resize(II);
@@ -1553,6 +1582,8 @@ int ckmi_get_arrhenius(const ckmi_mech* m, double* A, double* b, double* E) {
 
 int ckmi_set_afactor(ckmi_mech* m, int32_t irxn, double A) {
   if (!m || irxn < 0 || irxn >= m->II || !(A > 0.0)) return fail(CKMI_ERR_ARG, "bad reaction index or A");
+  if (m->rtype_orig[irxn] == CKMI_RXN_PLOG)
+    return fail(CKMI_ERR_UNSUPPORTED, "A-factor of a PLOG reaction (its rates come from the PLOG table)");
   const double lnA = std::log(A);
   m->lnA_orig[irxn] = lnA;
   const int s = m->slot_of[irxn];
@@ -1638,7 +1669,9 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
                ext ? ext->t_adap : nullptr, ext ? ext->y_adap : nullptr, ext ? ext->n_adap : nullptr};
   const int nvar = m->KK + 1;
   int rc;
-  if (nvar <= 32) rc = launch_reactors<32>(m, n, io, (hipStream_t)stream);
+  // PLOG mechanisms use one (64-wide) reactor variant, so that the PLOG branch costs compile time once
+  if (m->has_plog) rc = launch_reactors<64, true>(m, n, io, (hipStream_t)stream);
+  else if (nvar <= 32) rc = launch_reactors<32>(m, n, io, (hipStream_t)stream);
   else if (nvar <= 54) rc = launch_reactors<54>(m, n, io, (hipStream_t)stream);
   else rc = launch_reactors<64>(m, n, io, (hipStream_t)stream);
   if (rc) return rc;

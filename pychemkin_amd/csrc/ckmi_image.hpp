@@ -181,22 +181,51 @@ struct Rxn {
 // and Mg are LDS arrays of the calling wave.  Same arithmetic as oracle/ckoracle.c
 // eval_reaction() (standard Chemkin-II gas kinetics: Arrhenius, third body, Lindemann /
 // Troe / SRI falloff, reverse rates from equilibrium or explicit REV parameters).
+// PLOG = false compiles the mechanism-without-PLOG kernels exactly as before PLOG existed (the
+// PLOG branch costs 2-4 % of rate throughput in register allocation even when never taken).
+template <bool PLOG = false>
 __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t inf, uint32_t rs, uint32_t ps,
-                                            uint32_t nuw, double T, double lnT, double invT, double lnPRT,
+                                            uint32_t nuw, double T, double lnT, double invT, double lnPRT, double P,
                                             const double* C, const double* gRT, const double* hRT, const double* Mg,
                                             bool need_h, int pslot = -1, double plnf = 0.0, double gfac = 1.0) {
   constexpr double INV_LN10 = 0.43429448190325176;
   const int type = rx_type(inf);
   // pslot / plnf: per-reactor A-factor perturbation (brute-force sensitivity)
   const double lnA = V.lnA()[i] + (i == pslot ? plnf : 0.0), b = V.beta()[i], Ea = V.Ea()[i];
-  const double lnkinf = lnA + b * lnT - Ea * invT;
+  double lnkinf = lnA + b * lnT - Ea * invT;
+  double dlkf = (b + Ea * invT) * invT;
+  if constexpr (PLOG) {
+    if (type == 3) {
+      // PLOG (lnA, b, Ea of the slot are 0): ln k linear in ln P between the bracketing table
+      // pressures, clamped outside; aux stream = npts, then (ln P, ln A, b, E/R) per point.
+      // Same arithmetic as oracle/ckoracle.c plog_rate().
+      const double* pt = V.aux() + AUXW * rx_aux(inf);
+      const int n = (int)pt[0];
+      const double lnP = log(P);
+      int j = 0;
+      while (j < n - 2 && lnP > pt[1 + 4 * (j + 1)]) ++j;
+      const double* t0 = pt + 1 + 4 * j;
+      const double lk0 = t0[1] + t0[2] * lnT - t0[3] * invT;
+      const double dk0 = (t0[2] + t0[3] * invT) * invT;
+      double lk = lk0, dk = dk0;
+      if (n > 1) {
+        const double* t1 = t0 + 4;
+        const double lk1 = t1[1] + t1[2] * lnT - t1[3] * invT;
+        const double dk1 = (t1[2] + t1[3] * invT) * invT;
+        const double w = fmin(fmax((lnP - t0[0]) / (t1[0] - t0[0]), 0.0), 1.0);
+        lk = lk0 + w * (lk1 - lk0);
+        dk = dk0 + w * (dk1 - dk0);
+      }
+      lnkinf += lk;
+      dlkf = dk;
+    }
+  }
   const double* e2t = V.e2t();
   const double kf_inf = fexp(lnkinf, e2t);
   double kf = kf_inf;
-  const double dlkf = (b + Ea * invT) * invT;
   double mfac = 1.0;
   const double* ax = V.aux() + AUXW * rx_aux(inf);
-  if (type != 0) {
+  if (PLOG ? (type == 1 || type == 2) : type != 0) {
     const int tb = V.tb()[i];
     const double Mc = tb >= 0 ? Mg[tb] : C[-tb - 2];
     if (type == 1) {

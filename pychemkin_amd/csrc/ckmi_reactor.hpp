@@ -119,6 +119,7 @@ __device__ __forceinline__ void jac_scatter(const MechView& V, int oJ, int nr, i
 // caller holds its lock).  Same formulation as oracle/ckoracle.c reactor_rhs().  with_j is a
 // run-time (wave-uniform) flag and the Jacobian terms are a second pass over the reactions,
 // so the integrator has a single RHS call site and the register peak is that of one pass.
+template <bool PL>
 __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R, double t, double yl,
                                               const WaveLds& L, int oJ, int lane, int ncol, bool with_j
 #ifdef CKMI_PHASE_TIMERS
@@ -211,7 +212,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     const int nr = rx_nr(inf), np = rx_np(inf);
     if (nr + np != 0) {
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
-      const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), false,
+      const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), false,
                                  R.pslot, R.plnf, R.gfac);
       const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
 #ifdef CKMI_EXPT_NOATOM  // timing experiment only: plain stores instead of LDS atomics (wrong wdot)
@@ -243,7 +244,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       const int nr = rx_nr(inf), np = rx_np(inf);
       if (nr + np == 0) continue;
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
-      const Rxn e = eval_rxn_img(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, C, L.gRT(), L.hRT(), L.Mg(), true,
+      const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), true,
                                  R.pslot, R.plnf, R.gfac);
       const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
       double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);

@@ -12,7 +12,7 @@ Supported syntax (Chemkin-II gas phase): ELEMENTS (with optional /weight/), SPEC
 optional THERMO block, REACTIONS with unit keywords, ``=``/``<=>``/``=>``, ``+M``,
 ``(+M)``/``(+species)`` falloff, LOW, TROE (3 or 4 parameters), SRI (3 or 5), REV,
 DUPLICATE, third-body efficiencies, FORD/RORD (parsed, rejected by the device path),
-PLOG (parsed, rejected by the device path).
+PLOG (elementary reactions; ln k interpolated in ln P, clamped outside the table).
 """
 from __future__ import annotations
 
@@ -23,7 +23,7 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
-from .constants import R_GAS, R_GAS_CAL, AVOGADRO
+from .constants import R_GAS, R_GAS_CAL, AVOGADRO, P_ATM
 
 # Chemkin default atomic weights [g/mol] (reproduces loadmechanism.baseline "state-AWT")
 ATOMIC_WEIGHTS = {
@@ -44,6 +44,7 @@ RXN_ELEMENTARY = 0
 RXN_THIRDBODY = 1
 RXN_FALLOFF = 2
 RXN_CHEMACT = 3  # chemically activated (HIGH/) - parsed, not on the device path yet
+TAB_PLOG = 3     # rtype of a PLOG reaction in to_tables() (CKMI_RXN_PLOG in include/ckmi.h)
 
 FALL_NONE = 0
 FALL_LINDEMANN = 1
@@ -505,16 +506,26 @@ class Mechanism:
         eff_ptr = [0]
         eff_sp: List[int] = []
         eff_val: List[float] = []
+        plog_ptr = np.zeros(II + 1, np.int32)     # CSR into plog_par (rtype TAB_PLOG)
+        plog_par: List[Tuple[float, float, float, float]] = []  # ln P [dyn/cm2], ln A [cgs], b, E/R
         for i, rx in enumerate(self.reactions):
             if rx.ford or rx.rord:
                 raise MechanismError(f"FORD/RORD not supported on the device path ({rx.equation})")
             if rx.plog:
-                raise MechanismError(f"PLOG not supported on the device path ({rx.equation})")
+                if rx.kind != RXN_ELEMENTARY or rx.rev is not None:
+                    raise MechanismError(f"PLOG on a third-body/falloff reaction or with REV ({rx.equation})")
+                pts = sorted(rx.plog, key=lambda e: e[0])
+                if any(pts[j][0] == pts[j + 1][0] for j in range(len(pts) - 1)) or pts[0][0] <= 0.0:
+                    raise MechanismError(f"PLOG pressures must be positive and distinct ({rx.equation})")
+                for p_atm, a, b, e in pts:
+                    Ap = self._A_cgs(rx, a, rx.reactants, True, 0)
+                    plog_par.append((math.log(p_atm * P_ATM), math.log(Ap), b, e * rx.E_scale))
             if rx.kind == RXN_CHEMACT:
                 raise MechanismError(f"chemically activated (HIGH/) not supported ({rx.equation})")
             if len(rx.reactants) > S or len(rx.products) > S:
                 raise MechanismError(f"more than {S} species on one side of {rx.equation}")
-            rtype[i] = rx.kind
+            rtype[i] = TAB_PLOG if rx.plog else rx.kind
+            plog_ptr[i + 1] = len(plog_par)
             rev[i] = 1 if rx.reversible else 0
             nr[i] = len(rx.reactants)
             np_[i] = len(rx.products)
@@ -575,6 +586,8 @@ class Mechanism:
             arr=arr, low=low, revp=revp, has_rev=has_rev, ftype=ftype, fpar=fpar, tbsp=tbsp,
             eff_ptr=np.asarray(eff_ptr, np.int32), eff_sp=np.asarray(eff_sp, np.int32),
             eff_val=np.asarray(eff_val, np.float64),
+            plog_ptr=plog_ptr,
+            plog_par=np.asarray(plog_par if plog_par else [(0.0, 0.0, 0.0, 0.0)], np.float64).reshape(-1, 4),
         )
 
 

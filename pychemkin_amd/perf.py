@@ -36,6 +36,8 @@ def count_ops(tables: Dict[str, np.ndarray]) -> Dict[str, float]:
         slots = int(nr[i] + np_[i])
         powf = float(np.sum(rnu[i][: nr[i]]) + np.sum(pnu[i][: np_[i]]))
         r = 4 + T                    # forward Arrhenius
+        if rtype[i] == 3:            # PLOG: log P, two Arrhenius exponents, interpolation
+            r += T + 8 + 6
         if rtype[i] == 2:            # falloff
             r += 4 + T + 2           # k0, Pr
             if ftype[i] in (2, 3):
