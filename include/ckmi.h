@@ -44,6 +44,7 @@ extern "C" {
 #define CKMI_RXN_THIRDBODY 1
 #define CKMI_RXN_FALLOFF 2
 #define CKMI_RXN_PLOG 3 /* elementary with a PLOG table: ln k linear in ln P, clamped outside */
+#define CKMI_RXN_CHEMACT 4 /* chemically activated: arr = k0, low = HIGH (k_inf); k = k0 F / (1 + Pr) */
 /* falloff forms */
 #define CKMI_FALL_NONE 0
 #define CKMI_FALL_LINDEMANN 1

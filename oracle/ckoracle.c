@@ -86,7 +86,7 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
     kf = exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
     dlkf = (a[1] + a[2] * invT) * invT;
   }
-  if (type == 1 || type == 2) {
+  if (type == 1 || type == 2 || type == 4) {
     double M;
     if (m->tbsp[i] >= 0) {
       M = C[m->tbsp[i]];
@@ -98,8 +98,9 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
       mfac = M;
     } else {
       const double* l = m->low + 3 * i;
+      /* falloff: main = k_inf, l = LOW; chemically activated (4): main = k0, l = HIGH */
       double k0 = exp(l[0] + l[1] * lnT - l[2] * invT);
-      double Pr = k0 * M / kf;
+      double Pr = type == 4 ? kf * M / k0 : k0 * M / kf;
       double F = 1.0;
       const int ft = m->ftype[i];
       const double* fp = m->fpar + 5 * i;
@@ -116,7 +117,7 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
         double X = 1.0 / (1.0 + lPr * lPr);
         F = fp[3] * pow(fp[0] * exp(-fp[1] * invT) + exp(-T / fp[2]), X) * pow(T, fp[4]);
       }
-      kf = kf * (Pr / (1.0 + Pr)) * F;
+      kf = type == 4 ? kf * (1.0 / (1.0 + Pr)) * F : kf * (Pr / (1.0 + Pr)) * F;
     }
   }
   double kr = 0.0, dlkr = 0.0;
@@ -124,7 +125,7 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
     if (m->has_rev[i]) {
       const double* r = m->revp + 3 * i;
       kr = exp(r[0] + r[1] * lnT - r[2] * invT);
-      if (type == 2) kr *= kf / exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
+      if (type == 2 || type == 4) kr *= kf / exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
       dlkr = (r[1] + r[2] * invT) * invT;
     } else {
       double dG = 0.0, dH = 0.0, dnu = 0.0;

@@ -24,7 +24,7 @@ typedef struct {
   int KK, II;
   const double* wt;      /* [KK] g/mol */
   const double* thermo;  /* [KK][17]: tlow, tmid, thigh, low a1..a7, high a1..a7 */
-  const int* rtype;      /* 0 elementary, 1 third body, 2 falloff, 3 PLOG */
+  const int* rtype;      /* 0 elementary, 1 third body, 2 falloff, 3 PLOG, 4 chemically activated */
   const int* rev;        /* reversible flag */
   const int* nr; const int* np;
   const int* rsp; const int* psp;      /* [II][4] */

@@ -75,10 +75,11 @@ class NumpyKinetics:
         tbc = self.tbsp >= 0
         M = np.where(tbc, C[np.maximum(self.tbsp, 0)], M)
         mfac = np.where(self.rtype == 1, M, 1.0)
-        fo = self.rtype == 2
+        ca = self.rtype == 4  # chemically activated: arr = k0, low = HIGH (k_inf)
+        fo = (self.rtype == 2) | ca
         k0 = np.exp(self.low[:, 0] + self.low[:, 1] * np.log(T) - self.low[:, 2] / T)
         with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
-            Pr = np.where(fo, k0 * M / kf, 0.0)
+            Pr = np.where(ca, kf * M / k0, np.where(fo, k0 * M / kf, 0.0))
             a, T3, T1, T2 = self.fpar[:, 0], self.fpar[:, 1], self.fpar[:, 2], self.fpar[:, 3]
             Fc = (1 - a) * np.exp(-T / np.where(T3 != 0, T3, 1.0)) + a * np.exp(-T / np.where(T1 != 0, T1, 1.0))
             Fc = Fc + np.where(self.ftype == 3, np.exp(-T2 / T), 0.0)
@@ -92,7 +93,7 @@ class NumpyKinetics:
             Fsri = self.fpar[:, 3] * (self.fpar[:, 0] * np.exp(-self.fpar[:, 1] / T) + np.exp(-T / np.where(self.fpar[:, 2] != 0, self.fpar[:, 2], 1.0))) ** X * T ** self.fpar[:, 4]
         F = np.where((self.ftype == 2) | (self.ftype == 3), Ftroe, np.where(self.ftype == 4, Fsri, 1.0))
         kinf = kf.copy()
-        kf = np.where(fo, kf * Pr / (1 + Pr) * F, kf)
+        kf = np.where(ca, kf / (1 + Pr) * F, np.where(fo, kf * Pr / (1 + Pr) * F, kf))
         dG = self.dnu_mat @ g
         dn = self.dnu_mat.sum(axis=1)
         Kc = np.exp(-dG) * (PATM / (RU * T)) ** dn

@@ -1181,7 +1181,7 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     unu[s] = nu;
     const int fl = flags[s];
     const int type = fl & 3;
-    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10);
+    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10) | (uint32_t)(fl & 0x2000);
     if (slots[s] >= 0 && type == CKMI_RXN_PLOG) {
       // PLOG stream: npts, then (ln P, ln A, b, E/R) per point, over ceil((1 + 4 npts) / AUXW) records
       const int i = slots[s], p0 = d->plog_ptr[i], n = d->plog_ptr[i + 1] - p0;
@@ -1377,11 +1377,12 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   m->II = II;
   // ---- order reactions: elementary, then third-body, then falloff
   std::vector<int> ordr;
-  for (int t = 0; t < 4; ++t)
+  // strips stay type-uniform: chemically activated reactions run in the falloff strips
+  for (int t : {CKMI_RXN_ELEMENTARY, CKMI_RXN_THIRDBODY, CKMI_RXN_FALLOFF, CKMI_RXN_CHEMACT, CKMI_RXN_PLOG})
     for (int i = 0; i < II; ++i)
       if (d->rtype[i] == t) ordr.push_back(i);
   for (int i = 0; i < II; ++i) {
-    if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_PLOG) {
+    if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_CHEMACT) {
       delete m;
       return fail(CKMI_ERR_UNSUPPORTED, "unsupported reaction type");
     }
@@ -1445,8 +1446,9 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     orig[s] = i;
     if (i < 0) continue;
     m->slot_of[i] = s;
-    const int type = d->rtype[i];
-    flags[s] = type | (d->rev[i] ? 4 : 0) | (d->has_rev[i] ? 8 : 0) | ((d->ftype[i] & 7) << 4);
+    const bool chemact = d->rtype[i] == CKMI_RXN_CHEMACT;  // device type 2 + info bit 13
+    const int type = chemact ? CKMI_RXN_FALLOFF : d->rtype[i];
+    flags[s] = type | (d->rev[i] ? 4 : 0) | (d->has_rev[i] ? 8 : 0) | ((d->ftype[i] & 7) << 4) | (chemact ? 0x2000 : 0);
     const int nr = d->nr[i], np = d->np[i];
     for (int u = 0; u < nr; ++u)
       if (d->rnu[i * SLOTS + u] != std::floor(d->rnu[i * SLOTS + u]) || d->rnu[i * SLOTS + u] < 1.0) {
@@ -1495,7 +1497,9 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   }
   m->G = (int)gmap.size();
   m->rtype_orig.assign(d->rtype, d->rtype + II);
-  m->has_plog = std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_PLOG) > 0;
+  // PLOG and chemically activated reactions are evaluated by the extended kernel variant
+  m->has_plog = std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_PLOG) > 0 ||
+                std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_CHEMACT) > 0;
   m->lnA_orig.resize(II);
   m->b_orig.resize(II);
   m->E_orig.resize(II);

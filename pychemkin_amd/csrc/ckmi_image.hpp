@@ -232,7 +232,11 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
       mfac = Mc;
     } else {
       // Pr = k0 [M] / k_inf from the Arrhenius exponents (one exp, no division)
-      const double lnPr = ax[0] + ax[1] * lnT - ax[2] * invT - lnkinf + log(Mc > 1e-300 ? Mc : 1e-300);
+      // chemically activated (extended variant, info bit 13): the slot's Arrhenius is k0 and the
+      // aux record holds HIGH (k_inf), so Pr = k0 [M] / k_inf and k = k0 F / (1 + Pr)
+      const bool ca = PLOG && (inf & 0x2000u);
+      const double lnlim = ax[0] + ax[1] * lnT - ax[2] * invT;
+      const double lnPr = (ca ? lnkinf - lnlim : lnlim - lnkinf) + log(Mc > 1e-300 ? Mc : 1e-300);
       const double Pr = fexp(lnPr, e2t);
       const double lPr = fmax(lnPr * INV_LN10, -300.0);  // log10(max(Pr, 1e-300))
       double F = 1.0;
@@ -250,7 +254,7 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
         const double X = 1.0 / (1.0 + lPr * lPr);
         F = ax[6] * pow(ax[3] * exp(-ax[4] * invT) + exp(-T * ax[5]), X) * pow(T, ax[7]);
       }
-      kf = kf_inf * (Pr / (1.0 + Pr)) * F;
+      kf = ca ? kf_inf * (1.0 / (1.0 + Pr)) * F : kf_inf * (Pr / (1.0 + Pr)) * F;
     }
   }
   double kr = 0.0, dlkr = 0.0;

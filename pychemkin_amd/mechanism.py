@@ -43,8 +43,9 @@ ATOMIC_WEIGHTS = {
 RXN_ELEMENTARY = 0
 RXN_THIRDBODY = 1
 RXN_FALLOFF = 2
-RXN_CHEMACT = 3  # chemically activated (HIGH/) - parsed, not on the device path yet
+RXN_CHEMACT = 3  # chemically activated (HIGH/): main line = k0, HIGH = k_inf
 TAB_PLOG = 3     # rtype of a PLOG reaction in to_tables() (CKMI_RXN_PLOG in include/ckmi.h)
+TAB_CHEMACT = 4  # rtype of a chemically activated reaction (CKMI_RXN_CHEMACT)
 
 FALL_NONE = 0
 FALL_LINDEMANN = 1
@@ -460,7 +461,7 @@ class Mechanism:
         rx = self.reactions[i]
         if i in self._A_override:
             return self._A_override[i]
-        return self._A_cgs(rx, rx.A, rx.reactants, True, 1 if rx.kind == RXN_THIRDBODY else 0)
+        return self._A_cgs(rx, rx.A, rx.reactants, True, 1 if rx.kind in (RXN_THIRDBODY, RXN_CHEMACT) else 0)
 
     def arrhenius(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """A [cgs], b, E/R [K] as KINGetReactionRateParameters returns them."""
@@ -520,11 +521,9 @@ class Mechanism:
                 for p_atm, a, b, e in pts:
                     Ap = self._A_cgs(rx, a, rx.reactants, True, 0)
                     plog_par.append((math.log(p_atm * P_ATM), math.log(Ap), b, e * rx.E_scale))
-            if rx.kind == RXN_CHEMACT:
-                raise MechanismError(f"chemically activated (HIGH/) not supported ({rx.equation})")
             if len(rx.reactants) > S or len(rx.products) > S:
                 raise MechanismError(f"more than {S} species on one side of {rx.equation}")
-            rtype[i] = TAB_PLOG if rx.plog else rx.kind
+            rtype[i] = TAB_PLOG if rx.plog else (TAB_CHEMACT if rx.kind == RXN_CHEMACT else rx.kind)
             plog_ptr[i + 1] = len(plog_par)
             rev[i] = 1 if rx.reversible else 0
             nr[i] = len(rx.reactants)
@@ -538,11 +537,16 @@ class Mechanism:
             extra = 1 if rx.kind == RXN_THIRDBODY else 0
             A = self.A_cgs(i)
             arr[i] = (math.log(A) if A > 0 else -1e300, rx.b, rx.E * rx.E_scale)
-            if rx.kind == RXN_FALLOFF:
-                if rx.low is None:
+            if rx.kind in (RXN_FALLOFF, RXN_CHEMACT):
+                if rx.kind == RXN_FALLOFF and rx.low is None:
                     raise MechanismError(f"falloff reaction without LOW: {rx.equation}")
-                A0 = self._A_cgs(rx, rx.low[0], rx.reactants, True, 1)
-                low[i] = (math.log(A0), rx.low[1], rx.low[2] * rx.E_scale)
+                if rx.kind == RXN_CHEMACT and (rx.high is None or rx.low is not None):
+                    raise MechanismError(f"chemically activated reaction needs HIGH and no LOW: {rx.equation}")
+                # falloff: low[] = LOW (k0, main line = k_inf); chemically activated: low[] = HIGH
+                # (k_inf, main line = k0), Chemkin's k = k0 F / (1 + Pr) with Pr = k0 [M] / k_inf
+                lim = rx.low if rx.kind == RXN_FALLOFF else rx.high
+                A0 = self._A_cgs(rx, lim[0], rx.reactants, True, 1 if rx.kind == RXN_FALLOFF else 0)
+                low[i] = (math.log(A0), lim[1], lim[2] * rx.E_scale)
                 if rx.troe is not None:
                     t = list(rx.troe)
                     if len(t) == 3:
@@ -567,7 +571,7 @@ class Mechanism:
                 has_rev[i] = 1
                 Ar = self._A_cgs(rx, rx.rev[0], rx.products, False, extra)
                 revp[i] = (math.log(Ar) if Ar > 0 else -1e300, rx.rev[1], rx.rev[2] * rx.E_scale)
-            if rx.kind in (RXN_THIRDBODY, RXN_FALLOFF) and tbsp[i] < 0:
+            if rx.kind in (RXN_THIRDBODY, RXN_FALLOFF, RXN_CHEMACT) and tbsp[i] < 0:
                 for sp, val in rx.efficiencies.items():
                     eff_sp.append(idx[sp])
                     eff_val.append(val)

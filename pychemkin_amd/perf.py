@@ -38,7 +38,7 @@ def count_ops(tables: Dict[str, np.ndarray]) -> Dict[str, float]:
         r = 4 + T                    # forward Arrhenius
         if rtype[i] == 3:            # PLOG: log P, two Arrhenius exponents, interpolation
             r += T + 8 + 6
-        if rtype[i] == 2:            # falloff
+        if rtype[i] in (2, 4):       # falloff / chemically activated
             r += 4 + T + 2           # k0, Pr
             if ftype[i] in (2, 3):
                 r += 6 + 2 * T + (T + 1 if ftype[i] == 3 else 0)  # Fcent

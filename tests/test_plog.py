@@ -1,8 +1,9 @@
-"""PLOG (pressure-dependent Arrhenius tables) on the oracle and the device path.
+"""PLOG (pressure-dependent Arrhenius tables) and chemically activated (HIGH/) reactions on the
+oracle and the device path.
 
 Mechanism: data/gri30_plog_chem.inp (data/make_plog_mechanism.py), GRI-3.0 with PLOG tables of
-1 to 5 points on seven elementary reactions.  No PLOG mechanism or golden exists in the
-reference, so parity with Chemkin is unpinned here: the C oracle is checked against the numpy
+1 to 5 points on seven elementary reactions and three falloff reactions rewritten as chemically
+activated ones (one Lindemann, two Troe).  No such mechanism or golden exists in the reference, so parity with Chemkin is unpinned here: the C oracle is checked against the numpy
 restatement and against the PLOG definition directly (ln k linear in ln P, end values outside
 the table), and the GPU kernels against the oracle with the GRI-3.0 bars of
 test_gpu_kernels.py / test_gpu_reactor.py.
@@ -50,6 +51,27 @@ def test_plog_tables(pmech):
     for i in plog:
         lnp = t["plog_par"][t["plog_ptr"][i]:t["plog_ptr"][i + 1], 0]
         assert np.all(np.diff(lnp) > 0)
+
+
+def test_chemact_tables_and_rate_definition(pmech, porc):
+    """O+CO(+M)<=>CO2(+M) as chemically activated Lindemann: kf = k0 / (1 + k0 [M] / k_inf)."""
+    t = pmech.to_tables()
+    assert int(np.sum(t["rtype"] == 4)) == 3
+    i = next(j for j, rx in enumerate(pmech.reactions) if rx.equation == "O+CO(+M)<=>CO2(+M)")
+    rx = pmech.reactions[i]
+    assert t["rtype"][i] == 4 and t["ftype"][i] == 1
+    T = 1300.0
+    Y = np.random.default_rng(2).dirichlet(np.ones(pmech.KK))
+    for p in (0.1, 1.0, 30.0):
+        P = p * P_ATM
+        qf, _, _ = porc.rates(T, P, Y)
+        C = P / (R_GAS * T) * Y / pmech.wt / np.sum(Y / pmech.wt)
+        M = C.sum() + sum((e - 1.0) * C[pmech.species.index(sp)] for sp, e in rx.efficiencies.items())
+        k0 = rx.A * T ** rx.b * math.exp(-rx.E * rx.E_scale / T)
+        kinf = rx.high[0] * T ** rx.high[1] * math.exp(-rx.high[2] * rx.E_scale / T)
+        expect = k0 / (1.0 + k0 * M / kinf)
+        kO, kCO = pmech.species.index("O"), pmech.species.index("CO")
+        assert abs(qf[i] / (C[kO] * C[kCO]) / expect - 1) < 1e-9
 
 
 def test_plog_rate_definition(pmech, porc):
