@@ -6,6 +6,7 @@ format, {"reactor": {...}, "rop": {...}}, averaged over the dispatches of each k
 """
 import collections
 import csv
+import re
 import glob
 import json
 import os
@@ -21,8 +22,8 @@ def main():
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
             kind = ("reactor" if "reactor_kernel" in k else
-                    "rop" if "rop_kernel<0, 1>" in k else           # GRI-3.0 (KK <= 63)
-                    "rop_161sp" if "rop_kernel<0, 3>" in k else     # synthetic 161-species mechanism
+                    "rop" if re.search(r"rop_kernel<0, 1[,>]", k) else        # GRI-3.0 (KK <= 63)
+                    "rop_161sp" if re.search(r"rop_kernel<0, 3[,>]", k) else  # synthetic 161-species mechanism
                     "lu" if "lu_factor_kernel" in k else None)
             if kind is None:
                 continue
