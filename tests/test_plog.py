@@ -175,3 +175,27 @@ def test_plog_afactor_set_rejected(pmech, pdm):
     i = int(np.nonzero(pmech.to_tables()["rtype"] == 3)[0][0])
     with pytest.raises(_native.NativeError):
         pdm.set_afactor(i, 1.0e10)
+
+
+@pytest.mark.gpu
+def test_drop_in_api_on_plog_mechanism(pmech, porc):
+    """Chemistry.preprocess / Mixture.ROP / RxnRates (mixture.py:1693-1808) on the PLOG + HIGH
+    mechanism, through the extended GPU kernel variant, at pressures inside and outside the tables."""
+    import pychemkin_amd as ck
+
+    chem = ck.Chemistry(label="gri30-plog")
+    chem.chemfile = PLOG_CHEM
+    chem.thermfile = THERM
+    chem.preprocess()
+    assert chem.KK == 53 and chem.IIGas == 325
+    for p in (0.005, 0.7, 40.0, 500.0):
+        m = ck.Mixture(chem)
+        m.temperature = 1650.0
+        m.pressure = p * P_ATM
+        m.X = [("CH4", 0.05), ("O2", 0.15), ("N2", 0.7), ("OH", 0.01), ("H", 0.01), ("O", 0.01), ("CO", 0.05),
+               ("HO2", 0.01), ("CH2O", 0.01)]
+        qfo, qro, wo = porc.rates(1650.0, p * P_ATM, m.Y)
+        assert np.max(np.abs(m.ROP() - wo)) < 1e-11 * np.max(np.abs(wo))
+        qf, qr = m.RxnRates()
+        assert np.max(np.abs(qf - qfo)) < 1e-11 * np.max(np.abs(qfo))
+        assert np.max(np.abs(qr - qro)) < 1e-11 * np.max(np.abs(qro))
