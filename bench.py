@@ -1,19 +1,27 @@
 #!/usr/bin/env python3
 """Benchmark: GRI-Mech 3.0 constant-pressure ignition sweep on MI355X (BASELINE.json metric).
 
-One "step" = one ckmi_reactor_run over this rank's shard of the ignition-delay sweep
-(configs[2]: 64 T0 x 32 phi x 32 P = 65,536 CONP adiabatic CH4/air reactors per GPU,
-t_end = 1 s, TIFP ignition, ATOL/RTOL = 1e-10/1e-8).  For N GPUs the sweep has 64*N
-temperatures and rank r takes every N-th one (weak scaling, no collectives on the data path).
-Inputs are resident in HBM before the timed region.  value = reactors integrated by all
-ranks / max-over-ranks wall time.
+Headline (`value`): configs[2] -- one "step" = one ckmi_reactor_run over this rank's shard of the
+ignition-delay sweep, 64 T0 x 32 phi x 32 P = 65,536 CONP adiabatic CH4/air reactors per GPU,
+t_end = 1 s, TIFP ignition, ATOL/RTOL = 1e-10/1e-8.  For N GPUs the sweep has 64*N temperatures
+and rank r takes every N-th one (weak scaling, no collectives on the data path).  Inputs are
+resident in HBM before the timed region; value = reactors integrated by all ranks / max-over-ranks
+wall time.  PCIe transfers are excluded from `value`; the PCIe-inclusive rate of the same launch is
+reported beside it (`pcie_inclusive`).
 
-Also reported: the ROP+thermo evaluation rate (configs[1], random (T, P, Y) states), a
-roofline object for the reactor kernel (algorithmic FLOPs from solver statistics, see
-pychemkin_amd/perf.py) and the CPU baseline (oracle/ C restatement, OpenMP, timed on a
-strided sample of the same sweep on this host).
+Secondary lines in the same JSON object (each sharded over the ranks, max-over-ranks timing):
+  c4   configs[3]: 2^20 GRI-3.0 reactors, CONP/CONV alternating, strong scaling (total fixed)
+  c5   configs[4]: 262,144 reactors of the 161-species stand-in mechanism (no ~160-species
+       n-heptane mechanism exists offline; parity with Chemkin unpinned), workgroup-per-reactor
+       kernel, strong scaling
+  rop  configs[1]: ROP + thermo of 10M random (T, P, Y) states
+  lu / rop_161sp: configs[4] components (batched MFMA LU, 161-species ROP)
+Each carries a roofline object (algorithmic FLOPs from the solver statistics, pychemkin_amd/perf.py,
+over the kernel time measured with HIP events on the launch stream) and, on rank 0 at N = 1, a
+CPU baseline: the oracle C restatement (OpenMP) timed on a bounded sample of the same workload on
+this host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu]
 """
 from __future__ import annotations
 
@@ -36,11 +44,12 @@ from pychemkin_amd.mechanism import Mechanism  # noqa: E402
 from pychemkin_amd.perf import count_ops, reactor_flops  # noqa: E402
 
 P_ATM = 1.01325e6
-FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak, MI355X_MICROARCH.md / SURVEY 8d
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector (= FP64 matrix) peak, SURVEY 8d
 HBM_PEAK_GBS = 8000.0     # MI355X HBM3E peak
 # HBM traffic per launch from rocprofv3 PMC passes of this same bench workload (FETCH_SIZE x2 per the
 # gfx950 calibration + WRITE_SIZE; scripts/pmc_traffic.sh -> scripts/traffic_summary.py)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+RUN = dict(energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
 
 
 def load_traffic(kernel: str, units: int):
@@ -55,23 +64,56 @@ def load_traffic(kernel: str, units: int):
     return float(t["bytes_per_launch"])
 
 
+def cpu_threads():
+    """Threads for the CPU baseline: the OpenMP allotment of this job (the GPU box sets
+    OMP_NUM_THREADS to its CPU share), else every CPU of the host; nproc is reported beside it."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() and int(env) > 0 else (os.cpu_count() or 1)
+
+
+def host_info():
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
 def mechanism():
     return Mechanism.from_files(os.path.join(ROOT, "data", "grimech30_chem.inp"),
                                 os.path.join(ROOT, "data", "grimech30_thermo.dat"))
 
 
-def ch4_air_Y(mech, phi):
-    """CH4/air at equivalence ratio phi (X_by_Equivalence_Ratio, mixture.py:2383-2539), mass fractions."""
+def big_mechanism():
+    return Mechanism.from_files(os.path.join(ROOT, "data", "gri30_tracer161_chem.inp"),
+                                os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat"))
+
+
+def ch4_air_Y(mech, phi, tracer=0.0):
+    """CH4/air at equivalence ratio phi (X_by_Equivalence_Ratio, mixture.py:2383-2539), mass
+    fractions; tracer > 0 replaces that fraction of the N2 by AX1 (161-species stand-in)."""
     KK = mech.KK
     iCH4, iO2, iN2 = mech.species.index("CH4"), mech.species.index("O2"), mech.species.index("N2")
-    alpha = 2.0 / 0.21
     X = np.zeros((len(phi), KK))
     X[:, iCH4] = phi
-    X[:, iO2] = 0.21 * alpha
-    X[:, iN2] = 0.79 * alpha
+    X[:, iO2] = 2.0
+    X[:, iN2] = 2.0 * 0.79 / 0.21 * (1.0 - tracer)
+    if tracer > 0.0:
+        X[:, mech.species.index("AX1")] = 2.0 * 0.79 / 0.21 * tracer
     X /= X.sum(axis=1, keepdims=True)
     Y = X * mech.wt
     return Y / Y.sum(axis=1, keepdims=True)
+
+
+def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
+    """Rank's shard of the (64*world) x 32 x 32 ignition sweep (configs[2] at world = 1)."""
+    T_all = 1100.0 + 600.0 * np.arange(nT * world) / (nT * world - 1)
+    T_sel = T_all[rank::world]
+    phi = 0.5 + 1.5 * np.arange(nphi) / (nphi - 1)
+    P = P_ATM * 10.0 ** (2.0 * np.arange(nP) / (nP - 1))
+    TT, FF, PP = np.meshgrid(T_sel, phi, P, indexing="ij")
+    TT, FF, PP = TT.ravel(), FF.ravel(), PP.ravel()
+    return TT, PP, ch4_air_Y(mech, FF), np.ones(TT.size, np.int32)
 
 
 def sweep_c4(mech, world, rank):
@@ -87,44 +129,175 @@ def sweep_c4(mech, world, rank):
     return TT[sel], PP[sel], ch4_air_Y(mech, FF[sel]), prob[sel]
 
 
-def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
-    """Rank's shard of the (64*world) x 32 x 32 ignition sweep (configs[2] at world = 1)."""
-    T_all = 1100.0 + 600.0 * np.arange(nT * world) / (nT * world - 1)
-    T_sel = T_all[rank::world]
-    phi = 0.5 + 1.5 * np.arange(nphi) / (nphi - 1)
-    P = P_ATM * 10.0 ** (2.0 * np.arange(nP) / (nP - 1))
-    TT, FF, PP = np.meshgrid(T_sel, phi, P, indexing="ij")
+def sweep_c5(mech, world, rank):
+    """configs[4] on the 161-species stand-in: 64 T0 x 64 phi x 64 P = 262,144 CONP reactors in total
+    (strong scaling), T0 1100-1700 K (the stand-in's chemistry is CH4's: the n-heptane grid's
+    700-1300 K would not ignite), phi 0.5-2, P 10-60 atm, 20 % of the N2 replaced by the tracer AX1
+    so the tracer exchange chemistry is live.  Strided over ranks."""
+    T = 1100.0 + 600.0 * np.arange(64) / 63
+    phi = 0.5 + 1.5 * np.arange(64) / 63
+    P = P_ATM * (10.0 + 50.0 * np.arange(64) / 63)
+    TT, FF, PP = np.meshgrid(T, phi, P, indexing="ij")
     TT, FF, PP = TT.ravel(), FF.ravel(), PP.ravel()
-    return TT, PP, ch4_air_Y(mech, FF)
+    sel = slice(rank, None, world)
+    return TT[sel], PP[sel], ch4_air_Y(mech, FF[sel], tracer=0.2), np.ones(TT[sel].size, np.int32)
 
 
-def rop_bench(dev, mech, ns, reps=3):
-    """ROP + thermo over ns random (T, P, Y) states of `mech` (ckmi_rop_thermo), HIP-event timed."""
-    tables = mech.to_tables()
-    ops = count_ops(tables)
-    dm = _native.DeviceMechanism(tables, device=dev)
+class Shard:
+    """One rank's reactors of a sweep, resident in HBM, with preallocated outputs."""
+
+    def __init__(self, dm, dev, T0, P0, Y0, prob):
+        self.dm, self.dev, self.n = dm, dev, len(T0)
+        self.host = (T0, P0, Y0, prob)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.T0 = torch.as_tensor(T0, device=dev)
+        self.P0 = torch.as_tensor(P0, device=dev)
+        self.V0 = torch.ones(self.n, **f64)
+        self.Y0 = torch.as_tensor(Y0, device=dev).contiguous()
+        self.prob = torch.as_tensor(prob, device=dev)
+        self.out = dict(tau=torch.empty(self.n, **f64), T=torch.empty(self.n, **f64), P=torch.empty(self.n, **f64),
+                        V=torch.empty(self.n, **f64), Y=torch.empty((self.n, dm.KK), **f64),
+                        stats=torch.empty((self.n, _native.NSTAT), dtype=torch.int32, device=dev),
+                        t_stop=torch.empty(self.n, **f64))
+
+    def step(self, cfg, lo=0, hi=None):
+        if hi is None:
+            return self.dm.reactor_run(cfg, self.prob, self.T0, self.P0, self.V0, self.Y0, out=self.out)
+        return self.dm.reactor_run(cfg, self.prob[lo:hi], self.T0[lo:hi], self.P0[lo:hi], self.V0[lo:hi],
+                                   self.Y0[lo:hi])
+
+
+def timed(world, fn, steps):
+    """Run fn() `steps` times between barrier + synchronize fences; returns (max-over-ranks wall
+    seconds, per-launch HIP-event milliseconds on the launch stream, last result)."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    res = None
+    for k in range(steps):
+        ev[k][0].record()
+        res = fn()
+        ev[k][1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=torch.cuda.current_device())
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    return tmax.item(), kern_ms, res
+
+
+def solver_summary(stats):
+    return {"mean_steps": float(stats[:, 0].mean()), "mean_rhs": float(stats[:, 1].mean()),
+            "mean_jac": float(stats[:, 2].mean()), "mean_lu": float(stats[:, 3].mean()),
+            "mean_newton": float(stats[:, 7].mean())}
+
+
+def reactor_roofline(ops, stats, kern_s, kernel, traffic_key, n):
+    flops = reactor_flops(ops, stats)
+    tf = flops / kern_s / 1e12
+    return {"bound": "valu", "pipe": "fp64-valu", "kernel": kernel, "achieved": tf, "peak": FP64_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS, "traffic": load_traffic(traffic_key, n),
+            "flops_per_launch": flops, "flops_per_reactor": flops / n, "kernel_ms": kern_s * 1e3}
+
+
+def cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau_gpu, seconds, max_sample, single=True):
+    """Oracle C restatement (OpenMP over reactors) on a random subset of a strided sample of the same
+    sweep, in chunks until ~seconds of CPU work; plus the same oracle on one core."""
+    from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
+
+    orc = Oracle(mech)
+    n = len(T0)
+    stride = max(1, n // max_sample)
+    order = np.random.default_rng(0).permutation(np.arange(0, n, stride)[:max_sample])
+    threads = cpu_threads()
+    chunk = 32 * threads
+    done, tcpu, dmax = 0, 0.0, 0.0
+    while done < order.size and tcpu < seconds:
+        idx = order[done: done + chunk]
+        tc = time.perf_counter()
+        _, cres, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=prob[idx], V0=np.ones(len(idx)),
+                                       nthreads=threads, **RUN)
+        tcpu += time.perf_counter() - tc
+        ctau = np.array([r.tau for r in cres])
+        dmax = max(dmax, float(np.max(np.abs(tau_gpu[idx] / ctau - 1))))
+        done += len(idx)
+    out = {"value": done / tcpu, "unit": "reactors/s", "cores": threads, "kind": "port", "host": host_info(),
+           "sample": f"{done} reactors (random subset of every {stride}th reactor of this GPU's sweep), "
+                     f"oracle C restatement, OpenMP over reactors",
+           "tau_max_rel_diff_vs_gpu": dmax, "seconds": tcpu}
+    if single:
+        idx1 = order[: max(4, min(32, order.size))]
+        tc = time.perf_counter()
+        orc.reactor_batch(T0[idx1], P0[idx1], Y0[idx1], problem=prob[idx1], V0=np.ones(len(idx1)), nthreads=1, **RUN)
+        out["single_core_value"] = len(idx1) / (time.perf_counter() - tc)
+        out["single_core_sample"] = f"{len(idx1)} reactors of the same sample, 1 thread"
+    return out
+
+
+def rop_line(dev, mech, ops, ns, rank, world, cpu_sample, kernel_name="rop_kernel<0,1>", traffic_key="rop",
+             label=None):
+    """ROP + thermo over ns random (T, P, Y) states (ckmi_rop_thermo), HIP-event timed."""
+    dm = _native.DeviceMechanism(mech.to_tables(), device=dev)
     rng = np.random.default_rng(0)
     Ts = torch.as_tensor(rng.uniform(300.0, 3000.0, ns), device=dev)
     Ps = torch.as_tensor(P_ATM * 10.0 ** rng.uniform(-1.0, 2.0, ns), device=dev)
     Ys = torch.as_tensor(rng.dirichlet(0.5 * np.ones(mech.KK), ns).T.copy(), device=dev)
-    dm.rop_thermo(Ts, Ps, Ys)
+    wdot = torch.empty((mech.KK, ns), dtype=torch.float64, device=dev)
+    cp = torch.empty(ns, dtype=torch.float64, device=dev)
+    hh = torch.empty(ns, dtype=torch.float64, device=dev)
+    dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
     torch.cuda.synchronize()
+    reps = 3
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        dm.rop_thermo(Ts, Ps, Ys)
+        dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
     e1.record()
     torch.cuda.synchronize()
     sec = e0.elapsed_time(e1) / 1e3 / reps
     tf = ops["F_rop"] * ns / sec / 1e12
-    return {"mechanism": f"synthetic GRI-3.0 + tracers, KK = {mech.KK}, II = {mech.II}", "states": ns,
-            "value": ns / sec, "unit": "states/s", "ms_per_launch": sec * 1e3,
-            "roofline": {"bound": "mfma", "pipe": "fp64-valu", "achieved": tf, "peak": FP64_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
-                         "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "traffic": load_traffic("rop_161sp", ns)}}
+    gbs = ops["bytes_rop"] * ns / sec / 1e9
+    out = {"value": ns / sec, "unit": "states/s", "states": ns, "ms_per_launch": sec * 1e3,
+           "roofline": {"bound": "valu", "pipe": "fp64-valu", "kernel": kernel_name, "achieved": tf,
+                        "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
+                        "hbm_GBs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(traffic_key, ns)},
+           "cpu_baseline": None}
+    if label:
+        out["mechanism"] = label
+    if rank == 0 and world == 1 and cpu_sample > 0:
+        from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
+
+        orc_r = Oracle(mech)
+        threads = cpu_threads()
+        m = min(ns, 200_000)
+        Th, Ph, Yh = Ts[:m].cpu().numpy(), Ps[:m].cpu().numpy(), Ys[:, :m].cpu().numpy()
+        tc = time.perf_counter()
+        wc, _, _ = orc_r.rop_batch(Th, Ph, Yh, nthreads=threads)
+        t_all = time.perf_counter() - tc
+        m1 = min(m, 20_000)
+        tc = time.perf_counter()
+        orc_r.rop_batch(Th[:m1], Ph[:m1], np.ascontiguousarray(Yh[:, :m1]), nthreads=1)
+        t_one = time.perf_counter() - tc
+        wg = wdot[:, :m].cpu().numpy()
+        out["cpu_baseline"] = {
+            "value": m / t_all, "unit": "states/s", "cores": threads, "kind": "port", "host": host_info(),
+            "single_core_value": m1 / t_one,
+            "sample": f"first {m} of the same {ns} states ({m1} on one core), oracle C restatement, OpenMP over states",
+            "wdot_max_rel_diff_vs_gpu": float(np.max(np.abs(wg - wc) / np.max(np.abs(wc), axis=0, keepdims=True))),
+        }
+    del Ts, Ps, Ys, wdot, cp, hh
+    dm.close()
+    return out
 
 
-def lu_bench(dev, nsys, n):
+def lu_line(dev, nsys, n):
     """Batched LU (ckmi_lu_factor_batched) on nsys Newton-like matrices I - gamma J of size n, timed with HIP
     events on the stream it is launched on; algorithmic work (2/3) n^3 per matrix."""
     g = torch.Generator(device=dev).manual_seed(0)
@@ -154,7 +327,33 @@ def lu_bench(dev, nsys, n):
                          "hbm_GBs": nbytes / sec / 1e9, "traffic": load_traffic("lu", nsys)}}
 
 
-RUN = dict(energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
+def secondary_sweep(name, dm, dev, mech, ops, sweep_fn, world, rank, args, kernel, traffic_key, workload, scaling):
+    """One timed launch over this rank's shard of a secondary sweep (c4 / c5), after a small warm-up."""
+    T0, P0, Y0, prob = sweep_fn(mech, world, rank)
+    if args.sub_reactors:
+        T0, P0, Y0, prob = T0[: args.sub_reactors], P0[: args.sub_reactors], Y0[: args.sub_reactors], prob[
+            : args.sub_reactors]
+    sh = Shard(dm, dev, T0, P0, Y0, prob)
+    cfg = _native.make_cfg(**RUN)
+    sh.step(cfg, 0, min(sh.n, 256))  # warm-up launch (code objects, LDS configuration)
+    tmax, kern_ms, res = timed(world, lambda: sh.step(cfg), 1)
+    stats = res["stats"].cpu().numpy()
+    tau = res["tau"].cpu().numpy()
+    total = torch.tensor([sh.n], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(total)
+    total = int(total.item())
+    line = {"metric": f"reactor integrations/sec ({workload})", "value": total / tmax, "unit": "reactors/s",
+            "reactors_total": total, "reactors_per_gpu": sh.n, "seconds": tmax, "scaling": scaling,
+            "failed_reactors": int((stats[:, 6] != 0).sum()), "not_ignited": int((tau <= 0).sum()),
+            "solver": solver_summary(stats),
+            "roofline": reactor_roofline(ops, stats, float(np.mean(kern_ms)) / 1e3, kernel, traffic_key, sh.n),
+            "cpu_baseline": None}
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        line["cpu_baseline"] = cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau, args.cpu_seconds_secondary,
+                                                    args.cpu_sample, single=True)
+    del sh, res
+    return line
 
 
 def main():
@@ -162,19 +361,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reactors", type=int, default=0, help="override reactors per GPU (0 = full 65,536 shard)")
+    ap.add_argument("--reactors", type=int, default=0, help="override the headline reactors per GPU (0 = full 65,536)")
+    ap.add_argument("--sub-reactors", type=int, default=0, help="cap the c4 / c5 shards (0 = full sweeps)")
+    ap.add_argument("--lines", default="c3,c4,c5,rop,lu,rop161",
+                    help="comma list of: c3 (headline, always run), c4, c5, rop, lu, rop161")
     ap.add_argument("--rop-states", type=int, default=10_000_000)
-    ap.add_argument("--lu-systems", type=int, default=16384,
-                    help="configs[4] component: batched n = 161 Newton-matrix LU on MFMA (0 = skip)")
-    ap.add_argument("--big-states", type=int, default=1_000_000,
-                    help="configs[4] component: ROP+thermo on the synthetic 161-species mechanism (0 = skip)")
-    ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
-    ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
-                    help="c3: configs[2], 65,536 CONP reactors per GPU (weak scaling, the metric); "
-                         "c4: configs[3], 2^20 CONP+CONV reactors in total (strong scaling)")
+    ap.add_argument("--lu-systems", type=int, default=16384)
+    ap.add_argument("--big-states", type=int, default=1_000_000)
+    ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in a CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget of the headline")
+    ap.add_argument("--cpu-seconds-secondary", type=float, default=6.0, help="CPU-baseline budget of c4 / c5")
     args = ap.parse_args()
+    lines = set(args.lines.split(","))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -189,173 +387,64 @@ def main():
     ops = count_ops(tables)
     dm = _native.DeviceMechanism(tables, device=dev)
 
-    if args.workload == "c4":
-        T0, P0, Y0, prob = sweep_c4(mech, world, rank)
-    else:
-        T0, P0, Y0 = sweep(mech, world, rank)
-        prob = np.ones(len(T0), np.int32)
+    # ---- headline: configs[2]
+    T0, P0, Y0, prob = sweep(mech, world, rank)
     if args.reactors:
         T0, P0, Y0, prob = T0[: args.reactors], P0[: args.reactors], Y0[: args.reactors], prob[: args.reactors]
-    n = len(T0)
-    T0_d = torch.as_tensor(T0, device=dev)
-    P0_d = torch.as_tensor(P0, device=dev)
-    V0_d = torch.ones(n, dtype=torch.float64, device=dev)
-    Y0_d = torch.as_tensor(Y0, device=dev).contiguous()
-    prob_d = torch.as_tensor(prob, device=dev)
+    sh = Shard(dm, dev, T0, P0, Y0, prob)
+    n = sh.n
     cfg = _native.make_cfg(**RUN)
-    out = dict(tau=torch.empty(n, dtype=torch.float64, device=dev), T=torch.empty(n, dtype=torch.float64, device=dev),
-               P=torch.empty(n, dtype=torch.float64, device=dev), V=torch.empty(n, dtype=torch.float64, device=dev),
-               Y=torch.empty((n, mech.KK), dtype=torch.float64, device=dev),
-               stats=torch.empty((n, _native.NSTAT), dtype=torch.int32, device=dev))
-
-    def step():
-        return dm.reactor_run(cfg, prob_d, T0_d, P0_d, V0_d, Y0_d, out=out)
-
     for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record()
-        res = step()
-        ev[k][1].record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    tmax = tmax.item()
-
+        sh.step(cfg)
+    tmax, kern_ms, res = timed(world, lambda: sh.step(cfg), args.steps)
     stats = res["stats"].cpu().numpy()
     tau = res["tau"].cpu().numpy()
-    nbad = int((stats[:, 6] != 0).sum())
-    nnoign = int((tau <= 0).sum())
-    flops = reactor_flops(ops, stats)
     kern_s = float(np.mean(kern_ms)) / 1e3
-    achieved_tf = flops / kern_s / 1e12
-
-    total_reactors = n * world * args.steps
-    value = total_reactors / tmax
+    value = n * world * args.steps / tmax
 
     # PCIe-inclusive rate (reported beside value, never as value): host numpy inputs -> H2D ->
     # one launch -> D2H of tau, T, P, V, Y, stats, on this rank
     torch.cuda.synchronize()
     tp = time.perf_counter()
     rp = dm.reactor_run(cfg, prob, T0, P0, np.ones(n), Y0)
-    host_out = {k: v.cpu().numpy() for k, v in rp.items()}
+    host_out = {k: v.cpu().numpy() for k, v in rp.items() if not k.startswith("_")}
     torch.cuda.synchronize()
     pcie_s = time.perf_counter() - tp
-    pcie = {"reactors_per_s": n / pcie_s, "seconds": pcie_s,
+    pcie = {"reactors_per_s": n / pcie_s, "seconds": pcie_s, "vs_value": (n / pcie_s) / (value / world),
             "bytes_h2d": int(T0.nbytes + P0.nbytes + Y0.nbytes + prob.nbytes + 8 * n),
             "bytes_d2h": int(sum(a.nbytes for a in host_out.values()))}
     del rp, host_out
 
-    # ---- ROP + thermo (configs[1]) : secondary metric
-    rop = None
-    if args.rop_states > 0:
-        rng = np.random.default_rng(0)
-        ns = args.rop_states
-        Ts = torch.as_tensor(rng.uniform(300.0, 3000.0, ns), device=dev)
-        Ps = torch.as_tensor(P_ATM * 10.0 ** rng.uniform(-1.0, 2.0, ns), device=dev)
-        Ys = torch.as_tensor(rng.dirichlet(0.5 * np.ones(mech.KK), ns).T.copy(), device=dev)
-        wdot = torch.empty((mech.KK, ns), dtype=torch.float64, device=dev)
-        cp = torch.empty(ns, dtype=torch.float64, device=dev)
-        hh = torch.empty(ns, dtype=torch.float64, device=dev)
-        dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
-        torch.cuda.synchronize()
-        reps = 3
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(reps):
-            dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
-        e1.record()
-        torch.cuda.synchronize()
-        sec = e0.elapsed_time(e1) / 1e3 / reps
-        rop = {
-            "value": ns / sec, "unit": "states/s", "states": ns, "ms_per_launch": sec * 1e3,
-            "roofline": {
-                "bound": "mfma", "pipe": "fp64-valu", "achieved": ops["F_rop"] * ns / sec / 1e12,
-                "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": ops["F_rop"] * ns / sec / 1e12 / FP64_PEAK_TFLOPS,
-                "hbm_GBs": ops["bytes_rop"] * ns / sec / 1e9, "hbm_frac": ops["bytes_rop"] * ns / sec / 1e9 / HBM_PEAK_GBS,
-                "traffic": load_traffic("rop", ns),
-            },
-            "cpu_baseline": None,
-        }
-        if rank == 0 and world == 1 and args.cpu_sample > 0:
-            # oracle C restatement over the first 200k of the same states (OpenMP over states), and
-            # over the first 20k on one core; the GPU result of the same states is the checker
-            from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
-            orc_r = Oracle(mech)
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            m = min(ns, 200_000)
-            Th, Ph, Yh = Ts[:m].cpu().numpy(), Ps[:m].cpu().numpy(), Ys[:, :m].cpu().numpy()
-            tc = time.perf_counter()
-            wc, _, _ = orc_r.rop_batch(Th, Ph, Yh, nthreads=threads)
-            t_all = time.perf_counter() - tc
-            m1 = min(m, 20_000)
-            tc = time.perf_counter()
-            orc_r.rop_batch(Th[:m1], Ph[:m1], np.ascontiguousarray(Yh[:, :m1]), nthreads=1)
-            t_one = time.perf_counter() - tc
-            wg = wdot[:, :m].cpu().numpy()
-            rop["cpu_baseline"] = {
-                "value": m / t_all, "unit": "states/s", "cores": threads, "kind": "port",
-                "single_core_value": m1 / t_one,
-                "sample": f"first {m} of the same 10M states ({m1} on one core), oracle C restatement, OpenMP over states",
-                "wdot_max_rel_diff_vs_gpu": float(np.max(np.abs(wg - wc) / np.max(np.abs(wc), axis=0, keepdims=True))),
-            }
-        del Ts, Ps, Ys, wdot, cp, hh
-
-    # ---- configs[4] component: batched FP64 LU of n = 161 Newton matrices (MFMA trailing updates)
-    lu = None
-    if rank == 0 and args.lu_systems > 0:
-        lu = lu_bench(dev, args.lu_systems, 161)
-
-    rop_big = None
-    if rank == 0 and args.big_states > 0:
-        rop_big = rop_bench(dev, Mechanism.from_files(os.path.join(ROOT, "data", "gri30_tracer161_chem.inp"),
-                                                      os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat")),
-                            args.big_states)
-
-    # ---- CPU baseline (rank 0, N = 1): oracle C restatement on a strided sample
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
-        from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
-        orc = Oracle(mech)
-        # strided sample of the same sweep, processed in chunks until ~cpu_seconds of CPU work
-        stride = max(1, n // args.cpu_sample)
-        order = np.random.default_rng(0).permutation(np.arange(0, n, stride)[: args.cpu_sample])
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        chunk = 32 * threads
-        done, tcpu, dmax = 0, 0.0, 0.0
-        while done < order.size and tcpu < args.cpu_seconds:
-            idx = order[done: done + chunk]
-            tc = time.perf_counter()
-            nfail, cres, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=prob[idx],
-                                               V0=np.ones(len(idx)), nthreads=threads, **RUN)
-            tcpu += time.perf_counter() - tc
-            ctau = np.array([r.tau for r in cres])
-            dmax = max(dmax, float(np.max(np.abs(tau[idx] / ctau - 1))))
-            done += len(idx)
-        # the same oracle on one core, over the first chunk of the sample (~3 s)
-        idx1 = order[: max(8, min(64, order.size))]
-        tc = time.perf_counter()
-        orc.reactor_batch(T0[idx1], P0[idx1], Y0[idx1], problem=prob[idx1], V0=np.ones(len(idx1)), nthreads=1, **RUN)
-        one_core = len(idx1) / (time.perf_counter() - tc)
-        cpu = {"value": done / tcpu, "unit": "reactors/s", "cores": threads, "kind": "port",
-               "single_core_value": one_core, "single_core_sample": f"{len(idx1)} reactors of the same sample",
-               "sample": f"{done} reactors (random subset of every {stride}th of this GPU's sweep), oracle C restatement, "
-                         f"OpenMP over reactors",
-               "tau_max_rel_diff_vs_gpu": dmax,
-               "seconds": tcpu}
+        cpu = cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau, args.cpu_seconds, args.cpu_sample)
+    del sh, res
+
+    c4 = c5 = rop = lu = rop_big = None
+    if "c4" in lines:
+        c4 = secondary_sweep("c4", dm, dev, mech, ops, sweep_c4, world, rank, args, "reactor_kernel<54>", "reactor_c4",
+                             "configs[3]: GRI-3.0 CH4/air 128 T0 x 64 phi x 64 P x {CONP, CONV} = 2^20 reactors in total",
+                             "strong")
+    if "c5" in lines:
+        bm = big_mechanism()
+        bops = count_ops(bm.to_tables())
+        bdm = _native.DeviceMechanism(bm.to_tables(), device=dev)
+        c5 = secondary_sweep("c5", bdm, dev, bm, bops, sweep_c5, world, rank, args, "big_reactor_kernel<11>",
+                             "big_reactor",
+                             "configs[4] stand-in: 161-species GRI-3.0 + 108-tracer mechanism (no n-heptane mechanism "
+                             "offline; parity with Chemkin unpinned), 64 T0 x 64 phi x 64 P = 262,144 CONP reactors in "
+                             "total", "strong")
+        c5["mechanism"] = f"data/gri30_tracer161 (KK = {bm.KK}, II = {bm.II}, n = {bm.KK + 1})"
+        bdm.close()
+    if "rop" in lines and args.rop_states > 0:
+        rop = rop_line(dev, mech, ops, args.rop_states, rank, world, args.cpu_sample)
+    if "lu" in lines and rank == 0 and args.lu_systems > 0:
+        lu = lu_line(dev, args.lu_systems, 161)
+    if "rop161" in lines and rank == 0 and args.big_states > 0:
+        bm = big_mechanism()
+        rop_big = rop_line(dev, bm, count_ops(bm.to_tables()), args.big_states, rank, world, 0,
+                           kernel_name="rop_kernel<0,3>", traffic_key="rop_161sp",
+                           label=f"synthetic GRI-3.0 + tracers, KK = {bm.KK}, II = {bm.II}")
 
     if rank == 0:
         line = {
@@ -367,31 +456,26 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": tmax / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak" if args.workload == "c3" else "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": ("configs[2]: GRI-3.0 CONP CH4/air ignition sweep 64 T0 x 32 phi x 32 P per GPU"
-                                    if args.workload == "c3" else
-                                    "configs[3]: GRI-3.0 CH4/air 128 T0 x 64 phi x 64 P x {CONP, CONV} = 2^20 "
-                                    "reactors in total"),
-                       "reactors_per_gpu": n, "t_end_s": 1.0, "atol": 1e-10, "rtol": 1e-8, "ignition": "TIFP",
-                       "parallelism": f"shard-by-condition x{world}"},
+            "config": {"workload": "configs[2]: GRI-3.0 CONP CH4/air ignition sweep 64 T0 x 32 phi x 32 P per GPU",
+                       "reactors_per_gpu": n, "t_end_s": RUN["t_end"], "atol": RUN["atol"], "rtol": RUN["rtol"],
+                       "ignition": "TIFP", "parallelism": f"shard-by-condition x{world}"},
+            "value_excludes_pcie": True,
             "reactors_per_min": value * 60.0,
-            "failed_reactors": nbad,
-            "not_ignited": nnoign,
-            "solver": {"mean_steps": float(stats[:, 0].mean()), "mean_rhs": float(stats[:, 1].mean()),
-                       "mean_jac": float(stats[:, 2].mean()), "mean_lu": float(stats[:, 3].mean()),
-                       "mean_newton": float(stats[:, 7].mean())},
-            "roofline": {"bound": "mfma", "pipe": "fp64-valu", "kernel": "reactor_kernel<54>",
-                         "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": load_traffic("reactor", n),
-                         "flops_per_launch": flops, "kernel_ms": kern_s * 1e3},
+            "failed_reactors": int((stats[:, 6] != 0).sum()),
+            "not_ignited": int((tau <= 0).sum()),
+            "solver": solver_summary(stats),
+            "roofline": reactor_roofline(ops, stats, kern_s, "reactor_kernel<54>", "reactor", n),
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
+            "c4": c4,
+            "c5": c5,
             "rop": rop,
             "lu": lu,
             "rop_161sp": rop_big,
-            "pcie_inclusive": pcie,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

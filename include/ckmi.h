@@ -133,6 +133,9 @@ typedef struct {
   double* t_adap;          /* [n][max_adap] device */
   double* y_adap;          /* [n][max_adap][KK+1] device (T, Y) */
   int32_t* n_adap;         /* [n] device: points written */
+  /* time of the final state (Tend, Yend): t_end, or the time the run stopped early (IGN_STOP,
+   * solver failure).  DTSV rows after it (y_save) are NaN. */
+  double* t_stop;          /* [n] device */
 } ckmi_reactor_ext;
 
 /* per-reactor statistics written by ckmi_reactor_run (int32 [n][8]) */
@@ -198,6 +201,11 @@ int ckmi_reactor_run_ex(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int3
                         const ckmi_reactor_ext* ext, double* tau, double* Tend, double* Pend, double* Vend,
                         double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
                         void* stream);
+
+/* Reactor kernel selection (diagnostic / testing): 0 = automatic (one wave per reactor for KK + 1 <= 64,
+ * one 4-wave workgroup per reactor above, up to KK + 1 = 192), 1 = the workgroup-per-reactor kernel for
+ * every mechanism (lets tests run both integrators on the same GRI-3.0 reactors).  Process-wide. */
+int ckmi_set_reactor_path(int32_t path);
 
 /* Batched dense LU of Newton iteration matrices too large for one wave (mechanisms with more
  * than 63 species).  Replaces the factorisation inside the reference's

@@ -57,7 +57,7 @@ class ReactorCfg(ct.Structure):
 
 class ReactorExt(ct.Structure):
     _fields_ = [("afac_rxn", _P), ("afac", _P), ("max_adap", ct.c_int32), ("t_adap", _P), ("y_adap", _P),
-                ("n_adap", _P)]
+                ("n_adap", _P), ("t_stop", _P)]
 
 
 _lib: Optional[ct.CDLL] = None
@@ -78,6 +78,7 @@ PROTOTYPES = {
                                      _P, ct.c_int32, _P, _P, _P]),
     "ckmi_reactor_run_ex": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P,
                                         ct.POINTER(ReactorExt), _P, _P, _P, _P, _P, _P, ct.c_int32, _P, _P, _P]),
+    "ckmi_set_reactor_path": (ct.c_int, [ct.c_int32]),
     "ckmi_lu_factor_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
     "ckmi_lu_solve_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
     "ckmi_lu_last_error": (ct.c_char_p, []),
@@ -278,6 +279,7 @@ class DeviceMechanism:
         Vend = o.get("V", torch.empty(n, **f64))
         Yend = o.get("Y", torch.empty((n, self.KK), **f64))
         stats = o.get("stats", torch.empty((n, NSTAT), dtype=torch.int32, device=dev))
+        t_stop = o.get("t_stop", torch.empty(n, **f64))
         nsave = 0
         ts = ys = None
         if t_save is not None:
@@ -285,6 +287,7 @@ class DeviceMechanism:
             nsave = ts.numel()
             ys = torch.empty((n, nsave, self.KK + 1), **f64)
         ext = ReactorExt()
+        ext.t_stop = _ptr(t_stop)
         keep = []
         if afac_rxn is not None:
             ar = self._dev(afac_rxn, torch.int32).reshape(-1)
@@ -305,15 +308,24 @@ class DeviceMechanism:
                                          _ptr(Y0), ct.byref(ext), _ptr(tau), _ptr(Tend), _ptr(Pend), _ptr(Vend),
                                          _ptr(Yend), _ptr(stats), nsave, _ptr(ts), _ptr(ys), _stream_ptr(dev)),
                "ckmi_reactor_run_ex")
-        res = dict(tau=tau, T=Tend, P=Pend, V=Vend, Y=Yend, stats=stats)
+        res = dict(tau=tau, T=Tend, P=Pend, V=Vend, Y=Yend, stats=stats, t_stop=t_stop)
         if adap is not None:
             res.update(adap)
         if keep:
-            torch.cuda.current_stream(dev).synchronize()
+            # the per-reactor A-factor inputs stay referenced by the result: the launch is
+            # asynchronous on this stream, and the caching allocator may only reuse their memory
+            # for work ordered after it (no host synchronisation needed)
+            res["_inputs"] = keep
         if ys is not None:
             res["t_save"] = ts
             res["y_save"] = ys
         return res
+
+
+def set_reactor_path(path: int) -> None:
+    """0: automatic (wave per reactor for KK + 1 <= 64, workgroup per reactor above); 1: the
+    workgroup-per-reactor kernel for every mechanism (testing both integrators on one mechanism)."""
+    _check(lib().ckmi_set_reactor_path(int(path)), "ckmi_set_reactor_path")
 
 
 # ------------------------------------------------------------------ batched dense LU (n <= 192)

@@ -342,13 +342,22 @@ class BatchReactors(ReactorModel):
         self._final = dict(T=float(res["T"][0].item()), P=float(res["P"][0].item()), V=float(res["V"][0].item()),
                            Y=res["Y"][0].cpu().numpy())
         ys = res["y_save"][0].cpu().numpy()
+        t_stop = float(res["t_stop"][0].item())
+        if t_stop < ts[-1]:
+            # IGN_STOP or a failed run: the solution ends at the stop time (the kernel leaves NaN
+            # in the DTSV rows after it); the final state closes the trajectory
+            keep_rows = ~np.isnan(ys[:, 0])
+            ts, ys = ts[keep_rows], ys[keep_rows]
+            if ts.size == 0 or t_stop > ts[-1]:
+                yf = np.concatenate([[self._final["T"]], self._final["Y"]])
+                ts, ys = np.append(ts, t_stop), np.vstack([ys, yf])
         if max_adap:
             na = int(res["n_adap"][0].item())
             if na == max_adap:
                 logger.warning("adaptive solution points truncated at %d", max_adap)
             ta = res["t_adap"][0, :na].cpu().numpy()
             ya = res["y_adap"][0, :na].cpu().numpy()
-            keep = ~np.isin(ta, ts)
+            keep = ~np.isin(ta, ts) & (ta <= ts[-1])
             t_all = np.concatenate([ts, ta[keep]])
             order = np.argsort(t_all, kind="stable")
             ts, ys = t_all[order], np.concatenate([ys, ya[keep]])[order]

@@ -273,8 +273,11 @@ class Chemistry:
         mech = self._need()
         if reaction_index < 1 or reaction_index > mech.II:
             raise ChemistryError(f"reaction index is out of bound, range = [1 ~ {mech.II}]")
-        if AFactor < 0.0:
-            raise ChemistryError("A-factor must be >= 0")
+        # validate everything before any state changes, so host and device tables stay consistent
+        if not AFactor > 0.0:
+            raise ChemistryError("A-factor must be > 0")
+        if mech.reactions[reaction_index - 1].plog:
+            raise ChemistryError("the A-factor of a PLOG reaction is set by its PLOG table")
         mech.set_A_cgs(reaction_index - 1, AFactor)
         for (cid, dev), dm in list(_device._cache.items()):
             if cid == id(self):

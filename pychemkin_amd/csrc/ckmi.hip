@@ -11,12 +11,15 @@
 
 #include "../../include/ckmi.h"
 #include "ckmi_reactor.hpp"
+#include "ckmi_run.hpp"
+#include "ckmi_internal.hpp"
 
 using namespace ckmi;
 
 namespace {
 
 thread_local std::string g_err;
+int g_reactor_path = 0;  // ckmi_set_reactor_path
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -29,7 +32,6 @@ int fail(int code, const std::string& msg) {
     if (_e != hipSuccess) return fail(CKMI_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-enum { NF_FIRST = 0, NF_CONV_FAIL = 1, NF_ERR_FAIL = 2 };
 
 // Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py): per-reactor shader
 // cycles spent in each phase, written to a debug buffer no other code reads.
@@ -43,64 +45,8 @@ __device__ unsigned long long* g_phase_buf = nullptr;
 #define PH_T0() (void)0
 #define PH_ADD(slot) (void)0
 #endif
-enum { CF_NONE = 0, CF_BAD_J = 1, CF_OTHER = 2 };
 
 // ---------------------------------------------------------------- reactor kernel
-// ignition monitor (uniform scalars), mirrors oracle ign_* helpers
-struct Ign {
-  int mode, comp, found, started, have_prev, have_next;
-  double thresh, best, tbest, tprev, vprev, tnext, vnext, tlast, vlast, tau;
-};
-
-__device__ __forceinline__ void ign_peak_update(Ign& g, double t, double v) {
-  if (g.started && g.found == 0 && v > g.best) {
-    g.tprev = g.tlast;
-    g.vprev = g.vlast;
-    g.have_prev = 1;
-    g.best = v;
-    g.tbest = t;
-    g.have_next = 0;
-  } else if (g.started && !g.have_next && g.tbest != 0.0 && t > g.tbest) {
-    g.tnext = t;
-    g.vnext = v;
-    g.have_next = 1;
-  } else if (!g.started) {
-    g.best = v;
-    g.tbest = t;
-    g.have_prev = 0;
-  }
-  g.started = 1;
-  g.tlast = t;
-  g.vlast = v;
-}
-
-__device__ __forceinline__ double ign_peak_time(const Ign& g) {
-  if (g.tbest <= 0.0) return -1.0;
-  if (!(g.have_prev && g.have_next)) return g.tbest;
-  const double x0 = g.tprev, x1 = g.tbest, x2 = g.tnext;
-  const double y0 = g.vprev, y1 = g.best, y2 = g.vnext;
-  const double d01 = (y1 - y0) / (x1 - x0), d12 = (y2 - y1) / (x2 - x1);
-  const double a = (d12 - d01) / (x2 - x0);
-  if (!(a < 0.0)) return x1;
-  const double bc = d01 - a * (x0 + x1);
-  const double tv = -bc / (2.0 * a);
-  if (tv < x0 || tv > x2) return x1;
-  return tv;
-}
-
-// Device copy of the run configuration: the public struct plus the integration stop points
-// (the sorted union of both profiles' breakpoints in (0, t_end), where derivatives jump),
-// computed on the host by ckmi_reactor_run_ex.
-struct DevCfg {
-  ckmi_reactor_cfg c;
-  int ncrit;
-  double tcrit[128];
-};
-__device__ __forceinline__ int n_crit(const DevCfg* d) { return d->ncrit + 1; }
-__device__ __forceinline__ double crit_time(const DevCfg* d, double tend, int idx) {
-  return idx < d->ncrit ? d->tcrit[idx] : tend;
-}
-
 __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, double t, double yl, int lane, double& P,
                                          double& V) {
   const int KK = M.KK;
@@ -119,35 +65,6 @@ __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, dou
   }
 }
 
-struct ReactorIO {
-  const int* problem;
-  const double *T0, *P0, *V0, *Y0;
-  double *tau, *T, *P, *V, *Y;
-  int* stats;
-  int nsave;
-  const double* t_save;
-  double* y_save;
-  // ckmi_reactor_ext
-  const int* afac_rxn;
-  const double* afac;
-  int max_adap;
-  double* t_adap;
-  double* y_adap;
-  int* n_adap;
-};
-
-// Integrator control state of one wave (wave-uniform scalars, kept in the wave's LDS slice).
-struct Ctl {
-  int r, first, nflag, convfail, call_setup, failed, mm, ncf, nef, rc, isave, icrit, ncrit, status, nst, stopped;
-  int is_count, max_steps, nadap;
-  double avar_last;
-  double delp, saved_t, told, dsm, tc, tend, hmax, T0;
-  double st_h0, st_tout, st_h, is_hg, is_hub, is_hlb, is_t0;
-};
-
-// Per-wave LDS slice: 6 species vectors, third-body sums, integrator scalars, control state,
-// ignition monitor.
-__host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
 __host__ __device__ constexpr int slice_vec_bytes(int G) { return align16(8 * (6 * VL + (G > 0 ? G : 1))); }
 #ifdef CKMI_PHASE_TIMERS
 constexpr int PH_SLICE = 8 * 40;  // per-state (0..19) and per-strip (24..29) cycle counters
@@ -163,30 +80,6 @@ __host__ __device__ constexpr int jscratch_bytes() {
   return align16(8 * N * LDJ) + 16;  // + lock
 }
 
-// integrator states; the ones marked (f) resume after the RHS requested by their predecessor
-enum {
-  ST_NEXT = 0,       // pull the next reactor
-  ST_START_F,        // (f) f(t, y0) for the Nordsieck history
-  ST_INITSTEP_F,     // (f) one probe of the initial step-size estimate
-  ST_START_FINISH,   // initial step chosen: set up the history
-  ST_IGN0_F,         // (f) dT/dt at t = 0 for the inflection-point monitor
-  ST_STEP_BEGIN,     // top of the time loop
-  ST_STEP_ATTEMPT,   // predict + coefficients, begin a Newton solve
-  ST_NLS_ATTEMPT,    // request f at the predictor
-  ST_NLS_F,          // (f) f at the predictor; decide the Newton-matrix setup
-  ST_NLS_J,          // (f) fresh Jacobian is in the shared scratch
-  ST_SETUP,          // M = I - gamma J, LU
-  ST_NEWTON_ITER,    // one Newton iteration
-  ST_NEWTON_F,       // (f) f at the Newton iterate
-  ST_NLS_FAIL,       // Newton failure: retry with a fresh J or fail the step
-  ST_STEP_CONVFAIL,  // step failed to converge: shrink h
-  ST_ERRTEST,        // local error test
-  ST_ERR_F,          // (f) f after repeated error-test failures at order 1
-  ST_STEP_COMPLETE,  // accept the step, choose the next h and q
-  ST_STEP_END,       // outputs, ignition monitor, stops, critical-time restarts
-  ST_FINISH,         // write the reactor's results
-  ST_EXIT
-};
 
 // Persistent reactor kernel: one workgroup of RWAVES waves per CU slot.  The workgroup stages
 // the mechanism image into LDS once; each wave then pulls reactor indices from an HBM work
@@ -871,6 +764,13 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           double Pf, Vf;
           state_PV(V, R, tf, yf, lane, Pf, Vf);
           const int r = c.r;
+          // a run that ended early (IGN_STOP, solver failure) has no solution after tf: its
+          // remaining DTSV rows are NaN, never stale memory (the host trims them)
+          while (c.isave < io.nsave) {
+            if (act) io.y_save[((size_t)r * io.nsave + c.isave) * n + lane] = __builtin_nan("");
+            c.isave++;
+          }
+          if (io.t_stop && lane == 0) io.t_stop[r] = tf;
           if (lane == 0) {
             io.tau[r] = g.tau;
             io.T[r] = yf;
@@ -1108,20 +1008,6 @@ __global__ void species_thermo_kernel(MechDev M, int nstate, const double* __res
 }  // namespace
 
 // ====================================================================== host side
-struct ckmi_mech {
-  int device;
-  int KK, II, IIpad, G;
-  MechDev d;
-  MechImage img;  // compact LDS image (device copy in img.blob)
-  std::vector<void*> allocs;
-  // host copies of the forward Arrhenius (original order) for get/set
-  std::vector<double> lnA_orig, b_orig, E_orig;
-  std::vector<int> rtype_orig;
-  bool has_plog = false;
-  std::vector<int> slot_of;  // original reaction -> device slot
-  DevCfg* cfg_dev;
-  mutable DevCfg cfg_host;  // host staging of the per-call configuration
-};
 
 namespace {
 
@@ -1282,8 +1168,23 @@ size_t reactor_lds_bytes(const ckmi_mech* m) {
 }
 // Grid = (CUs x resident workgroups per CU), capped by the batch; J workspace = one
 // column-major N x 64 matrix per wave slot, allocated stream-ordered (~55 MB for GRI-3.0).
+// Per-launch copy of the run configuration: it lives in the launch's stream-ordered workspace,
+// so launches with different configurations on one mechanism handle (other streams, other host
+// threads) never share it.  The host staging copy is released by a host function enqueued
+// behind the copy, i.e. only once the stream has consumed it.
+int stage_cfg(const DevCfg& dc, DevCfg* dst, hipStream_t stream) {
+  auto* hc = new DevCfg(dc);
+  const hipError_t e = hipMemcpyAsync(dst, hc, sizeof(DevCfg), hipMemcpyHostToDevice, stream);
+  if (e != hipSuccess) {
+    delete hc;
+    return fail(CKMI_ERR_HIP, std::string("cfg copy: ") + hipGetErrorString(e));
+  }
+  HIP_CHECK(hipLaunchHostFunc(stream, [](void* p) { delete static_cast<DevCfg*>(p); }, hc));
+  return CKMI_OK;
+}
+
 template <int N, bool PL = false>
-int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t stream) {
+int launch_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO& io, hipStream_t stream) {
   const size_t lds = reactor_lds_bytes<N>(m);
   static thread_local std::map<int, int> max_lds_set;
   if (lds > 64 * 1024 && max_lds_set[m->device] < (int)lds) {
@@ -1296,16 +1197,22 @@ int launch_reactors(const ckmi_mech* m, int n, const ReactorIO& io, hipStream_t 
   if (per_cu < 1) return fail(CKMI_ERR_SIZE, "reactor kernel does not fit on a CU (LDS " + std::to_string(lds) + " B)");
   const int want = (n + RWAVES - 1) / RWAVES;
   const int grid = std::max(1, std::min(ncu * per_cu, want));
-  const size_t jbytes = (size_t)grid * RWAVES * N * WAVE * sizeof(double);
+  // the wave's parked Jacobian is FP32 (N x 64 floats per wave slot)
+  const size_t jbytes = ((size_t)grid * RWAVES * N * WAVE * sizeof(float) + 255) & ~(size_t)255;
+  const size_t cbytes = (sizeof(DevCfg) + 255) & ~(size_t)255;
   void* ws = nullptr;
-  HIP_CHECK(hipMallocAsync(&ws, jbytes + 256, stream));
-  int* queue = (int*)((char*)ws + jbytes);
-  HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(int), stream));
-  hipLaunchKernelGGL((reactor_kernel<N, PL>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, m->cfg_dev, n, queue,
-                     (double*)ws, io);
-  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMallocAsync(&ws, jbytes + cbytes + 256, stream));
+  DevCfg* dcfg = (DevCfg*)((char*)ws + jbytes);
+  int* queue = (int*)((char*)ws + jbytes + cbytes);
+  int rc = stage_cfg(dc, dcfg, stream);
+  if (rc == CKMI_OK) {
+    HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(int), stream));
+    hipLaunchKernelGGL((reactor_kernel<N, PL>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, dcfg, n, queue,
+                       (double*)ws, io);
+    HIP_CHECK(hipGetLastError());
+  }
   HIP_CHECK(hipFreeAsync(ws, stream));
-  return CKMI_OK;
+  return rc;
 }
 
 template <int MODE, int NCH, bool PL>
@@ -1347,6 +1254,8 @@ int launch_rop(const ckmi_mech* m, int n, const double* T, const double* P, cons
 }
 
 }  // namespace
+
+int ckmi::set_error(int code, const std::string& msg) { return fail(code, msg); }
 
 extern "C" {
 
@@ -1548,10 +1457,6 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   rc |= upload(m, geff, &D.geff);
   rc |= build_image(m, d, slots, flags, nrp, rsp, psp, rnu, pnu, lnA, beta, Ea, lnA0, beta0, Ea0, fp, rlnA, rbeta, rEa,
                     tb, gptr, gsp, geff, wt, rwt);
-  void* cp = nullptr;
-  if (hipMalloc(&cp, sizeof(DevCfg)) != hipSuccess) rc |= CKMI_ERR_HIP;
-  else m->allocs.push_back(cp);
-  m->cfg_dev = static_cast<DevCfg*>(cp);
   if (rc) {
     ckmi_mech_destroy(m);
     return rc;
@@ -1628,9 +1533,6 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
                         double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
                         void* stream) {
   if (!m || !cfg || n < 0) return fail(CKMI_ERR_ARG, "bad argument");
-  if (m->KK + 1 > 64)  // the wave-per-reactor integrator: lane = state component
-    return fail(CKMI_ERR_UNSUPPORTED, "batch reactors with more than 63 species are not supported yet "
-                                      "(the ROP/thermo kernels and ckmi_lu_factor_batched are)");
   if (cfg->nprof < 0 || cfg->nprof > 64) return fail(CKMI_ERR_ARG, "nprof must be in [0, 64]");
   if (!(cfg->t_end > 0.0) || !(cfg->rtol > 0.0) || !(cfg->atol > 0.0)) return fail(CKMI_ERR_ARG, "t_end, rtol, atol must be > 0");
   if (cfg->energy != 1 && cfg->energy != 2) return fail(CKMI_ERR_ARG, "energy must be 1 or 2");
@@ -1652,8 +1554,8 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   if (cfg->nprof2 > 0 && cfg->energy != 1) return fail(CKMI_ERR_ARG, "QPRO / AEXT need an energy-equation run");
   if (cfg->avar > m->KK || cfg->avar < -1) return fail(CKMI_ERR_ARG, "avar must be -1, 0 (T) or 1 + species index");
   if (n == 0) return CKMI_OK;
+  DevCfg dc;  // this call's configuration (staged per launch: no state shared between calls)
   {
-    DevCfg& dc = m->cfg_host;
     dc.c = *cfg;
     if (dc.c.gfac == 0.0) dc.c.gfac = 1.0;
     std::vector<double> tc;
@@ -1665,21 +1567,28 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
     tc.erase(std::unique(tc.begin(), tc.end()), tc.end());
     dc.ncrit = (int)tc.size();
     std::copy(tc.begin(), tc.end(), dc.tcrit);
-    // pageable source: the runtime stages it before returning
-    HIP_CHECK(hipMemcpyAsync(m->cfg_dev, &dc, sizeof(DevCfg), hipMemcpyHostToDevice, (hipStream_t)stream));
   }
   ReactorIO io{problem, T0, P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save,
                ext ? ext->afac_rxn : nullptr, ext ? ext->afac : nullptr, ext ? ext->max_adap : 0,
-               ext ? ext->t_adap : nullptr, ext ? ext->y_adap : nullptr, ext ? ext->n_adap : nullptr};
+               ext ? ext->t_adap : nullptr, ext ? ext->y_adap : nullptr, ext ? ext->n_adap : nullptr,
+               ext ? ext->t_stop : nullptr};
   const int nvar = m->KK + 1;
   int rc;
   // PLOG mechanisms use one (64-wide) reactor variant, so that the PLOG branch costs compile time once
-  if (m->has_plog) rc = launch_reactors<64, true>(m, n, io, (hipStream_t)stream);
-  else if (nvar <= 32) rc = launch_reactors<32>(m, n, io, (hipStream_t)stream);
-  else if (nvar <= 54) rc = launch_reactors<54>(m, n, io, (hipStream_t)stream);
-  else rc = launch_reactors<64>(m, n, io, (hipStream_t)stream);
+  // more than 63 species: one workgroup per reactor (ckmi_big.hip); else one wave per reactor
+  if (nvar > 64 || g_reactor_path == 1) rc = launch_big_reactors(m, n, dc, io, (hipStream_t)stream);
+  else if (m->has_plog) rc = launch_reactors<64, true>(m, n, dc, io, (hipStream_t)stream);
+  else if (nvar <= 32) rc = launch_reactors<32>(m, n, dc, io, (hipStream_t)stream);
+  else if (nvar <= 54) rc = launch_reactors<54>(m, n, dc, io, (hipStream_t)stream);
+  else rc = launch_reactors<64>(m, n, dc, io, (hipStream_t)stream);
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
+  return CKMI_OK;
+}
+
+int ckmi_set_reactor_path(int32_t path) {
+  if (path != 0 && path != 1) return fail(CKMI_ERR_ARG, "reactor path must be 0 (automatic) or 1 (workgroup)");
+  g_reactor_path = path;
   return CKMI_OK;
 }
 

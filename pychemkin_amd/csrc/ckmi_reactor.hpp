@@ -564,23 +564,30 @@ struct BdfS {
 // The Nordsieck history lives in the wave's LDS slice (zn[j] of lane l at base_l + j * 512):
 // it is touched a few times per step, and its 12 VGPRs are worth more to the register-resident
 // Newton matrix.
-struct ZnLds {
-  int base;  // LDS byte offset of this lane's zn[0]
-  __device__ __forceinline__ double& operator[](int j) const { return *lds_at<double>(base + j * WAVE * 8); }
+// ST = threads per Nordsieck row: WAVE for the wave-per-reactor kernel, the workgroup size for
+// the workgroup-per-reactor kernel of large mechanisms (ckmi_big.hip).
+template <int ST>
+struct ZnLdsT {
+  int base;  // LDS byte offset of this thread's zn[0]
+  __device__ __forceinline__ double& operator[](int j) const { return *lds_at<double>(base + j * ST * 8); }
 };
+using ZnLds = ZnLdsT<WAVE>;
 constexpr int ZN_BYTES = (QMAX + 1) * WAVE * 8;
 
-struct Bdf {
-  ZnLds zn;
+template <int ST>
+struct BdfT {
+  ZnLdsT<ST> zn;
   double ewt, acor, tempv, ftemp, y;
 };
+using Bdf = BdfT<WAVE>;
 
 __device__ __forceinline__ double wrms_lane(double v, double ewt, int n) {
   const double x = v * ewt;
   return sqrt(wave_sum(x * x) / n);
 }
 
-__device__ __forceinline__ void bdf_rescale(Bdf& b, BdfS& S) {
+template <class BB>
+__device__ __forceinline__ void bdf_rescale(BB& b, BdfS& S) {
   double factor = S.eta;
 #pragma unroll
   for (int j = 1; j <= QMAX; ++j) {
@@ -594,7 +601,8 @@ __device__ __forceinline__ void bdf_rescale(Bdf& b, BdfS& S) {
 }
 
 // zn_{j-1} += zn_j for k = 1..q, j = q..k (Pascal-triangle prediction), in registers
-__device__ __forceinline__ void bdf_predict(Bdf& b, BdfS& S) {
+template <class BB>
+__device__ __forceinline__ void bdf_predict(BB& b, BdfS& S) {
   S.tn += S.h;
   const int q = S.q;
   double z[QMAX + 1];
@@ -609,7 +617,8 @@ __device__ __forceinline__ void bdf_predict(Bdf& b, BdfS& S) {
   for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
-__device__ __forceinline__ void bdf_restore(Bdf& b, BdfS& S, double saved_t) {
+template <class BB>
+__device__ __forceinline__ void bdf_restore(BB& b, BdfS& S, double saved_t) {
   S.tn = saved_t;
   const int q = S.q;
   double z[QMAX + 1];
@@ -624,7 +633,8 @@ __device__ __forceinline__ void bdf_restore(Bdf& b, BdfS& S, double saved_t) {
   for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
-__device__ __forceinline__ void bdf_set(Bdf& b, BdfS& S) {
+template <class BB>
+__device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
   const int q = S.q;
   double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = S.h;
   S.l[0] = S.l[1] = 1.0;
@@ -680,7 +690,8 @@ __device__ __forceinline__ void bdf_set(Bdf& b, BdfS& S) {
   S.gamrat = (S.nst > 0) ? S.gamma / S.gammap : 1.0;
 }
 
-__device__ __forceinline__ void bdf_adjust_order(Bdf& b, BdfS& S, int deltaq) {
+template <class BB>
+__device__ __forceinline__ void bdf_adjust_order(BB& b, BdfS& S, int deltaq) {
   const int q = S.q;
 #pragma unroll
   for (int i = 0; i <= QMAX; ++i) S.l[i] = 0.0;
@@ -731,7 +742,8 @@ __device__ __forceinline__ void bdf_adjust_order(Bdf& b, BdfS& S, int deltaq) {
   }
 }
 
-__device__ __forceinline__ double dky0_lane(const Bdf& b, const BdfS& S, double t) {
+template <class BB>
+__device__ __forceinline__ double dky0_lane(const BB& b, const BdfS& S, double t) {
   const double sc = (t - S.tn) / S.h;
   double v = 0.0;
 #pragma unroll

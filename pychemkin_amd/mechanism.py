@@ -388,6 +388,9 @@ class Mechanism:
                 if current.kind != RXN_FALLOFF:
                     raise MechanismError(f"LOW on a non-falloff reaction {current.equation}")
             elif k == "HIGH":
+                # chemically activated: only a (+M) pressure-dependent reaction can carry HIGH
+                if current.kind not in (RXN_FALLOFF, RXN_CHEMACT) or current.third_body is None:
+                    raise MechanismError(f"HIGH on a reaction without (+M): {current.equation}")
                 current.high = tuple(nums[:3])
                 current.kind = RXN_CHEMACT
             elif k == "TROE":

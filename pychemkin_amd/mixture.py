@@ -275,8 +275,10 @@ class Mixture:
         return self.ROP() * self._WT
 
     def volHRR(self) -> float:
-        """Volumetric heat release rate [erg/cm3-s] = -sum_k h_k wdot_k (mixture.py:2172)."""
-        return float(-np.sum(self.species_H() * self.ROP()))
+        """Volumetric "heat release rate" [erg/cm3-s] = sum_k H_k ROP_k, sign as the reference
+        returns it (mixture.py:2172-2202: np.dot(H, ROP), no negation; negative when heat is
+        released)."""
+        return float(np.dot(self.species_H(), self.ROP()))
 
     @staticmethod
     def _sorted_nonzero(values: np.ndarray, threshold: float):

@@ -16,7 +16,7 @@ from pychemkin_amd import _native
 from oracle.oracle import Oracle
 mech = bench.mechanism()
 dm = _native.DeviceMechanism(mech.to_tables(), device=0)
-T0, P0, Y0 = bench.sweep(mech, 1, 0)
+T0, P0, Y0, _ = bench.sweep(mech, 1, 0)
 idx = np.arange(0, len(T0), len(T0) // 16)[:16]
 res = dm.reactor_run(_native.make_cfg(**bench.RUN), np.ones(len(idx), np.int32), T0[idx], P0[idx], np.ones(len(idx)),
                      Y0[idx])

@@ -29,7 +29,7 @@ def main():
     mech = Mechanism.from_files(os.path.join(ROOT, "data", "grimech30_chem.inp"),
                                 os.path.join(ROOT, "data", "grimech30_thermo.dat"))
     dm = _native.DeviceMechanism(mech.to_tables(), device=0)
-    T0, P0, Y0 = bench.sweep(mech, 1, 0)
+    T0, P0, Y0, _ = bench.sweep(mech, 1, 0)
     prob, V0 = np.ones(len(T0), np.int32), np.ones(len(T0))
     idx = np.arange(0, len(T0), max(1, len(T0) // n))[:n]
     buf = torch.zeros((len(idx), 48), dtype=torch.int64, device="cuda:0")

@@ -23,7 +23,7 @@ def main():
     ns = int(os.environ.get("PMC_STATES", "2000000"))
     mech = bench.mechanism()
     dm = _native.DeviceMechanism(mech.to_tables(), device=0)
-    T0, P0, Y0 = bench.sweep(mech, 1, 0)
+    T0, P0, Y0, _ = bench.sweep(mech, 1, 0)
     idx = np.arange(0, len(T0), max(1, len(T0) // nr))[:nr]
     res = dm.reactor_run(_native.make_cfg(**bench.RUN), np.ones(len(idx), np.int32), T0[idx], P0[idx],
                          np.ones(len(idx)), Y0[idx])

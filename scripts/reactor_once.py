@@ -19,7 +19,7 @@ def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
     mech = bench.mechanism()
     dm = _native.DeviceMechanism(mech.to_tables(), device=0)
-    T0, P0, Y0 = bench.sweep(mech, 1, 0)
+    T0, P0, Y0, _ = bench.sweep(mech, 1, 0)
     idx = np.arange(0, len(T0), max(1, len(T0) // n))[:n]
     res = dm.reactor_run(_native.make_cfg(**bench.RUN), np.ones(len(idx), np.int32), T0[idx], P0[idx],
                          np.ones(len(idx)), Y0[idx])

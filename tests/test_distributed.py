@@ -30,7 +30,7 @@ def _worker(rank, world, port, q):
     from oracle.oracle import Oracle
 
     mech = bench.mechanism()
-    T0, P0, Y0 = bench.sweep(mech, world, rank, nT=4, nphi=2, nP=2)
+    T0, P0, Y0, _ = bench.sweep(mech, world, rank, nT=4, nphi=2, nP=2)
     orc = Oracle(mech)
     _, res, Yend = orc.reactor_batch(T0, P0, Y0, problem=np.ones(len(T0), np.int32), V0=np.ones(len(T0)),
                                      nthreads=1, energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
@@ -59,7 +59,7 @@ def test_two_rank_shards_partition_the_sweep_and_match_single_rank():
     outs.sort()
     assert all(o[5] == 2.0 for o in outs)  # max-over-ranks reduction
     mech = bench.mechanism()
-    T_f, P_f, Y_f = bench.sweep(mech, 1, 0, nT=8, nphi=2, nP=2)
+    T_f, P_f, Y_f, _ = bench.sweep(mech, 1, 0, nT=8, nphi=2, nP=2)
     key = lambda T, P, yo2: (T, P, yo2)  # (T0, P0, Y_O2) identifies a condition (phi sets Y_O2)
     got = sorted(key(*c) for o in outs for c in zip(o[1], o[2], o[3]))
     assert got == sorted(key(*c) for c in zip(T_f.tolist(), P_f.tolist(), Y_f[:, 3].tolist()))  # disjoint, complete
@@ -67,10 +67,33 @@ def test_two_rank_shards_partition_the_sweep_and_match_single_rank():
     from oracle.oracle import Oracle
 
     orc = Oracle(mech)
-    T0, P0, Y0 = bench.sweep(mech, 1, 0, nT=8, nphi=2, nP=2)
+    T0, P0, Y0, _ = bench.sweep(mech, 1, 0, nT=8, nphi=2, nP=2)
     _, res, _ = orc.reactor_batch(T0, P0, Y0, problem=np.ones(len(T0), np.int32), V0=np.ones(len(T0)), nthreads=1,
                                   energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
     full = {key(a, b, c): r.tau for a, b, c, r in zip(T0.tolist(), P0.tolist(), Y0[:, 3].tolist(), res)}
     for o in outs:
         for a, b, c, t in zip(o[1], o[2], o[3], o[4]):
             assert full[key(a, b, c)] == t
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_secondary_sweeps_partition_over_ranks(world):
+    """configs[3] (2^20 GRI reactors) and configs[4] (262,144 stand-in reactors) are strong-scaling
+    sweeps: the ranks' strided shards are disjoint and together are exactly the single-rank sweep."""
+    import bench
+
+    mech = bench.mechanism()
+    T1, P1, Y1, pr1 = bench.sweep_c4(mech, 1, 0)
+    assert T1.size == 2 ** 20 and set(np.unique(pr1)) == {1, 2}
+    parts = [bench.sweep_c4(mech, world, r) for r in range(world)]
+    assert sum(p[0].size for p in parts) == T1.size
+    for r, p in enumerate(parts):
+        assert np.array_equal(p[0], T1[r::world]) and np.array_equal(p[3], pr1[r::world])
+        assert np.array_equal(p[2], Y1[r::world])
+    big = bench.big_mechanism()
+    T5, P5, Y5, _ = bench.sweep_c5(big, 1, 0)
+    assert T5.size == 262144 and np.all(Y5[:, big.species.index("AX1")] > 0)
+    parts = [bench.sweep_c5(big, world, r) for r in range(world)]
+    assert sum(p[0].size for p in parts) == T5.size
+    for r, p in enumerate(parts):
+        assert np.array_equal(p[1], P5[r::world])

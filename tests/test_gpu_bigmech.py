@@ -88,14 +88,28 @@ def test_newton_matrices_161_species_lu(big):
         np.testing.assert_allclose(LU[s], lu_ref, rtol=0, atol=1e-12 * np.abs(lu_ref).max())
 
 
-def test_reactor_run_rejects_161_species_loudly(big):
-    from pychemkin_amd import _native
+def test_reactor_run_rejects_more_than_191_species_loudly(tmp_path):
+    """161 species run on the workgroup-per-reactor kernel (test_gpu_bigreactor.py); above KK = 191 the
+    Newton matrix no longer fits the register file of a CU, and ckmi_reactor_run says so."""
+    import sys
 
-    mech, _, dm = big
+    from pychemkin_amd import _native
+    from pychemkin_amd.mechanism import Mechanism
+
+    sys.path.insert(0, str(__import__("pathlib").Path(__file__).resolve().parents[1] / "data"))
+    from make_tracer_mechanism import write_big_mechanism
+
+    cp, tp = write_big_mechanism(str(tmp_path), n_tracer=150)  # 203 species
+    mech = Mechanism.from_files(cp, tp)
+    assert mech.KK == 203
+    dm = _native.DeviceMechanism(mech.to_tables())
     Y0 = np.zeros((1, mech.KK))
     Y0[0, mech.species.index("N2")] = 1.0
-    with pytest.raises(_native.NativeError, match="63 species"):
+    with pytest.raises(_native.NativeError, match="191 species"):
         dm.reactor_run(_native.make_cfg(energy=1, t_end=1e-3), np.ones(1, np.int32), [1000.0], [P_ATM], [1.0], Y0)
+    # the rate kernels still take it (mechanism image up to 255 species)
+    w, _, _ = dm.rop_thermo(np.array([1500.0]), np.array([P_ATM]), np.full((mech.KK, 1), 1.0 / mech.KK))
+    assert np.isfinite(w.cpu().numpy()).all()
 
 
 def test_drop_in_api_on_161_species_mechanism(big):

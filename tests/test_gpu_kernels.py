@@ -107,4 +107,5 @@ def test_mixture_rop_and_hrr(chem, oracle, mech):
     _, _, wo = oracle.rates(1500.0, 2 * P_ATM, m.Y)
     assert np.max(np.abs(m.ROP() - wo)) < 1e-11 * np.max(np.abs(wo))
     cpo, ho, _ = oracle.thermo(1500.0)
-    assert abs(m.volHRR() / -np.sum(wo * ho * R * 1500.0) - 1) < 1e-10
+    # reference mixture.py:2172-2202 returns np.dot(H, ROP) without negation
+    assert abs(m.volHRR() / np.sum(wo * ho * R * 1500.0) - 1) < 1e-10

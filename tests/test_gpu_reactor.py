@@ -183,7 +183,7 @@ def test_determinism_and_batch_order_invariance(dm, mech):
 
     import bench
 
-    T0, P0, Y0 = bench.sweep(mech, 1, 0, nT=8, nphi=4, nP=4)
+    T0, P0, Y0, _ = bench.sweep(mech, 1, 0, nT=8, nphi=4, nP=4)
     n = T0.size
     cfg = _native.make_cfg(**bench.RUN)
     prob = np.ones(n, np.int32)
@@ -202,7 +202,7 @@ def test_sweep_properties_at_scale(dm, mech):
 
     import bench
 
-    T0, P0, Y0 = bench.sweep(mech, 1, 0, nT=16, nphi=16, nP=16)
+    T0, P0, Y0, _ = bench.sweep(mech, 1, 0, nT=16, nphi=16, nP=16)
     n = T0.size
     res = {k: v.cpu().numpy() for k, v in dm.reactor_run(_native.make_cfg(**bench.RUN), np.ones(n, np.int32), T0, P0,
                                                           np.ones(n), Y0).items()}
