@@ -9,9 +9,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "ckmi.hip")        # kinetics, thermo and reactor kernels + C ABI
 LU_SRC = os.path.join(HERE, "csrc", "ckmi_lu.hip")  # batched MFMA LU (large mechanisms)
 BIG_SRC = os.path.join(HERE, "csrc", "ckmi_big.hip")  # workgroup-per-reactor integrator (64 <= KK + 1 <= 192)
+KIN_SRC = os.path.join(HERE, "csrc", "ckmi_kin.cpp")  # KIN-compatible host shims (include/ckmi_kin.h)
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp", "ckmi_image.hpp",
                                                 "ckmi_run.hpp", "ckmi_internal.hpp")] + [
-    os.path.join(HERE, "..", "include", "ckmi.h")]
+    os.path.join(HERE, "..", "include", "ckmi.h"), os.path.join(HERE, "..", "include", "ckmi_kin.h")]
 OUT = os.path.join(HERE, "_lib", "libckmi.so")
 OBJ_DIR = os.path.join(HERE, "_lib", "obj")
 ARCH = "gfx950"  # MI355X only
@@ -30,6 +31,7 @@ LU_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", f"--offload
 BIG_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-mcode-object-version=5", f"--offload-arch={ARCH}",
              "-mllvm", "-disable-machine-licm", "-mllvm", "-disable-machine-sink",
              "-mllvm", "-pragma-unroll-threshold=2000000"]
+KIN_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall"]  # host code only
 
 
 def _stale(target: str, sources) -> bool:
@@ -40,7 +42,7 @@ def _stale(target: str, sources) -> bool:
 
 
 def needs_build() -> bool:
-    return _stale(OUT, [SRC, LU_SRC, BIG_SRC] + DEPS)
+    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC] + DEPS)
 
 
 PROF_OUT = os.path.join(HERE, "_lib", "libckmi_prof.so")  # diagnostic phase-timer build
@@ -56,8 +58,8 @@ def _compile(src: str, obj: str, flags, verbose: bool) -> None:
 def build(force: bool = False, verbose: bool = False, prof: bool = False, out: str = None, extra=()) -> str:
     """Build libckmi.so (or the phase-timer build, or an A/B variant at `out` with `extra` flags).
 
-    Three translation units, compiled separately (the reactor kernel alone takes ~2 min) and linked
-    into one shared library: ckmi.hip, ckmi_lu.hip and ckmi_big.hip."""
+    Four translation units, compiled separately (the reactor kernel alone takes ~2 min) and linked
+    into one shared library: ckmi.hip, ckmi_lu.hip, ckmi_big.hip and the host-only ckmi_kin.cpp."""
     default = out is None and not prof and not extra
     out = out or (PROF_OUT if prof else OUT)
     if not force and default and not needs_build():
@@ -69,11 +71,14 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     big_obj = os.path.join(OBJ_DIR, "ckmi_big.o" if default else f"ckmi_big_{'prof' if prof else 'main'}.o")
     if force or _stale(big_obj, [BIG_SRC] + DEPS):
         _compile(BIG_SRC, big_obj, BIG_FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []), verbose)
+    kin_obj = os.path.join(OBJ_DIR, "ckmi_kin.o")
+    if force or _stale(kin_obj, [KIN_SRC] + DEPS):
+        _compile(KIN_SRC, kin_obj, KIN_FLAGS, verbose)
     tag = "main" if default else os.path.splitext(os.path.basename(out))[0]
     main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
     if force or (not default and not prof) or _stale(main_obj, [SRC] + DEPS):
         _compile(SRC, main_obj, FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(extra), verbose)
-    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj]
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj, kin_obj]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

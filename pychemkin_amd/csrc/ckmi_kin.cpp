@@ -1,0 +1,735 @@
+// ckmi_kin.cpp -- KIN-compatible C ABI shims (include/ckmi_kin.h) over the batched ckmi engine.
+//
+// The reference drives one native 0-D reactor per process through a sequence of by-pointer calls
+// (batchreactor.py:1149-1159, :1036-1047, :1083-1114): Setup -> SetupBatchInputs -> profile and
+// keyword text -> Calculate -> GetIgnitionDelay / GetGasSolnResponse.  This file keeps that global
+// state machine on the host (guarded by a mutex: the reference's library is not re-entrant either),
+// translates the keyword text into the typed ckmi_reactor_cfg, and runs the reactor as a batch of
+// one on the GPU kernels of ckmi.hip / ckmi_big.hip.  Per-state thermo / ROP calls stage their
+// state into a small device buffer of the chemistry set and run the batched kernels with n = 1.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/ckmi.h"
+#include "../../include/ckmi_kin.h"
+
+namespace {
+
+constexpr double RU = 1.3806504e-16 * 6.02214179e23;  // erg/mol-K (reference constants.py:37)
+constexpr int NAME_LEN = 16;                            // MAX_SPECIES_LENGTH - 1 (chemistry.py:41-43)
+constexpr int MAX_ADAP = 20000;                         // adaptive solution points per run
+
+thread_local std::string g_err;
+std::recursive_mutex g_mu;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+struct ChemSet {
+  ckmi_mech* mech = nullptr;
+  int device = 0, KK = 0, II = 0, MM = 0;
+  std::vector<double> wt, awt, thermo;  // thermo [KK][17] for the per-mass conversions
+  std::vector<int32_t> ncf;             // [MM][KK] row-major
+  std::vector<std::string> names, elements;
+  double* dbuf = nullptr;               // device scratch for single-state calls
+  size_t dbuf_n = 0;
+};
+std::vector<ChemSet*> g_sets;  // chemistry set id = index + 1
+int g_active = 0;
+
+ChemSet* get_set(const int* id) {
+  if (!id || *id < 1 || *id > (int)g_sets.size() || !g_sets[*id - 1]) return nullptr;
+  return g_sets[*id - 1];
+}
+
+struct Profile {
+  std::string key;
+  std::vector<double> x, y;
+};
+
+// the one configured 0-D reactor (KINAll0D_*), as in the reference's native library
+struct Reactor0D {
+  int chemset = 0, problem = 0, energy = 0;
+  bool setup = false, inputs = false;
+  double t_end = 0, T0 = 0, P0 = 0, V0 = 0, qloss = 0;
+  std::vector<double> Y0;
+  std::vector<std::pair<std::string, std::string>> kw;  // keyword, value text (in order)
+  std::vector<Profile> prof;
+  // results
+  bool done = false;
+  double tau = -1.0;
+  std::vector<double> t, T, P, V, Y;  // Y [npts][KK]
+};
+Reactor0D g_r;
+
+std::string upper(std::string s) {
+  for (char& c : s) c = (char)std::toupper((unsigned char)c);
+  return s;
+}
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+  return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+
+int hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) return fail(CKMI_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return CKMI_OK;
+}
+
+int ensure_scratch(ChemSet* s, size_t n) {
+  if (s->dbuf_n >= n) return CKMI_OK;
+  if (s->dbuf) (void)hipFree(s->dbuf);
+  s->dbuf = nullptr;
+  s->dbuf_n = 0;
+  int rc = hip_ok(hipMalloc((void**)&s->dbuf, n * sizeof(double)), "hipMalloc");
+  if (rc == CKMI_OK) s->dbuf_n = n;
+  return rc;
+}
+
+// cp/R, h/RT, s/R of every species at T on the device (ckmi_species_thermo, n = 1)
+int species_thermo(ChemSet* s, double T, std::vector<double>& cpR, std::vector<double>& hRT,
+                   std::vector<double>& sR) {
+  const int KK = s->KK;
+  int rc = ensure_scratch(s, 1 + 3 * (size_t)KK);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, &T, sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  rc = ckmi_species_thermo(s->mech, 1, s->dbuf, s->dbuf + 1, s->dbuf + 1 + KK, s->dbuf + 1 + 2 * KK, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  std::vector<double> out(3 * (size_t)KK);
+  if ((rc = hip_ok(hipMemcpy(out.data(), s->dbuf + 1, out.size() * sizeof(double), hipMemcpyDeviceToHost), "D2H")))
+    return rc;
+  cpR.assign(out.begin(), out.begin() + KK);
+  hRT.assign(out.begin() + KK, out.begin() + 2 * KK);
+  sR.assign(out.begin() + 2 * KK, out.end());
+  return CKMI_OK;
+}
+
+// wdot[KK], mixture cp and h (per mass) at one (T, P, Y) state (ckmi_rop_thermo, n = 1)
+int rop_state(ChemSet* s, double T, double P, const double* Y, double* wdot, double* cp, double* h) {
+  const int KK = s->KK;
+  int rc = ensure_scratch(s, 2 + 2 * (size_t)KK + 2);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  std::vector<double> in(2 + KK);
+  in[0] = T;
+  in[1] = P;
+  std::copy(Y, Y + KK, in.begin() + 2);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  double* o = s->dbuf + 2 + KK;
+  rc = ckmi_rop_thermo(s->mech, 1, s->dbuf, s->dbuf + 1, s->dbuf + 2, o, o + KK, o + KK + 1, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  std::vector<double> out(KK + 2);
+  if ((rc = hip_ok(hipMemcpy(out.data(), o, out.size() * sizeof(double), hipMemcpyDeviceToHost), "D2H"))) return rc;
+  if (wdot) std::copy(out.begin(), out.begin() + KK, wdot);
+  if (cp) *cp = out[KK];
+  if (h) *h = out[KK + 1];
+  return CKMI_OK;
+}
+
+std::vector<double> save_times(double t_end, double dtsv) {
+  // 0, dt, 2 dt, ... accumulated like the Python run() (batchreactor.py save_times), ending at t_end
+  std::vector<double> t{0.0};
+  double tc = 0.0;
+  while (tc + dtsv < t_end * (1.0 - 1e-12)) {
+    tc += dtsv;
+    t.push_back(tc);
+  }
+  t.push_back(t_end);
+  return t;
+}
+
+double value_of(const std::string& v, bool* ok) {
+  char* end = nullptr;
+  const double x = std::strtod(v.c_str(), &end);
+  *ok = end && end != v.c_str() && trim(std::string(end)).empty();
+  return x;
+}
+
+int species_index(const ChemSet* s, const std::string& name) {
+  const std::string u = upper(trim(name));
+  for (int k = 0; k < (int)s->names.size(); ++k)
+    if (upper(s->names[k]) == u) return k;
+  return -1;
+}
+
+// Keyword text (reactormodel.py:349-372: "KEY    value", or "KEY" for booleans) -> ckmi_reactor_cfg.
+// Unknown keywords are errors (the reference's library rejects what it does not know).
+int apply_keywords(const ChemSet* s, ckmi_reactor_cfg& c, double& dtsv, bool& adap) {
+  for (const auto& kv : g_r.kw) {
+    const std::string& k = kv.first;
+    const std::string& v = kv.second;
+    bool ok = true;
+    auto num = [&](double& dst) {
+      dst = value_of(v, &ok);
+      return ok;
+    };
+    double x = 0.0;
+    if (k == "ATOL") ok = num(c.atol);
+    else if (k == "RTOL") ok = num(c.rtol);
+    else if (k == "HO") ok = num(c.h0);
+    else if (k == "STPT") ok = num(c.hmax);
+    else if (k == "NNEG") c.nneg = 1;
+    else if (k == "TIFP") c.ign_mode = 1;
+    else if (k == "DTIGN") { c.ign_mode = 2; ok = num(c.ign_val); }
+    else if (k == "TLIM") { c.ign_mode = 3; ok = num(c.ign_val); }
+    else if (k == "KLIM") {
+      c.ign_mode = 4;
+      c.ign_species = species_index(s, v);
+      ok = c.ign_species >= 0;
+    } else if (k == "IGN_STOP") c.ign_stop = 1;
+    else if (k == "DTSV") ok = num(dtsv) && dtsv > 0.0;
+    else if (k == "DELT" || k == "VOL" || k == "AREA" || k == "NADAP" || k == "NO_SDOUTPUT_WRITE" ||
+             k == "NO_XMLOUTPUT_WRITE")
+      ok = v.empty() || num(x);  // print interval, volume / area (given by SetupBatchInputs), output files
+    else if (k == "ADAP") adap = true;
+    else if (k == "ASTEPS") { ok = num(x) && x >= 1.0; c.asteps = (int)x; }
+    else if (k == "AVAR") {
+      const std::string u = upper(trim(v));
+      c.avar = (u == "T" || u == "TEMP" || u == "TEMPERATURE") ? 0 : 1 + species_index(s, v);
+      ok = c.avar >= 0;
+    } else if (k == "AVALUE") ok = num(c.avalue);
+    else if (k == "GFAC") ok = num(c.gfac);
+    else if (k == "QLOS") ok = num(c.qloss);
+    else if (k == "HTC") ok = num(c.htc);
+    else if (k == "TAMB") ok = num(c.tamb);
+    else if (k == "AREAQ") ok = num(c.areaq);
+    else if (k == "MAXIT" || k == "NSTP") { ok = num(x) && x >= 1.0; c.max_steps = (int)x; }
+    else return fail(CKMI_ERR_UNSUPPORTED, "keyword " + k + " is not supported on the device path");
+    if (!ok) return fail(CKMI_ERR_ARG, "bad value for keyword " + k + ": '" + v + "'");
+  }
+  if (adap && c.asteps == 0 && c.avar < 0) c.asteps = 20;  // ADAP default ASTEPS (batchreactor.py:373-460)
+  if (!adap) c.asteps = 0, c.avar = -1;
+  return CKMI_OK;
+}
+
+int apply_profiles(ckmi_reactor_cfg& c) {
+  for (const Profile& p : g_r.prof) {
+    const int np = (int)p.x.size();
+    if (np < 1 || np > 64) return fail(CKMI_ERR_ARG, "profile " + p.key + " must have 1..64 points");
+    if (p.key == "VPRO" || p.key == "PPRO" || p.key == "TPRO") {
+      if (p.key == "VPRO" && g_r.problem != 2) return fail(CKMI_ERR_ARG, "VPRO needs a given-volume (CONV) reactor");
+      if (p.key == "PPRO" && g_r.problem != 1) return fail(CKMI_ERR_ARG, "PPRO needs a given-pressure (CONP) reactor");
+      if (p.key == "TPRO" && g_r.energy != 2) return fail(CKMI_ERR_ARG, "TPRO needs a fixed-temperature reactor");
+      c.nprof = np;
+      c.prof_kind = p.key == "TPRO" ? 1 : 0;
+      std::copy(p.x.begin(), p.x.end(), c.prof_t);
+      std::copy(p.y.begin(), p.y.end(), c.prof_v);
+    } else if (p.key == "QPRO" || p.key == "AEXT") {
+      if (c.nprof2 > 0) return fail(CKMI_ERR_UNSUPPORTED, "QPRO together with AEXT");
+      c.nprof2 = np;
+      c.prof2_kind = p.key == "QPRO" ? 1 : 2;
+      std::copy(p.x.begin(), p.x.end(), c.prof2_t);
+      std::copy(p.y.begin(), p.y.end(), c.prof2_v);
+    } else {
+      return fail(CKMI_ERR_UNSUPPORTED, "profile " + p.key + " is not supported on the device path");
+    }
+  }
+  return CKMI_OK;
+}
+
+double pwl(const std::vector<double>& x, const std::vector<double>& y, double t) {
+  if (t <= x.front()) return y.front();
+  if (t >= x.back()) return y.back();
+  size_t j = 0;
+  while (j + 2 < x.size() && t >= x[j + 1]) ++j;
+  return y[j] + (y[j + 1] - y[j]) / (x[j + 1] - x[j]) * (t - x[j]);
+}
+
+int run_reactor(ChemSet* s) {
+  const int KK = s->KK, n = KK + 1;
+  ckmi_reactor_cfg c;
+  std::memset(&c, 0, sizeof(c));
+  c.energy = g_r.energy;
+  c.t_end = g_r.t_end;
+  c.atol = 1.0e-12;  // the reference's defaults (batchreactor.py:91-92)
+  c.rtol = 1.0e-6;
+  c.tamb = 300.0;
+  c.gfac = 1.0;
+  c.avar = -1;
+  c.qloss = g_r.qloss;
+  double dtsv = g_r.t_end / 100.0;  // default DTSV (batchreactor.py:296)
+  bool adap = false;
+  int rc = apply_keywords(s, c, dtsv, adap);
+  if (!rc) rc = apply_profiles(c);
+  if (rc) return rc;
+  const std::vector<double> ts = save_times(g_r.t_end, dtsv);
+  const int nsave = (int)ts.size();
+  const int max_adap = adap ? MAX_ADAP : 0;
+  (void)hipSetDevice(s->device);
+  // device buffers: inputs, outputs, save grid, adaptive points
+  const size_t nd = 4 + KK + 4 + KK + 1 + nsave + (size_t)nsave * n + (adap ? (size_t)max_adap * (n + 1) : 0);
+  double* d = nullptr;
+  int32_t* di = nullptr;
+  if ((rc = hip_ok(hipMalloc((void**)&d, nd * sizeof(double)), "hipMalloc"))) return rc;
+  if ((rc = hip_ok(hipMalloc((void**)&di, (2 + CKMI_NSTAT) * sizeof(int32_t)), "hipMalloc"))) {
+    (void)hipFree(d);
+    return rc;
+  }
+  double *T0 = d, *P0 = d + 1, *V0 = d + 2, *Y0 = d + 4, *tau = Y0 + KK, *Te = tau + 1, *Pe = tau + 2, *Ve = tau + 3;
+  double *Ye = tau + 4, *tstop = Ye + KK, *tsv = tstop + 1, *ysv = tsv + nsave, *tad = ysv + (size_t)nsave * n;
+  double* yad = tad + max_adap;
+  int32_t *prob = di, *nad = di + 1, *stats = di + 2;
+  std::vector<double> hin(4 + KK, 0.0);
+  hin[0] = g_r.T0;
+  hin[1] = g_r.P0;
+  hin[2] = g_r.V0 > 0.0 ? g_r.V0 : 1.0;
+  std::copy(g_r.Y0.begin(), g_r.Y0.end(), hin.begin() + 4);
+  const int32_t pr = g_r.problem;
+  rc = hip_ok(hipMemcpy(d, hin.data(), hin.size() * sizeof(double), hipMemcpyHostToDevice), "H2D");
+  if (!rc) rc = hip_ok(hipMemcpy(tsv, ts.data(), ts.size() * sizeof(double), hipMemcpyHostToDevice), "H2D");
+  if (!rc) rc = hip_ok(hipMemcpy(prob, &pr, sizeof(int32_t), hipMemcpyHostToDevice), "H2D");
+  ckmi_reactor_ext ext;
+  std::memset(&ext, 0, sizeof(ext));
+  ext.t_stop = tstop;
+  if (adap) {
+    ext.max_adap = max_adap;
+    ext.t_adap = tad;
+    ext.y_adap = yad;
+    ext.n_adap = nad;
+  }
+  if (!rc) {
+    rc = ckmi_reactor_run_ex(s->mech, &c, 1, prob, T0, P0, V0, Y0, &ext, tau, Te, Pe, Ve, Ye, stats, nsave, tsv, ysv,
+                             nullptr);
+    if (rc) rc = fail(rc, ckmi_last_error());
+  }
+  if (!rc) rc = hip_ok(hipDeviceSynchronize(), "reactor run");
+  std::vector<double> out;
+  std::vector<int32_t> iout(2 + CKMI_NSTAT);
+  if (!rc) {
+    out.resize(nd - (4 + KK));
+    rc = hip_ok(hipMemcpy(out.data(), tau, out.size() * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+  }
+  if (!rc) rc = hip_ok(hipMemcpy(iout.data(), di, iout.size() * sizeof(int32_t), hipMemcpyDeviceToHost), "D2H");
+  (void)hipFree(d);
+  (void)hipFree(di);
+  if (rc) return rc;
+  const double* o = out.data();  // relative to tau
+  const int status = iout[2 + CKMI_STAT_STATUS];
+  g_r.tau = o[0];
+  const double t_stop = o[4 + KK];
+  // solution points: the DTSV grid up to the stop time (+ the final state of an early stop),
+  // merged with the adaptive points
+  std::vector<std::pair<double, std::vector<double>>> pts;
+  const double* ys = o + 4 + KK + 1 + nsave;
+  for (int i = 0; i < nsave; ++i) {
+    if (std::isnan(ys[(size_t)i * n])) continue;
+    pts.push_back({ts[i], std::vector<double>(ys + (size_t)i * n, ys + (size_t)(i + 1) * n)});
+  }
+  if (t_stop < ts.back() && (pts.empty() || t_stop > pts.back().first)) {
+    std::vector<double> yf(n);
+    yf[0] = o[1];
+    std::copy(o + 4, o + 4 + KK, yf.begin() + 1);
+    pts.push_back({t_stop, yf});
+  }
+  if (adap) {
+    const int na = iout[1];
+    const double* ta = ys + (size_t)nsave * n;
+    const double* ya = ta + max_adap;
+    for (int i = 0; i < na; ++i) {
+      if (ta[i] > t_stop) continue;
+      bool dup = false;
+      for (double x : ts) dup = dup || x == ta[i];
+      if (!dup) pts.push_back({ta[i], std::vector<double>(ya + (size_t)i * n, ya + (size_t)(i + 1) * n)});
+    }
+    std::stable_sort(pts.begin(), pts.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  }
+  // pressure and volume of every point (CONP: P given, V from the mass; CONV: V given, P from the EOS)
+  double sw0 = 0.0;
+  for (int k = 0; k < KK; ++k) sw0 += g_r.Y0[k] / s->wt[k];
+  const Profile* pp = nullptr;
+  for (const Profile& p : g_r.prof)
+    if ((g_r.problem == 1 && p.key == "PPRO") || (g_r.problem == 2 && p.key == "VPRO")) pp = &p;
+  const double Vs = (g_r.problem == 2 && pp) ? pp->y.front() : hin[2];
+  const double rho0 = g_r.P0 / (RU * g_r.T0 * sw0);
+  g_r.t.clear(), g_r.T.clear(), g_r.P.clear(), g_r.V.clear(), g_r.Y.clear();
+  for (const auto& pt : pts) {
+    const double t = pt.first, T = pt.second[0];
+    double sw = 0.0;
+    for (int k = 0; k < KK; ++k) sw += pt.second[1 + k] / s->wt[k];
+    double P, V;
+    if (g_r.problem == 1) {
+      P = pp ? pwl(pp->x, pp->y, t) : g_r.P0;
+      V = rho0 * Vs / (P / (RU * T * sw));
+    } else {
+      V = pp ? pwl(pp->x, pp->y, t) : Vs;
+      P = (rho0 * Vs / V) * RU * T * sw;
+    }
+    g_r.t.push_back(t);
+    g_r.T.push_back(T);
+    g_r.P.push_back(P);
+    g_r.V.push_back(V);
+    g_r.Y.insert(g_r.Y.end(), pt.second.begin() + 1, pt.second.end());
+  }
+  g_r.done = true;
+  if (status != CKMI_RUN_OK)
+    return fail(100 + status, "reactor integration failed (status " + std::to_string(status) + ")");
+  return CKMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ckmi_kin_last_error(void) { return g_err.c_str(); }
+
+int ckmi_kin_register(const ckmi_mech_desc* desc, int32_t MM, const char* names, const char* elements,
+                      const double* awt, const int32_t* ncf, int32_t* chemset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!desc || !chemset || MM < 0) return fail(CKMI_ERR_ARG, "null argument");
+  auto* s = new ChemSet();
+  int rc = ckmi_mech_create(desc, &s->mech);
+  if (rc) {
+    delete s;
+    return fail(rc, ckmi_last_error());
+  }
+  (void)hipGetDevice(&s->device);
+  s->KK = desc->KK;
+  s->II = desc->II;
+  s->wt.assign(desc->wt, desc->wt + desc->KK);
+  s->thermo.assign(desc->thermo, desc->thermo + 17 * (size_t)desc->KK);
+  s->MM = (awt && ncf) ? MM : 0;
+  if (s->MM) {
+    s->awt.assign(awt, awt + MM);
+    s->ncf.assign(ncf, ncf + (size_t)MM * desc->KK);
+  }
+  for (int k = 0; names && k < s->KK; ++k) s->names.emplace_back(trim(std::string(names + NAME_LEN * k, strnlen(names + NAME_LEN * k, NAME_LEN))));
+  for (int m = 0; elements && m < MM; ++m)
+    s->elements.emplace_back(trim(std::string(elements + NAME_LEN * m, strnlen(elements + NAME_LEN * m, NAME_LEN))));
+  g_sets.push_back(s);
+  *chemset = (int32_t)g_sets.size();
+  g_active = *chemset;
+  return CKMI_OK;
+}
+
+int ckmi_kin_release(int32_t chemset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(&chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  if (s->dbuf) (void)hipFree(s->dbuf);
+  ckmi_mech_destroy(s->mech);
+  delete s;
+  g_sets[chemset - 1] = nullptr;
+  return CKMI_OK;
+}
+
+int KINSetUnitSystem(int* code) {
+  if (!code || *code != 1) return fail(CKMI_ERR_UNSUPPORTED, "only the cgs unit system (1) is supported");
+  return CKMI_OK;
+}
+
+int KINInitialize(int* chemset, int* flag) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)flag;
+  if (!get_set(chemset)) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  g_active = *chemset;
+  return CKMI_OK;
+}
+
+void KINFinish(void) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  g_r = Reactor0D();
+}
+
+int KINUpdateChemistrySet(int* chemset) { return KINInitialize(chemset, nullptr); }
+int KINSwitchChemistrySet(int* chemset) { return KINInitialize(chemset, nullptr); }
+
+int KINGetChemistrySizes(int* chemset, int* MM, int* KK, int* II, int* nmat, int* nsite, int* nbulk, int* nphase,
+                         int* nsurfrxn) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  if (MM) *MM = s->MM;
+  if (KK) *KK = s->KK;
+  if (II) *II = s->II;
+  if (nmat) *nmat = 1;  // gas phase only (no surface chemistry on this path)
+  if (nsite) *nsite = 0;
+  if (nbulk) *nbulk = 0;
+  if (nphase) *nphase = 1;
+  if (nsurfrxn) *nsurfrxn = 0;
+  return CKMI_OK;
+}
+
+static int copy_names(const std::vector<std::string>& v, char** out) {
+  if (!out) return fail(CKMI_ERR_ARG, "null name buffers");
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (!out[i]) return fail(CKMI_ERR_ARG, "null name buffer");
+    std::memset(out[i], 0, NAME_LEN + 1);
+    std::memcpy(out[i], v[i].c_str(), std::min<size_t>(v[i].size(), NAME_LEN));
+  }
+  return CKMI_OK;
+}
+
+int KINGetGasSpeciesNames(int* chemset, char** names) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  if ((int)s->names.size() != s->KK) return fail(CKMI_ERR_ARG, "species names were not registered");
+  return copy_names(s->names, names);
+}
+
+int KINGetElementNames(int* chemset, char** names) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  if ((int)s->elements.size() != s->MM) return fail(CKMI_ERR_ARG, "element names were not registered");
+  return copy_names(s->elements, names);
+}
+
+int KINGetAtomicWeights(int* chemset, double* awt) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !awt) return fail(CKMI_ERR_ARG, "bad argument");
+  std::copy(s->awt.begin(), s->awt.end(), awt);
+  return CKMI_OK;
+}
+
+int KINGetGasMolecularWeights(int* chemset, double* wt) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !wt) return fail(CKMI_ERR_ARG, "bad argument");
+  std::copy(s->wt.begin(), s->wt.end(), wt);
+  return CKMI_OK;
+}
+
+int KINGetGasSpeciesComposition(int* chemset, int32_t* ncf) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !ncf) return fail(CKMI_ERR_ARG, "bad argument");
+  for (int m = 0; m < s->MM; ++m)
+    for (int k = 0; k < s->KK; ++k) ncf[m + (size_t)s->MM * k] = s->ncf[(size_t)m * s->KK + k];  // F-order [MM, KK]
+  return CKMI_OK;
+}
+
+// per-mass species properties from the device NASA-7 kernel
+static int species_per_mass(int* chemset, double* T, double* out, int which) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !out || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  std::vector<double> cpR, hRT, sR;
+  int rc = species_thermo(s, *T, cpR, hRT, sR);
+  if (rc) return rc;
+  for (int k = 0; k < s->KK; ++k) {
+    const double r = RU / s->wt[k];
+    out[k] = which == 0 ? cpR[k] * r : (which == 1 ? hRT[k] * r * *T : (hRT[k] - 1.0) * r * *T);
+  }
+  return CKMI_OK;
+}
+
+int KINGetGasSpecificHeat(int* chemset, double* T, double* cp) { return species_per_mass(chemset, T, cp, 0); }
+int KINGetGasSpeciesEnthalpy(int* chemset, double* T, double* h) { return species_per_mass(chemset, T, h, 1); }
+int KINGetGasSpeciesInternalEnergy(int* chemset, double* T, double* u) { return species_per_mass(chemset, T, u, 2); }
+
+int KINGetMassDensity(int* chemset, double* T, double* P, double* Y, double* rho) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !P || !Y || !rho || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  double sw = 0.0;
+  for (int k = 0; k < s->KK; ++k) sw += Y[k] / s->wt[k];
+  *rho = *P / (RU * *T * sw);  // ideal-gas EOS (the only EOS of this path)
+  return CKMI_OK;
+}
+
+int KINGetGasMixtureSpecificHeat(int* chemset, double* T, double* Y, double* cp) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !Y || !cp || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  return rop_state(s, *T, 1.01325e6, Y, nullptr, cp, nullptr);
+}
+
+int KINGetGasMixtureEnthalpy(int* chemset, double* T, double* Y, double* h) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !Y || !h || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  return rop_state(s, *T, 1.01325e6, Y, nullptr, nullptr, h);
+}
+
+int KINGetGasROP(int* chemset, double* T, double* P, double* Y, double* wdot) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !P || !Y || !wdot || !(*T > 0.0) || !(*P > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  return rop_state(s, *T, *P, Y, wdot, nullptr, nullptr);
+}
+
+int KINGetGasReactionRates(int* chemset, double* T, double* P, double* Y, double* qf, double* qr) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !P || !Y || !qf || !qr || !(*T > 0.0) || !(*P > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  const int KK = s->KK, II = s->II;
+  int rc = ensure_scratch(s, 2 + (size_t)KK + 2 * (size_t)II);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  std::vector<double> in(2 + KK);
+  in[0] = *T;
+  in[1] = *P;
+  std::copy(Y, Y + KK, in.begin() + 2);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  double* o = s->dbuf + 2 + KK;
+  rc = ckmi_reaction_rates(s->mech, 1, s->dbuf, s->dbuf + 1, s->dbuf + 2, o, o + II, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  if ((rc = hip_ok(hipMemcpy(qf, o, II * sizeof(double), hipMemcpyDeviceToHost), "D2H"))) return rc;
+  return hip_ok(hipMemcpy(qr, o + II, II * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+}
+
+int KINGetReactionRateParameters(int* chemset, double* A, double* b, double* E_R) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  const int rc = ckmi_get_arrhenius(s->mech, A, b, E_R);
+  return rc ? fail(rc, ckmi_last_error()) : CKMI_OK;
+}
+
+int KINSetAFactorForAReaction(int* chemset, int* irxn, double* A) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !irxn || !A || *irxn == 0 || std::abs(*irxn) > s->II) return fail(CKMI_ERR_ARG, "bad reaction index");
+  if (*irxn > 0) {  // get (1-based)
+    std::vector<double> a(s->II);
+    const int rc = ckmi_get_arrhenius(s->mech, a.data(), nullptr, nullptr);
+    if (rc) return fail(rc, ckmi_last_error());
+    *A = a[*irxn - 1];
+    return CKMI_OK;
+  }
+  (void)hipSetDevice(s->device);
+  const int rc = ckmi_set_afactor(s->mech, -*irxn - 1, *A);  // negative index: put (chemistry.py:1660-1667)
+  return rc ? fail(rc, ckmi_last_error()) : CKMI_OK;
+}
+
+int KINAll0D_Setup(int* chemset, int* reactortype, int* problem, int* energy, int* solver, int* npsr,
+                   int32_t* ninlets, int* nzones) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)npsr, (void)ninlets, (void)nzones;
+  if (!get_set(chemset)) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  if (!reactortype || *reactortype != 1) return fail(CKMI_ERR_UNSUPPORTED, "only closed batch reactors (type 1)");
+  if (!solver || *solver != 1) return fail(CKMI_ERR_UNSUPPORTED, "only the transient solver (1)");
+  if (!problem || (*problem != 1 && *problem != 2)) return fail(CKMI_ERR_ARG, "problem must be 1 (CONP) or 2 (CONV)");
+  if (!energy || (*energy != 1 && *energy != 2)) return fail(CKMI_ERR_ARG, "energy must be 1 (ENRG) or 2 (TGIV)");
+  g_r = Reactor0D();
+  g_r.chemset = *chemset;
+  g_r.problem = *problem;
+  g_r.energy = *energy;
+  g_r.setup = true;
+  return CKMI_OK;
+}
+
+int KINAll0D_SetupWorkArrays(int* lout, int* chemset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)lout;
+  if (!get_set(chemset)) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  return CKMI_OK;  // device work arrays are allocated per run
+}
+
+int KINAll0D_SetupBatchInputs(int* chemset, double* t_end, double* T, double* P, double* V, double* qloss,
+                              double* area, double* Y, double* site, double* bulk) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)area, (void)site, (void)bulk;  // reactive surface area, site / bulk fractions: no surface chemistry
+  ChemSet* s = get_set(chemset);
+  if (!s || !g_r.setup || *chemset != g_r.chemset) return fail(CKMI_ERR_ARG, "KINAll0D_Setup first");
+  if (!t_end || !T || !P || !Y || !(*t_end > 0.0) || !(*T > 0.0) || !(*P > 0.0))
+    return fail(CKMI_ERR_ARG, "TIME, temperature and pressure must be > 0");
+  g_r.t_end = *t_end;
+  g_r.T0 = *T;
+  g_r.P0 = *P;
+  g_r.V0 = V ? *V : 0.0;
+  g_r.qloss = qloss ? *qloss : 0.0;
+  g_r.Y0.assign(Y, Y + s->KK);
+  g_r.kw.clear();
+  g_r.prof.clear();
+  g_r.inputs = true;
+  g_r.done = false;
+  return CKMI_OK;
+}
+
+int KINAll0D_IntegrateHeatRelease(void) { return CKMI_OK; }  // QRGEQ output: not produced (no KINAll0D_GetHeatRelease)
+
+int KINAll0D_SetProfilePoints(int* npoints) {
+  if (!npoints || *npoints < 0) return fail(CKMI_ERR_ARG, "bad profile size");
+  return CKMI_OK;
+}
+
+int KINAll0D_SetProfileParameter(char* key, int* npoints, double* x, double* y) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_r.inputs) return fail(CKMI_ERR_ARG, "KINAll0D_SetupBatchInputs first");
+  if (!key || !npoints || *npoints < 1 || *npoints > 64 || !x || !y) return fail(CKMI_ERR_ARG, "bad profile");
+  Profile p;
+  p.key = upper(trim(key));
+  p.x.assign(x, x + *npoints);
+  p.y.assign(y, y + *npoints);
+  for (auto& q : g_r.prof)
+    if (q.key == p.key) {
+      q = p;
+      return CKMI_OK;
+    }
+  g_r.prof.push_back(p);
+  return CKMI_OK;
+}
+
+int KINAll0D_SetUserKeyword(char* line) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_r.inputs) return fail(CKMI_ERR_ARG, "KINAll0D_SetupBatchInputs first");
+  if (!line) return fail(CKMI_ERR_ARG, "null keyword line");
+  std::string s = trim(line);
+  if (s.empty() || s[0] == '!') return CKMI_OK;  // '!' disables a keyword (reactormodel.py:341-372)
+  std::istringstream is(s);
+  std::string key, value, rest;
+  is >> key;
+  std::getline(is, rest);
+  value = trim(rest);
+  g_r.kw.push_back({upper(key), value});
+  return CKMI_OK;
+}
+
+int KINAll0D_Calculate(int* chemset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !g_r.inputs || *chemset != g_r.chemset) return fail(CKMI_ERR_ARG, "reactor is not set up");
+  g_r.done = false;
+  return run_reactor(s);
+}
+
+int KINAll0D_GetIgnitionDelay(double* tau) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!tau || !g_r.done) return fail(CKMI_ERR_ARG, "no completed run");
+  *tau = g_r.tau;
+  return CKMI_OK;
+}
+
+int KINAll0D_GetSolnResponseSize(int* nreac, int* npts) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!nreac || !npts || !g_r.done) return fail(CKMI_ERR_ARG, "no completed run");
+  *nreac = 1;
+  *npts = (int)g_r.t.size();
+  return CKMI_OK;
+}
+
+int KINAll0D_GetGasSolnResponse(int* nreac, int* npts, int* KK, double* t, double* T, double* P, double* V,
+                                double* Y) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_r.done) return fail(CKMI_ERR_ARG, "no completed run");
+  const int np = (int)g_r.t.size();
+  ChemSet* s = get_set(&g_r.chemset);
+  if (!nreac || *nreac != 1 || !npts || *npts != np || !KK || !s || *KK != s->KK)
+    return fail(CKMI_ERR_SIZE, "solution size mismatch (KINAll0D_GetSolnResponseSize)");
+  for (int i = 0; i < np; ++i) {
+    if (t) t[i] = g_r.t[i];
+    if (T) T[i] = g_r.T[i];
+    if (P) P[i] = g_r.P[i];
+    if (V) V[i] = g_r.V[i];
+    for (int k = 0; Y && k < s->KK; ++k) Y[k + (size_t)s->KK * i] = g_r.Y[(size_t)i * s->KK + k];  // [KK, npts] F-order
+  }
+  return CKMI_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,215 @@
+"""The reference's KIN call sequences on libckmi.so, through the KIN-compatible C ABI only.
+
+Every call here goes through ctypes with the reference's prototypes (pychemkin_amd.kin, restated
+from chemkin_wrapper.py) the way mixture.py / chemistry.py / batchreactor.py make them: scalars by
+pointer, host numpy arrays, int return.  The goldens are the reference's own example outputs."""
+import ctypes as ct
+
+import numpy as np
+import pytest
+
+from conftest import P_ATM, golden, h2_air_Y, within
+
+pytestmark = pytest.mark.gpu
+
+RU = 1.3806504e-16 * 6.02214179e23
+
+
+@pytest.fixture(scope="module")
+def K(mech):
+    from pychemkin_amd import kin
+
+    L = kin.bind()
+    cs = kin.register(mech)
+    yield L, ct.c_int(cs)
+    kin.release(cs)
+
+
+def _nasa(tables, T):
+    th = np.asarray(tables["thermo"])
+    a = np.where((T > th[:, 1])[:, None], th[:, 10:17], th[:, 3:10])
+    cpR = a[:, 0] + T * (a[:, 1] + T * (a[:, 2] + T * (a[:, 3] + T * a[:, 4])))
+    hRT = a[:, 0] + T * (a[:, 1] / 2 + T * (a[:, 2] / 3 + T * (a[:, 3] / 4 + T * a[:, 4] / 5))) + a[:, 5] / T
+    return cpR, hRT
+
+
+def test_sizes_and_tables(K, mech):
+    L, cs = K
+    s = [ct.c_int(-1) for _ in range(8)]
+    assert L.KINGetChemistrySizes(ct.byref(cs), *[ct.byref(x) for x in s]) == 0
+    assert [s[0].value, s[1].value, s[2].value] == [mech.MM, mech.KK, mech.II]
+    buf = (ct.POINTER(ct.c_char) * mech.KK)()
+    for i in range(mech.KK):
+        buf[i] = ct.create_string_buffer(17)  # MAX_SPECIES_LENGTH (chemistry.py:42)
+    assert L.KINGetGasSpeciesNames(ct.byref(cs), ct.cast(buf, ct.POINTER(ct.POINTER(ct.c_char)))) == 0
+    names = [ct.cast(buf[i], ct.c_char_p).value.decode() for i in range(mech.KK)]
+    assert names == mech.species
+    wt = np.zeros(mech.KK)
+    assert L.KINGetGasMolecularWeights(ct.byref(cs), wt) == 0
+    assert np.array_equal(wt, mech.wt)
+    awt = np.zeros(mech.MM)
+    assert L.KINGetAtomicWeights(ct.byref(cs), awt) == 0
+    assert np.array_equal(awt, np.asarray(mech.awt))
+    ncf = np.zeros((mech.MM, mech.KK), dtype=np.int32, order="F")
+    assert L.KINGetGasSpeciesComposition(ct.byref(cs), ncf) == 0
+    assert np.array_equal(ncf, mech.ncf)
+
+
+@pytest.mark.parametrize("T", [300.0, 999.0, 1000.0, 2500.0])
+def test_species_thermo_per_mass(K, mech, tables, T):
+    L, cs = K
+    cp, h, u = (np.zeros(mech.KK) for _ in range(3))
+    t = ct.c_double(T)
+    assert L.KINGetGasSpecificHeat(ct.byref(cs), ct.byref(t), cp) == 0
+    assert L.KINGetGasSpeciesEnthalpy(ct.byref(cs), ct.byref(t), h) == 0
+    assert L.KINGetGasSpeciesInternalEnergy(ct.byref(cs), ct.byref(t), u) == 0
+    cpR, hRT = _nasa(tables, T)
+    r = RU / mech.wt
+    assert np.allclose(cp, cpR * r, rtol=1e-12, atol=0)
+    assert np.allclose(h, hRT * r * T, rtol=1e-11, atol=1e-3)
+    assert np.allclose(u, h - r * T, rtol=1e-11, atol=1e-3)
+
+
+def test_density_and_mixture_thermo(K, mech, tables):
+    L, cs = K
+    Y = np.ascontiguousarray(h2_air_Y(mech))
+    T, P = ct.c_double(1234.5), ct.c_double(3.0 * P_ATM)
+    rho, cp, h = ct.c_double(0), ct.c_double(0), ct.c_double(0)
+    assert L.KINGetMassDensity(ct.byref(cs), ct.byref(T), ct.byref(P), Y, ct.byref(rho)) == 0
+    assert abs(rho.value / (3.0 * P_ATM / (RU * 1234.5 * np.sum(Y / mech.wt))) - 1) < 1e-14
+    assert L.KINGetGasMixtureSpecificHeat(ct.byref(cs), ct.byref(T), Y, ct.byref(cp)) == 0
+    assert L.KINGetGasMixtureEnthalpy(ct.byref(cs), ct.byref(T), Y, ct.byref(h)) == 0
+    cpR, hRT = _nasa(tables, 1234.5)
+    assert abs(cp.value / np.sum(Y * cpR * RU / mech.wt) - 1) < 1e-12
+    assert abs(h.value / np.sum(Y * hRT * RU * 1234.5 / mech.wt) - 1) < 1e-11
+
+
+def test_rop_and_rates_match_batched_kernels(K, mech, tables, oracle):
+    from pychemkin_amd import _native
+
+    L, cs = K
+    dm = _native.DeviceMechanism(tables)
+    rng = np.random.default_rng(3)
+    for T_, P_ in ((1500.0, P_ATM), (900.0, 20 * P_ATM)):
+        Y = rng.random(mech.KK)
+        Y /= Y.sum()
+        T, P = ct.c_double(T_), ct.c_double(P_)
+        wdot = np.zeros(mech.KK)
+        qf, qr = np.zeros(mech.II), np.zeros(mech.II)
+        assert L.KINGetGasROP(ct.byref(cs), ct.byref(T), ct.byref(P), Y, wdot) == 0
+        assert L.KINGetGasReactionRates(ct.byref(cs), ct.byref(T), ct.byref(P), Y, qf, qr) == 0
+        w_b, _, _ = dm.rop_thermo([T_], [P_], Y[:, None])
+        qf_b, qr_b = dm.reaction_rates([T_], [P_], Y[:, None])
+        assert np.array_equal(wdot, w_b.cpu().numpy()[:, 0])  # same kernel, batch of one
+        assert np.array_equal(qf, qf_b.cpu().numpy()[:, 0]) and np.array_equal(qr, qr_b.cpu().numpy()[:, 0])
+        w_o = oracle.rates(T_, P_, Y)[2]
+        scale = np.max(np.abs(w_o))
+        assert np.max(np.abs(wdot - w_o)) <= 1e-9 * scale
+
+
+def test_afactor_get_put_and_rate_parameters(K, mech):
+    L, cs = K
+    A, b, E = (np.zeros(mech.II) for _ in range(3))
+    assert L.KINGetReactionRateParameters(ct.byref(cs), A, b, E) == 0
+    i = 37
+    a = ct.c_double(0.0)
+    assert L.KINSetAFactorForAReaction(ct.byref(cs), ct.byref(ct.c_int(i + 1)), ct.byref(a)) == 0
+    assert a.value == A[i]
+    a2 = ct.c_double(2.5 * A[i])
+    assert L.KINSetAFactorForAReaction(ct.byref(cs), ct.byref(ct.c_int(-(i + 1))), ct.byref(a2)) == 0
+    chk = ct.c_double(0.0)
+    assert L.KINSetAFactorForAReaction(ct.byref(cs), ct.byref(ct.c_int(i + 1)), ct.byref(chk)) == 0
+    assert abs(chk.value / (2.5 * A[i]) - 1) < 1e-14
+    a0 = ct.c_double(A[i])
+    assert L.KINSetAFactorForAReaction(ct.byref(cs), ct.byref(ct.c_int(-(i + 1))), ct.byref(a0)) == 0
+    assert L.KINSetAFactorForAReaction(ct.byref(cs), ct.byref(ct.c_int(mech.II + 1)), ct.byref(chk)) != 0
+
+
+def _setup(L, cs, problem, energy, t_end, T, P, V, Y):
+    assert L.KINAll0D_Setup(ct.byref(cs), ct.byref(ct.c_int(1)), ct.byref(ct.c_int(problem)),
+                            ct.byref(ct.c_int(energy)), ct.byref(ct.c_int(1)), ct.byref(ct.c_int(1)),
+                            np.zeros(1, np.int32), ct.byref(ct.c_int(0))) == 0
+    assert L.KINAll0D_SetupWorkArrays(ct.byref(ct.c_int(6)), ct.byref(cs)) == 0
+    z = np.zeros(1)
+    assert L.KINAll0D_SetupBatchInputs(ct.byref(cs), ct.byref(ct.c_double(t_end)), ct.byref(ct.c_double(T)),
+                                       ct.byref(ct.c_double(P)), ct.byref(ct.c_double(V)), ct.byref(ct.c_double(0)),
+                                       ct.byref(ct.c_double(0)), np.ascontiguousarray(Y), z, z) == 0
+    if energy == 1:
+        assert L.KINAll0D_IntegrateHeatRelease() == 0
+
+
+def _solution(L, KK):
+    nr, npt = ct.c_int(0), ct.c_int(0)
+    assert L.KINAll0D_GetSolnResponseSize(ct.byref(nr), ct.byref(npt)) == 0
+    n = npt.value
+    t, T, P, V = (np.zeros(n) for _ in range(4))
+    Y = np.zeros((KK, n), order="F")
+    assert L.KINAll0D_GetGasSolnResponse(ct.byref(nr), ct.byref(npt), ct.byref(ct.c_int(KK)), t, T, P, V, Y) == 0
+    return t, T, P, V, Y
+
+
+def test_h2_golden_through_kin_calls(K, mech):
+    """closed_homogeneous__transient.py:61-131 as the reference's batchreactor.py drives the native
+    library (__process_keywords :980-1147, __run_model :1149-1159, solution :1297-1410)."""
+    L, cs = K
+    g = golden("closed_homogeneous__transient")
+    _setup(L, cs, 1, 1, 5e-4, 1000.0, P_ATM, 1.0, h2_air_Y(mech))
+    for line in ("ATOL    1e-20", "RTOL    1e-08", "NNEG", "DTSV    5e-06", "DTIGN    400", "!ADAP", "NADAP"):
+        assert L.KINAll0D_SetUserKeyword(line.encode()) == 0, line
+    assert L.KINAll0D_Calculate(ct.byref(cs)) == 0, L.ckmi_kin_last_error()
+    tau = ct.c_double(0.0)
+    assert L.KINAll0D_GetIgnitionDelay(ct.byref(tau)) == 0
+    t, T, P, V, Y = _solution(L, mech.KK)
+    assert t.tolist() == g["state-time"]
+    Tg = np.asarray(g["state-temperature"])
+    assert within(T, Tg, *g["tolerance-var"]).sum() >= 90
+    assert abs(T[-1] / Tg[-1] - 1) < 2e-5
+    assert abs(tau.value / np.interp(1400.0, Tg, t) - 1) < 2e-3
+    assert np.allclose(P, P_ATM, rtol=1e-14)
+    rho = P / (RU * T * (Y / mech.wt[:, None]).sum(axis=0))
+    assert np.all(np.abs(rho / np.asarray(g["state-density"]) - 1) < 2e-3)
+    assert np.allclose(Y.sum(axis=0), 1.0, atol=1e-10)
+
+
+def test_conv_volume_profile_golden_through_kin_calls(K, mech, chem, oracle):
+    """CONV.py:62-140: CONV + ENERGY with a VPRO profile, TIFP ignition."""
+    import pychemkin_amd as ck
+
+    L, cs = K
+    g = golden("CONV")
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    m = ck.Mixture(chem)
+    m.X_by_Equivalence_Ratio(chem, fuel.X, air.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"], 0.7)
+    _setup(L, cs, 2, 1, 0.1, 800.0, 3 * P_ATM, 10.0, m.Y)
+    x, v = np.array([0.0, 0.01, 2.0]), np.array([10.0, 4.0, 4.0])
+    assert L.KINAll0D_SetProfileParameter(b"VPRO", ct.byref(ct.c_int(3)), x, v) == 0
+    for line in ("ATOL    1e-10", "RTOL    1e-08", "NNEG", "DTSV    0.01", "TIFP"):
+        assert L.KINAll0D_SetUserKeyword(line.encode()) == 0, line
+    assert L.KINAll0D_Calculate(ct.byref(cs)) == 0, L.ckmi_kin_last_error()
+    t, T, P, V, Y = _solution(L, mech.KK)
+    assert np.all(within(T, g["state-temperature"], *g["tolerance-var"]))
+    assert np.allclose(V, np.interp(t, x, v), rtol=1e-14)
+    tau = ct.c_double(0.0)
+    assert L.KINAll0D_GetIgnitionDelay(ct.byref(tau)) == 0
+    res, _ = oracle.reactor(800.0, 3 * P_ATM, 10.0, m.Y, problem=2, energy=1, t_end=0.1, atol=1e-10, rtol=1e-8,
+                            nneg=True, ign_mode="TIFP", profile=(x, v))
+    assert abs(tau.value / res.tau - 1) < 1e-6
+
+
+def test_unknown_and_unsupported_keywords_fail(K, mech):
+    L, cs = K
+    _setup(L, cs, 1, 1, 1e-3, 1200.0, P_ATM, 1.0, h2_air_Y(mech))
+    assert L.KINAll0D_SetUserKeyword(b"BOGUS    3") == 0  # stored; rejected by Calculate
+    assert L.KINAll0D_Calculate(ct.byref(cs)) != 0
+    assert b"BOGUS" in L.ckmi_kin_last_error()
+    _setup(L, cs, 1, 1, 1e-3, 1200.0, P_ATM, 1.0, h2_air_Y(mech))
+    assert L.KINAll0D_SetUserKeyword(b"ATOL    abc") == 0
+    assert L.KINAll0D_Calculate(ct.byref(cs)) != 0
+    _setup(L, cs, 1, 1, 1e-3, 1200.0, P_ATM, 1.0, h2_air_Y(mech))
+    x = np.array([0.0, 1.0])
+    assert L.KINAll0D_SetProfileParameter(b"VPRO", ct.byref(ct.c_int(2)), x, x + 1) == 0
+    assert L.KINAll0D_Calculate(ct.byref(cs)) != 0  # VPRO on a CONP reactor
+    assert b"VPRO" in L.ckmi_kin_last_error()
