@@ -63,7 +63,9 @@ int KINGetGasMixtureEnthalpy(int* chemset, double* T, double* Y, double* h);    
 
 /* ---- kinetics (:482-511) */
 int KINGetGasROP(int* chemset, double* T, double* P, double* Y, double* wdot);  /* :482-489, mol/cm3-s [KK] */
-int KINGetGasReactionRates(int* chemset, double* T, double* P, double* Y, double* qf, double* qr); /* :490-498 */
+/* :490-498.  The composition is read as MOLE fractions (Chemkin CKKFKR convention; what the closed
+ * library does, as reactionrates.baseline shows -- see DESIGN.md "reaction rates golden"). */
+int KINGetGasReactionRates(int* chemset, double* T, double* P, double* X, double* qf, double* qr);
 int KINGetReactionRateParameters(int* chemset, double* A, double* b, double* E_R); /* :499-505 */
 int KINSetAFactorForAReaction(int* chemset, int* irxn, double* A);              /* :506-511: irxn > 0 get, < 0 put */
 

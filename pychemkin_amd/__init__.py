@@ -28,7 +28,8 @@ from .constants import (
     air,
 )
 from .logger import logger
-from .mixture import Mixture, interpolate_mixtures
+from .mixture import (Mixture, adiabatic_mixing, calculate_mixture_temperature_from_enthalpy, interpolate_mixtures,
+                      isothermal_mixing)
 from .reactormodel import Keyword, Profile
 
 __version__ = "0.1.0"

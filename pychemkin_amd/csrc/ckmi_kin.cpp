@@ -571,10 +571,18 @@ int KINGetGasReactionRates(int* chemset, double* T, double* P, double* Y, double
   int rc = ensure_scratch(s, 2 + (size_t)KK + 2 * (size_t)II);
   if (rc) return rc;
   (void)hipSetDevice(s->device);
+  // The composition argument of this entry point is read as MOLE fractions, like Chemkin's CKKFKR
+  // (P, T, X): the reference's golden (reactionrates.baseline) is reproduced to 1e-14 that way and
+  // misses by up to 1.8x when the array is read as mass fractions -- although mixture.py:1540
+  // passes mass fractions.  Drop-in means the same numbers, so the convention is kept here; the
+  // batched ckmi_reaction_rates takes mass fractions.
   std::vector<double> in(2 + KK);
   in[0] = *T;
   in[1] = *P;
-  std::copy(Y, Y + KK, in.begin() + 2);
+  double sxw = 0.0;
+  for (int k = 0; k < KK; ++k) sxw += Y[k] * s->wt[k];
+  if (!(sxw > 0.0)) return fail(CKMI_ERR_ARG, "composition sums to zero");
+  for (int k = 0; k < KK; ++k) in[2 + k] = Y[k] * s->wt[k] / sxw;
   if ((rc = hip_ok(hipMemcpy(s->dbuf, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
   double* o = s->dbuf + 2 + KK;
   rc = ckmi_reaction_rates(s->mech, 1, s->dbuf, s->dbuf + 1, s->dbuf + 2, o, o + II, nullptr);

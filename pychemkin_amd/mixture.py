@@ -242,9 +242,21 @@ class Mixture:
         """Species molar rates of production [mol/cm3-s] (KINGetGasROP, mixture.py:1693-1746)."""
         return self._rop_thermo()[0]
 
-    def RxnRates(self) -> Tuple[np.ndarray, np.ndarray]:
-        """Forward and reverse rates of progress [mol/cm3-s] (KINGetGasReactionRates)."""
+    def RxnRates(self, reference_compat: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+        """Forward and reverse rates of progress [mol/cm3-s] (KINGetGasReactionRates, mixture.py:1748-1810).
+
+        reference_compat (default) returns what the reference returns: its Mixture.reaction_rates
+        hands the mass fractions to KINGetGasReactionRates (mixture.py:1540), which reads its
+        composition argument as mole fractions (Chemkin CKKFKR convention), so the rates belong to
+        the state whose mole fractions equal this mixture's mass fractions.  The reactionrates
+        golden is reproduced to 1e-14 that way (tests/test_oracle_golden.py).  False gives the rates
+        of this mixture's own composition (consistent with ROP())."""
         dm, T, P, Y = self._state_tensors()
+        if reference_compat:
+            import torch
+
+            y = self.Y * self._WT
+            Y = torch.as_tensor((y / y.sum()).reshape(self._KK, 1), dtype=torch.float64, device=dm.device)
         qf, qr = dm.reaction_rates(T, P, Y)
         return qf[:, 0].cpu().numpy(), qr[:, 0].cpu().numpy()
 
@@ -350,3 +362,75 @@ def interpolate_mixtures(mixtureleft: Mixture, mixtureright: Mixture, ratio: flo
         m.volume = (1.0 - ratio) * mixtureleft.volume + ratio * mixtureright.volume
     m.Y = (1.0 - ratio) * mixtureleft.Y + ratio * mixtureright.Y
     return m
+
+
+def _combine(recipe, mode: str):
+    """Mole fractions of a mixed recipe [(Mixture, ratio), ...] and the normalised mixing mole
+    ratios (reference mixture.py:2920-2975 / 3108-3160): 'mole' ratios are used as given,
+    'mass' ratios are converted to moles with each mixture's WTM."""
+    if not recipe:
+        raise MixtureError("empty mixing recipe")
+    chem_id = recipe[0][0].chemID
+    x = np.zeros(recipe[0][0].KK)
+    ratios = np.zeros(len(recipe))
+    for i, (m, v) in enumerate(recipe):
+        if not isinstance(m, Mixture):
+            raise MixtureError("the recipe must hold Mixture objects")
+        if m.chemID != chem_id:
+            raise MixtureError(f"mixture {i} of the recipe uses a different chemistry set")
+        if v <= 0.0:
+            raise MixtureError(f"mixing ratio {i} must be > 0")
+        ratios[i] = v if mode.lower() == "mole" else v / m.WTM
+        x += m.X * ratios[i]
+    total = ratios.sum()
+    return x / total, ratios / total
+
+
+def isothermal_mixing(recipe: List[Tuple[Mixture, float]], mode: str, finaltemperature: float) -> Mixture:
+    """Mix gas mixtures at a given final temperature (reference mixture.py:2802-2988)."""
+    if finaltemperature <= 10.0:
+        raise MixtureError("the final mixture temperature must be given (> 10 K)")
+    x, _ = _combine(recipe, mode)
+    final = copy.deepcopy(recipe[0][0])
+    final.X = x
+    final.temperature = finaltemperature
+    return final
+
+
+def calculate_mixture_temperature_from_enthalpy(mixture: Mixture, mixtureH: float,
+                                                guesstemperature: float = 0.0) -> int:
+    """Newton iteration for T with HML(T) = mixtureH [erg/mol], converged when the correction is
+    below 0.1 K (reference mixture.py:3179-3266: the last, sub-0.1 K correction is not applied;
+    this keeps that, and returns 2 instead of looping when 200 iterations do not converge).
+    Mixture enthalpy and cp come from the device species thermo (only T is needed)."""
+    X = mixture.X
+    T = guesstemperature if guesstemperature > 0.0 else mixture.temperature
+    if T <= 1.0:
+        T = 300.0
+    chem = mixture.chemistry
+    for _ in range(200):
+        f = float(np.dot(X, chem.SpeciesH(T))) - mixtureH
+        df = float(np.dot(X, chem.SpeciesCp(T)))
+        if df == 0.0:
+            return 1
+        dt = f / df
+        if abs(dt) <= 0.1:
+            mixture.temperature = T
+            return 0
+        T -= dt
+    mixture.temperature = T
+    return 2
+
+
+def adiabatic_mixing(recipe: List[Tuple[Mixture, float]], mode: str) -> Mixture:
+    """Mix gas mixtures at constant total enthalpy (reference mixture.py:2990-3177)."""
+    x, ratios = _combine(recipe, mode)
+    h = 0.0
+    for (m, _), r in zip(recipe, ratios):
+        h += float(np.dot(m.X, m.chemistry.SpeciesH(m.temperature))) * r  # erg/mol of the final mixture
+    final = copy.deepcopy(recipe[0][0])
+    final.X = x
+    err = calculate_mixture_temperature_from_enthalpy(final, h)
+    if err != 0:
+        raise MixtureError(f"mixture temperature from enthalpy did not converge (error {err})")
+    return final

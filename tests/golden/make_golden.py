@@ -20,6 +20,8 @@ KEEP = {
     "createmixture": ["tolerance-var", "tolerance-frac", "tolerance-ROP", "state-temperature", "state-density"],
     "sensitivity": None,
     "adiabaticflametemperature": None,
+    "equilibriumcomposition": None,
+    "mixturemixing": None,
 }
 
 if __name__ == "__main__":

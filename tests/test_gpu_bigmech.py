@@ -130,7 +130,7 @@ def test_drop_in_api_on_161_species_mechanism(big):
     m.X = [("CH4", 0.05), ("O2", 0.15), ("N2", 0.6), ("OH", 0.01), ("AX1", 0.1), ("AX60", 0.05), ("AX108", 0.04)]
     qfo, qro, wo = orc.rates(1700.0, 3 * P_ATM, m.Y)
     assert np.max(np.abs(m.ROP() - wo)) < 1e-11 * np.max(np.abs(wo))
-    qf, qr = m.RxnRates()
+    qf, qr = m.RxnRates(reference_compat=False)
     assert np.max(np.abs(qf - qfo)) < 1e-11 * np.max(np.abs(qfo))
     assert np.max(np.abs(qr - qro)) < 1e-11 * np.max(np.abs(qro))
     # tracer exchange AX1 + H <=> AX2 + H carries a nonzero rate

@@ -14,31 +14,44 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _conservation(mech, Y0, Y, tol=1e-7):
-    # elements are conserved by each Newton update only up to the integrator's error control (the
-    # BDF corrector is not projected), so the worst of 2^20 reactors drifts ~1e-7 at rtol 1e-8 --
-    # the oracle's integrator behaves the same way
-    assert np.allclose(Y.sum(axis=1), 1.0, atol=1e-7)
+def _drift(mech, Y0, Y):
     ncf = mech.ncf.astype(float)
     e0 = (Y0 / mech.wt) @ ncf.T
     e1 = (Y / mech.wt) @ ncf.T
-    assert np.max(np.abs(e1 - e0) / np.max(e0, axis=1, keepdims=True)) < tol
+    return np.max(np.abs(e1 - e0) / np.max(e0, axis=1, keepdims=True), axis=1)
 
 
-def _oracle_sample(mech, T0, P0, Y0, prob, res, nsample, threads=16):
+def _conservation(mech, Y0, Y, tol=1e-7):
+    """Mass closes to 1e-7 and elements are conserved to `tol` in every reactor.  Elements are kept
+    only up to the Newton convergence of each BDF step (the corrector is not projected), so the
+    drift is a chaotic property of the step sequence: per reactor it does not correlate between
+    GPU and oracle (rounding flips step decisions), but its distribution matches
+    (scripts/drift_diag.py: median 1.7e-12 vs 1.5e-12, 99th pct 2e-10 vs 3e-10 on 1024 configs[2]
+    reactors).  The worst of 2^20 reactors drifts ~1e-7."""
+    assert np.allclose(Y.sum(axis=1), 1.0, atol=1e-7)
+    d = _drift(mech, Y0, Y)
+    assert d.max() < tol
+    return d
+
+
+def _oracle_sample(mech, T0, P0, Y0, prob, res, nsample, d_gpu, threads=16):
+    """tau and final T of a strided subsample against the oracle (1e-4), and the element-drift
+    distribution of the GPU on that subsample against the oracle's (90th percentile within 10x)."""
     from oracle.oracle import Oracle
 
     import bench
 
     idx = np.linspace(0, T0.size - 1, nsample).astype(np.int64)
     orc = Oracle(mech)
-    nfail, ref, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=prob[idx], V0=np.ones(idx.size),
-                                      nthreads=threads, **bench.RUN)
+    nfail, ref, Yo = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=prob[idx], V0=np.ones(idx.size),
+                                       nthreads=threads, **bench.RUN)
     assert nfail == 0
     tau_o = np.array([r.tau for r in ref])
     T_o = np.array([r.T for r in ref])
     assert np.max(np.abs(res["tau"][idx] / tau_o - 1)) < 1e-4
     assert np.max(np.abs(res["T"][idx] / T_o - 1)) < 1e-4
+    d_o = _drift(mech, Y0[idx], np.asarray(Yo))
+    assert np.percentile(d_gpu[idx], 90) <= 10.0 * np.percentile(d_o, 90) + 1e-11
 
 
 def _run(dm, T0, P0, Y0, prob):
@@ -63,10 +76,10 @@ def test_configs2_full_sweep(tables, mech):
     assert np.all(res["stats"][:, 6] == 0)
     assert np.all(res["tau"] > 0) and np.all(res["tau"] < 1.0)
     assert np.all(res["T"] > T0 + 300.0)
-    _conservation(mech, Y0, res["Y"])
+    d = _conservation(mech, Y0, res["Y"])
     tau = res["tau"].reshape(64, 32, 32)  # (T0, phi, P)
     assert np.all(np.diff(np.log(tau), axis=0) < 0)  # hotter ignites sooner (no NTC for CH4 at 1100-1700 K)
-    _oracle_sample(mech, T0, P0, Y0, prob, res, 256)
+    _oracle_sample(mech, T0, P0, Y0, prob, res, 256, d)
 
 
 def test_configs3_full_sweep(tables, mech):
@@ -81,7 +94,7 @@ def test_configs3_full_sweep(tables, mech):
     res = _run(dm, T0, P0, Y0, prob)
     assert np.all(res["stats"][:, 6] == 0)
     assert np.all(res["tau"] > 0) and np.all(res["tau"] < 1.0)
-    _conservation(mech, Y0, res["Y"], tol=3e-7)
+    d = _conservation(mech, Y0, res["Y"], tol=3e-7)
     conp, conv = prob == 1, prob == 2
     # CONP keeps P, CONV keeps V (V0 = 1) and raises P with the temperature
     assert np.allclose(res["P"][conp], P0[conp], rtol=1e-12)
@@ -90,7 +103,7 @@ def test_configs3_full_sweep(tables, mech):
     assert np.all(res["tau"][conv] <= res["tau"][conp] * (1 + 1e-3))
     tau = res["tau"][conp].reshape(128, 64, 64)
     assert np.all(np.diff(np.log(tau), axis=0) < 0)
-    _oracle_sample(mech, T0, P0, Y0, prob, res, 256)
+    _oracle_sample(mech, T0, P0, Y0, prob, res, 256, d)
 
 
 def test_configs4_sample(big_mech):
@@ -107,5 +120,5 @@ def test_configs4_sample(big_mech):
     assert np.all(res["stats"][:, 6] == 0)
     assert np.all(res["tau"] > 0) and np.all(res["tau"] < 1.0)
     assert np.all(res["T"] > T0 + 300.0)
-    _conservation(big_mech, Y0, res["Y"])
-    _oracle_sample(big_mech, T0, P0, Y0, prob, res, 64)
+    d = _conservation(big_mech, Y0, res["Y"], tol=3e-7)
+    _oracle_sample(big_mech, T0, P0, Y0, prob, res, 64, d)

@@ -99,9 +99,12 @@ def test_rop_and_rates_match_batched_kernels(K, mech, tables, oracle):
         assert L.KINGetGasROP(ct.byref(cs), ct.byref(T), ct.byref(P), Y, wdot) == 0
         assert L.KINGetGasReactionRates(ct.byref(cs), ct.byref(T), ct.byref(P), Y, qf, qr) == 0
         w_b, _, _ = dm.rop_thermo([T_], [P_], Y[:, None])
-        qf_b, qr_b = dm.reaction_rates([T_], [P_], Y[:, None])
+        y_x = Y * mech.wt / np.sum(Y * mech.wt)  # KINGetGasReactionRates reads mole fractions
+        qf_b, qr_b = dm.reaction_rates([T_], [P_], y_x[:, None])
         assert np.array_equal(wdot, w_b.cpu().numpy()[:, 0])  # same kernel, batch of one
-        assert np.array_equal(qf, qf_b.cpu().numpy()[:, 0]) and np.array_equal(qr, qr_b.cpu().numpy()[:, 0])
+        # (host X -> Y conversions may round differently in the last bit)
+        assert np.allclose(qf, qf_b.cpu().numpy()[:, 0], rtol=1e-13, atol=0)
+        assert np.allclose(qr, qr_b.cpu().numpy()[:, 0], rtol=1e-13, atol=0)
         w_o = oracle.rates(T_, P_, Y)[2]
         scale = np.max(np.abs(w_o))
         assert np.max(np.abs(wdot - w_o)) <= 1e-9 * scale
@@ -213,3 +216,21 @@ def test_unknown_and_unsupported_keywords_fail(K, mech):
     assert L.KINAll0D_SetProfileParameter(b"VPRO", ct.byref(ct.c_int(2)), x, x + 1) == 0
     assert L.KINAll0D_Calculate(ct.byref(cs)) != 0  # VPRO on a CONP reactor
     assert b"VPRO" in L.ckmi_kin_last_error()
+
+
+def test_reaction_rates_golden_through_kin_call(K, mech):
+    """reactionrates.baseline exactly as the reference produces it: mixture.py:1540 passes the mass
+    fractions to KINGetGasReactionRates, which reads them as mole fractions."""
+    from conftest import ch4_air_Y
+
+    L, cs = K
+    g = golden("reactionrates")
+    Y = np.ascontiguousarray(ch4_air_Y(mech, 1.0)[0])
+    qf, qr = np.zeros(mech.II), np.zeros(mech.II)
+    assert L.KINGetGasReactionRates(ct.byref(cs), ct.byref(ct.c_double(1800.0)), ct.byref(ct.c_double(5 * P_ATM)), Y,
+                                    qf, qr) == 0
+    net = qf - qr
+    nz = np.nonzero(net)[0]
+    order = nz[np.argsort(-net[nz], kind="stable")]
+    assert order.tolist() == g["state-order_1800"]
+    assert np.all(within(net[order], g["rate-net_reaction_rate_1800"], *g["tolerance-ROP"]))

@@ -82,19 +82,32 @@ def test_ch4_air_rcm_conv_with_volume_profile(oracle, mech):
 def test_reaction_rates_1800K_ordering(oracle, mech):
     """reactionrates.py:72-116: CH4/air phi=1, 5 atm, 1800 K, nonzero net rates in descending order.
 
-    Ordering and signs reproduce; magnitudes agree within a factor of two only (parity partial:
-    the five rates are trace reverse rates of reactions whose products are absent, extremely
-    sensitive to the high-temperature thermo of the vendor's packaged GRI data).
+    The reference's Mixture.RxnRates hands the MASS fractions to KINGetGasReactionRates
+    (mixture.py:1540), and the closed library reads that argument as MOLE fractions (Chemkin's
+    CKKFKR(P, T, X) convention).  The golden rates are those of the state whose mole fractions
+    equal the mixture's mass fractions: reproduced to <= 1.4e-5 that way (3 of 5 to 1e-14), while
+    reading the array as mass fractions misses by 0.85-1.82x (the round-1 "parity partial").
     """
     g = golden("reactionrates")
     Y0 = ch4_air_Y(mech, 1.0)[0]
-    qf, qr, _ = oracle.rates(1800.0, 5 * P_ATM, Y0)
-    net = qf - qr
-    nz = np.nonzero(net)[0]
-    order = nz[np.argsort(-net[nz], kind="stable")]
+    gold = np.asarray(g["rate-net_reaction_rate_1800"])
+
+    def net_order(Y):
+        qf, qr, _ = oracle.rates(1800.0, 5 * P_ATM, Y)
+        net = qf - qr
+        nz = np.nonzero(net)[0]
+        order = nz[np.argsort(-net[nz], kind="stable")]
+        return order, net[order]
+
+    y_as_x = Y0 * mech.wt / np.sum(Y0 * mech.wt)  # mass fractions of the state with X = Y0
+    order, net = net_order(y_as_x)
     assert order.tolist() == g["state-order_1800"]
-    ratio = net[order] / np.asarray(g["rate-net_reaction_rate_1800"])
-    assert np.all((ratio > 0.5) & (ratio < 2.0))
+    assert np.all(within(net, gold, *g["tolerance-ROP"]))
+    assert np.max(np.abs(net / gold - 1)) < 2e-5
+    # the same rates read as mass fractions: same ordering, magnitudes off by up to 1.8x
+    order_m, net_m = net_order(Y0)
+    assert order_m.tolist() == g["state-order_1800"]
+    assert np.max(np.abs(net_m / gold - 1)) > 0.5
 
 
 def test_afactor_sensitivity_golden(oracle, mech, chem):
@@ -133,3 +146,82 @@ def test_hp_equilibrium_adiabatic_flame_temperature(oracle, mech, tables):
         assert res.status == 0
         assert within(np.array([res.T]), np.array([Tg]), *g["tolerance-var"]).all()
         assert abs(res.T / Tg - 1) < 1e-7, (phi, res.T, Tg)
+
+
+def _equilibrium_premixed(mech):
+    """equilibriumcomposition.py:50-62: fuel X CH4/H2 = 0.8/0.2, air Y O2/N2 = 0.23/0.77, mixed
+    1 : 17.19 by mass (isothermal_mixing, mode="mass") -> mass fractions."""
+    Xf = np.zeros(mech.KK)
+    Xf[mech.species.index("CH4")], Xf[mech.species.index("H2")] = 0.8, 0.2
+    Yf = Xf * mech.wt / np.sum(Xf * mech.wt)
+    Ya = np.zeros(mech.KK)
+    Ya[mech.species.index("O2")], Ya[mech.species.index("N2")] = 0.23, 0.77
+    return (Yf + 17.19 * Ya) / 18.19
+
+
+def test_tp_equilibrium_no_golden(oracle, mech):
+    """equilibriumcomposition.baseline: TP-equilibrium NO [ppm] at 1 atm, T = 500..2480 K (100
+    points), by element-potential Gibbs minimisation over the oracle's NASA-7 thermo
+    (oracle/equilibrium.py).  Pins h and s of every species that matters for NO against the
+    vendor's equilibrium solver: all 100 points inside the golden tolerance."""
+    from oracle.equilibrium import TPEquilibrium
+
+    g = golden("equilibriumcomposition")
+    Y = _equilibrium_premixed(mech)
+    eq = TPEquilibrium(mech, oracle.thermo)
+    iNO = mech.species.index("NO")
+    Ts = np.asarray(g["state-temperature"])
+    no = np.zeros(Ts.size)
+    for i in range(Ts.size - 1, -1, -1):  # hot to cold: continuation from the previous solution
+        no[i] = eq.solve(Ts[i], 1.0, Y)[iNO] * 1e6
+    gold = np.asarray(g["species-NO_mole_fraction"])
+    assert np.all(within(no, gold, *g["tolerance-frac"]))
+    big = gold > 1.0  # >= 1 ppm: relative agreement
+    assert np.max(np.abs(no[big] / gold[big] - 1)) < 1e-7
+
+
+def test_mixing_golden_composition(chem, mech):
+    """mixturemixing.baseline, composition half (mixturemixing.py:40-60): CH4 + air 1 : 17.19 by
+    mass at 300 K, then 0.7 : 0.3 by moles with Ar at 600 K.  Host-side mixing, no GPU."""
+    import pychemkin_amd as ck
+
+    g = golden("mixturemixing")
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    fuel.temperature = 300.0
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    air.temperature = 300.0
+    premixed = ck.isothermal_mixing(recipe=[(fuel, 1.0), (air, 17.19)], mode="mass", finaltemperature=300.0)
+    assert np.all(within(premixed.X, g["species-premixed_mole_fraction"], *g["tolerance-frac"]))
+    assert premixed.temperature == g["state-temperature"][0]
+    ar = ck.Mixture(chem)
+    ar.X = [("AR", 1.0)]
+    ar.temperature = 600.0
+    x, _ = ck.mixture._combine([(premixed, 0.7), (ar, 0.3)], "mole")
+    assert np.all(within(x, g["species-diluted_mole_fraction"], *g["tolerance-frac"]))
+
+
+def test_adiabatic_mixing_temperature_host_logic(chem, mech, oracle, monkeypatch):
+    """mixturemixing.baseline, temperature half, with the oracle's thermo standing in for the device
+    species thermo (the GPU run of the same call is in test_gpu_kernels): the reference's Newton
+    iteration (mixture.py:3179-3266) lands within the golden tolerance of 368.674 K."""
+    import pychemkin_amd as ck
+    from pychemkin_amd.constants import R_GAS
+
+    monkeypatch.setattr(type(chem), "SpeciesH", lambda self, T, pres=None: oracle.thermo(T)[1] * R_GAS * T)
+    monkeypatch.setattr(type(chem), "SpeciesCp", lambda self, T, pres=None: oracle.thermo(T)[0] * R_GAS)
+    g = golden("mixturemixing")
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    fuel.temperature = 300.0
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    air.temperature = 300.0
+    premixed = ck.isothermal_mixing(recipe=[(fuel, 1.0), (air, 17.19)], mode="mass", finaltemperature=300.0)
+    ar = ck.Mixture(chem)
+    ar.X = [("AR", 1.0)]
+    ar.temperature = 600.0
+    diluted = ck.adiabatic_mixing(recipe=[(premixed, 0.7), (ar, 0.3)], mode="mole")
+    assert within(np.array([diluted.temperature]), np.array([g["state-temperature"][2]]), *g["tolerance-var"]).all()
+    assert ar.temperature == g["state-temperature"][1]

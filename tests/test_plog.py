@@ -196,6 +196,6 @@ def test_drop_in_api_on_plog_mechanism(pmech, porc):
                ("HO2", 0.01), ("CH2O", 0.01)]
         qfo, qro, wo = porc.rates(1650.0, p * P_ATM, m.Y)
         assert np.max(np.abs(m.ROP() - wo)) < 1e-11 * np.max(np.abs(wo))
-        qf, qr = m.RxnRates()
+        qf, qr = m.RxnRates(reference_compat=False)
         assert np.max(np.abs(qf - qfo)) < 1e-11 * np.max(np.abs(qfo))
         assert np.max(np.abs(qr - qro)) < 1e-11 * np.max(np.abs(qro))
