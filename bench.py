@@ -252,8 +252,13 @@ def rop_line(dev, mech, ops, ns, rank, world, cpu_sample, kernel_name="rop_kerne
     wdot = torch.empty((mech.KK, ns), dtype=torch.float64, device=dev)
     cp = torch.empty(ns, dtype=torch.float64, device=dev)
     hh = torch.empty(ns, dtype=torch.float64, device=dev)
-    dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)
+    dm.rop_thermo(Ts, Ps, Ys, wdot, cp, hh)  # warm-up: also compiles the specialised kernel (hipRTC)
     torch.cuda.synchronize()
+    jit = dm.rop_jit_state() == 1
+    if jit:
+        kernel_name, flops_key, traffic_key = "ckjit_rop", "F_rop_jit", traffic_key + "_jit"
+    else:
+        flops_key = "F_rop"
     reps = 3
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -262,13 +267,14 @@ def rop_line(dev, mech, ops, ns, rank, world, cpu_sample, kernel_name="rop_kerne
     e1.record()
     torch.cuda.synchronize()
     sec = e0.elapsed_time(e1) / 1e3 / reps
-    tf = ops["F_rop"] * ns / sec / 1e12
+    tf = ops[flops_key] * ns / sec / 1e12
     gbs = ops["bytes_rop"] * ns / sec / 1e9
     out = {"value": ns / sec, "unit": "states/s", "states": ns, "ms_per_launch": sec * 1e3,
            "roofline": {"bound": "valu", "pipe": "fp64-valu", "kernel": kernel_name, "achieved": tf,
                         "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": tf / FP64_PEAK_TFLOPS,
                         "hbm_GBs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS, "traffic": load_traffic(traffic_key, ns)},
-           "cpu_baseline": None}
+           "cpu_baseline": None,
+           "kernel": "mechanism-specialised, one state per lane (hipRTC)" if jit else "generic, one reaction per lane"}
     if label:
         out["mechanism"] = label
     if rank == 0 and world == 1 and cpu_sample > 0:

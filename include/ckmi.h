@@ -176,6 +176,19 @@ int ckmi_species_thermo(const ckmi_mech* mech, int32_t n, const double* T, doubl
 int ckmi_rop_thermo(const ckmi_mech* mech, int32_t n, const double* T, const double* P, const double* Y,
                     double* wdot, double* cp, double* h, void* stream);
 
+/* Kernel selection for ckmi_rop_thermo (process-wide): 0 = automatic (the mechanism-specialised
+ * kernel -- one state per lane, generated from the mechanism and compiled with hipRTC at first use
+ * -- for batches of >= 16384 states when the mechanism has no PLOG / chemically activated
+ * reactions, else the generic reaction-per-lane kernel), 1 = generic kernel, 2 = specialised kernel
+ * (error if it is unavailable).  ckmi_rop_jit_state: 0 not compiled yet, 1 ready, -1 unavailable
+ * (ckmi_last_error() then says why). */
+int ckmi_set_rop_path(int32_t path);
+int ckmi_rop_jit_state(const ckmi_mech* mech, int32_t* state);
+/* The generated source of the specialised kernel (len = its length; copied into buf when given) and
+ * a compile-only check (hipRTC, no GPU needed; code_bytes = size of the gfx950 code object). */
+int ckmi_rop_jit_source(const ckmi_mech_desc* desc, char* buf, int64_t cap, int64_t* len);
+int ckmi_rop_jit_compile(const ckmi_mech_desc* desc, int64_t* code_bytes);
+
 /* Batched forward/reverse rates of progress: qf[II][n], qr[II][n] mol/cm3-s. */
 int ckmi_reaction_rates(const ckmi_mech* mech, int32_t n, const double* T, const double* P, const double* Y,
                         double* qf, double* qr, void* stream);

@@ -79,6 +79,10 @@ PROTOTYPES = {
     "ckmi_reactor_run_ex": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P,
                                         ct.POINTER(ReactorExt), _P, _P, _P, _P, _P, _P, ct.c_int32, _P, _P, _P]),
     "ckmi_set_reactor_path": (ct.c_int, [ct.c_int32]),
+    "ckmi_set_rop_path": (ct.c_int, [ct.c_int32]),
+    "ckmi_rop_jit_state": (ct.c_int, [_P, ct.POINTER(ct.c_int32)]),
+    "ckmi_rop_jit_source": (ct.c_int, [ct.POINTER(MechDesc), ct.c_char_p, ct.c_int64, ct.POINTER(ct.c_int64)]),
+    "ckmi_rop_jit_compile": (ct.c_int, [ct.POINTER(MechDesc), ct.POINTER(ct.c_int64)]),
     "ckmi_lu_factor_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
     "ckmi_lu_solve_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
     "ckmi_lu_last_error": (ct.c_char_p, []),
@@ -162,6 +166,41 @@ def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: flo
     return c
 
 
+def mech_desc(tables: Dict[str, np.ndarray]):
+    """ckmi_mech_desc view of flat mechanism tables; returns (desc, arrays kept alive)."""
+    keep = {k: np.ascontiguousarray(v) for k, v in tables.items() if isinstance(v, np.ndarray) and v.ndim > 0}
+    d = MechDesc()
+    d.KK, d.II = int(tables["KK"]), int(tables["II"])
+    for name, _ in MechDesc._fields_[2:]:
+        setattr(d, name, keep[name].ctypes.data)
+    return d, keep
+
+
+def rop_jit_source(tables: Dict[str, np.ndarray]) -> str:
+    """Source of the mechanism-specialised ROP kernel (host only, no GPU)."""
+    d, keep = mech_desc(tables)
+    n = ct.c_int64(0)
+    _check(lib().ckmi_rop_jit_source(ct.byref(d), None, 0, ct.byref(n)), "ckmi_rop_jit_source")
+    buf = ct.create_string_buffer(n.value + 1)
+    _check(lib().ckmi_rop_jit_source(ct.byref(d), buf, n.value + 1, ct.byref(n)), "ckmi_rop_jit_source")
+    del keep
+    return buf.value.decode()
+
+
+def rop_jit_compile(tables: Dict[str, np.ndarray]) -> int:
+    """Compile the specialised ROP kernel with hipRTC (no GPU); returns the code object size."""
+    d, keep = mech_desc(tables)
+    n = ct.c_int64(0)
+    _check(lib().ckmi_rop_jit_compile(ct.byref(d), ct.byref(n)), "ckmi_rop_jit_compile")
+    del keep
+    return int(n.value)
+
+
+def set_rop_path(path: int) -> None:
+    """0 automatic, 1 generic reaction-per-lane kernel, 2 mechanism-specialised kernel."""
+    _check(lib().ckmi_set_rop_path(int(path)), "ckmi_set_rop_path")
+
+
 class DeviceMechanism:
     """Mechanism tables resident in HBM of one GPU (wraps a ckmi_mech handle)."""
 
@@ -196,6 +235,12 @@ class DeviceMechanism:
     @property
     def handle(self):
         return self._h
+
+    def rop_jit_state(self) -> int:
+        """Specialised ROP kernel of this mechanism: 0 not compiled yet, 1 ready, -1 unavailable."""
+        st = ct.c_int32(0)
+        _check(lib().ckmi_rop_jit_state(self._h, ct.byref(st)), "ckmi_rop_jit_state")
+        return int(st.value)
 
     # -------------------------------------------------------------- parameters
     def arrhenius(self):

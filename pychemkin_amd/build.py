@@ -10,6 +10,7 @@ SRC = os.path.join(HERE, "csrc", "ckmi.hip")        # kinetics, thermo and react
 LU_SRC = os.path.join(HERE, "csrc", "ckmi_lu.hip")  # batched MFMA LU (large mechanisms)
 BIG_SRC = os.path.join(HERE, "csrc", "ckmi_big.hip")  # workgroup-per-reactor integrator (64 <= KK + 1 <= 192)
 KIN_SRC = os.path.join(HERE, "csrc", "ckmi_kin.cpp")  # KIN-compatible host shims (include/ckmi_kin.h)
+JIT_SRC = os.path.join(HERE, "csrc", "ckmi_jit.cpp")  # mechanism-specialised ROP kernel generator (hipRTC)
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp", "ckmi_image.hpp",
                                                 "ckmi_run.hpp", "ckmi_internal.hpp")] + [
     os.path.join(HERE, "..", "include", "ckmi.h"), os.path.join(HERE, "..", "include", "ckmi_kin.h")]
@@ -31,7 +32,7 @@ LU_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", f"--offload
 BIG_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-mcode-object-version=5", f"--offload-arch={ARCH}",
              "-mllvm", "-disable-machine-licm", "-mllvm", "-disable-machine-sink",
              "-mllvm", "-pragma-unroll-threshold=2000000"]
-KIN_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall"]  # host code only
+KIN_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}"]  # host code only
 
 
 def _stale(target: str, sources) -> bool:
@@ -42,7 +43,7 @@ def _stale(target: str, sources) -> bool:
 
 
 def needs_build() -> bool:
-    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC] + DEPS)
+    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC, JIT_SRC] + DEPS)
 
 
 PROF_OUT = os.path.join(HERE, "_lib", "libckmi_prof.so")  # diagnostic phase-timer build
@@ -59,7 +60,8 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     """Build libckmi.so (or the phase-timer build, or an A/B variant at `out` with `extra` flags).
 
     Four translation units, compiled separately (the reactor kernel alone takes ~2 min) and linked
-    into one shared library: ckmi.hip, ckmi_lu.hip, ckmi_big.hip and the host-only ckmi_kin.cpp."""
+    into one shared library: ckmi.hip, ckmi_lu.hip, ckmi_big.hip and the host-only ckmi_kin.cpp and
+    ckmi_jit.cpp (linked with libhiprtc)."""
     default = out is None and not prof and not extra
     out = out or (PROF_OUT if prof else OUT)
     if not force and default and not needs_build():
@@ -74,11 +76,15 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     kin_obj = os.path.join(OBJ_DIR, "ckmi_kin.o")
     if force or _stale(kin_obj, [KIN_SRC] + DEPS):
         _compile(KIN_SRC, kin_obj, KIN_FLAGS, verbose)
+    jit_obj = os.path.join(OBJ_DIR, "ckmi_jit.o")
+    if force or _stale(jit_obj, [JIT_SRC] + DEPS):
+        _compile(JIT_SRC, jit_obj, KIN_FLAGS, verbose)
     tag = "main" if default else os.path.splitext(os.path.basename(out))[0]
     main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
     if force or (not default and not prof) or _stale(main_obj, [SRC] + DEPS):
         _compile(SRC, main_obj, FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(extra), verbose)
-    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj, kin_obj]
+    cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj, kin_obj, jit_obj,
+           "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

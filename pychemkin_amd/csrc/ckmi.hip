@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -20,6 +21,8 @@ namespace {
 
 thread_local std::string g_err;
 int g_reactor_path = 0;  // ckmi_set_reactor_path
+int g_rop_path = 0;      // ckmi_set_rop_path
+constexpr int JIT_MIN_STATES = 16384;  // automatic choice: the specialised kernel from this batch size up
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -1253,6 +1256,31 @@ int launch_rop(const ckmi_mech* m, int n, const double* T, const double* P, cons
   }
 }
 
+// compile and load the specialised ROP kernel of m once (thread-safe); CKMI_OK when it can run
+int jit_ready(ckmi_mech* m) {
+  if (!m->jit) return fail(CKMI_ERR_UNSUPPORTED, "no specialised ROP kernel");
+  JitRop& J = *m->jit;
+  std::lock_guard<std::mutex> lk(J.mu);
+  if (J.state == 1) return CKMI_OK;
+  if (J.state == -1) return fail(CKMI_ERR_UNSUPPORTED, "specialised ROP kernel unavailable: " + J.why);
+  std::vector<char> code;
+  std::string log;
+  const int rc = jit_rop_compile(J.src, code, log);
+  if (rc) {
+    J.state = -1;
+    J.why = "hipRTC compilation failed: " + log.substr(0, 2000);
+    return fail(CKMI_ERR_HIP, J.why);
+  }
+  if (hipModuleLoadData(&J.mod, code.data()) != hipSuccess ||
+      hipModuleGetFunction(&J.fn, J.mod, "ckjit_rop") != hipSuccess) {
+    J.state = -1;
+    J.why = "hipModuleLoadData / hipModuleGetFunction failed";
+    return fail(CKMI_ERR_HIP, J.why);
+  }
+  J.state = 1;
+  return CKMI_OK;
+}
+
 }  // namespace
 
 int ckmi::set_error(int code, const std::string& msg) { return fail(code, msg); }
@@ -1461,12 +1489,41 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     ckmi_mech_destroy(m);
     return rc;
   }
+  // the mechanism-specialised ROP kernel: source and parameter block now, compilation at first use
+  m->jit = new JitRop();
+  {
+    std::vector<double> prm;
+    const char* env = std::getenv("CKMI_ROP_JIT");
+    if (env && env[0] == '0') {
+      m->jit->state = -1;
+      m->jit->why = "disabled by CKMI_ROP_JIT=0";
+    } else if (!jit_rop_generate(d, m->jit->src, prm, m->jit->lnA_off, m->jit->why)) {
+      m->jit->state = -1;
+    } else {
+      const double* p = nullptr;
+      if (upload(m, prm, &p)) {
+        ckmi_mech_destroy(m);
+        return CKMI_ERR_HIP;
+      }
+      m->jit->prm = const_cast<double*>(p);
+      if (const char* dump = std::getenv("CKMI_JIT_DUMP")) {
+        if (FILE* f = std::fopen(dump, "w")) {
+          std::fputs(m->jit->src.c_str(), f);
+          std::fclose(f);
+        }
+      }
+    }
+  }
   *out = m;
   return CKMI_OK;
 }
 
 int ckmi_mech_destroy(ckmi_mech* m) {
   if (!m) return CKMI_OK;
+  if (m->jit) {
+    if (m->jit->mod) (void)hipModuleUnload(m->jit->mod);
+    delete m->jit;
+  }
   for (void* p : m->allocs) (void)hipFree(p);
   delete m;
   return CKMI_OK;
@@ -1499,6 +1556,11 @@ int ckmi_set_afactor(ckmi_mech* m, int32_t irxn, double A) {
   HIP_CHECK(hipMemcpy(const_cast<double*>(m->d.lnA) + s, &lnA, sizeof(double), hipMemcpyHostToDevice));
   HIP_CHECK(hipMemcpy((char*)m->img.blob + m->img.o_lnA + sizeof(double) * s, &lnA, sizeof(double),
                       hipMemcpyHostToDevice));
+  if (m->jit && m->jit->prm) {
+    HIP_CHECK(hipMemcpy(m->jit->prm + m->jit->lnA_off[irxn], &lnA, sizeof(double), hipMemcpyHostToDevice));
+    if (m->b_orig[irxn] == 0.0 && m->E_orig[irxn] == 0.0)  // k = A reactions read A itself (ckmi_jit.cpp)
+      HIP_CHECK(hipMemcpy(m->jit->prm + m->jit->lnA_off[irxn] + 1, &A, sizeof(double), hipMemcpyHostToDevice));
+  }
   return CKMI_OK;
 }
 
@@ -1517,7 +1579,58 @@ int ckmi_rop_thermo(const ckmi_mech* m, int32_t n, const double* T, const double
                     double* cp, double* h, void* stream) {
   if (!m || n < 0 || !wdot) return fail(CKMI_ERR_ARG, "bad argument");
   if (n == 0) return CKMI_OK;
+  const int path = g_rop_path;
+  if (path == 2 || (path == 0 && n >= JIT_MIN_STATES)) {
+    const int rc = jit_ready(const_cast<ckmi_mech*>(m));
+    if (rc == CKMI_OK) {
+      void* args[] = {&n, (void*)&T, (void*)&P, (void*)&Y, &wdot, &cp, &h, &m->jit->prm};
+      HIP_CHECK(hipModuleLaunchKernel(m->jit->fn, (unsigned)((n + 63) / 64), 1, 1, 64, 1, 1, 0, (hipStream_t)stream,
+                                      args, nullptr));
+      return CKMI_OK;
+    }
+    if (path == 2) return rc;
+  }
   return launch_rop<0>(m, n, T, P, Y, wdot, cp, h, (hipStream_t)stream);
+}
+
+int ckmi_set_rop_path(int32_t path) {
+  if (path < 0 || path > 2) return fail(CKMI_ERR_ARG, "rop path must be 0 (auto), 1 (generic) or 2 (specialised)");
+  g_rop_path = path;
+  return CKMI_OK;
+}
+
+int ckmi_rop_jit_source(const ckmi_mech_desc* d, char* buf, int64_t cap, int64_t* len) {
+  if (!d || !len) return fail(CKMI_ERR_ARG, "null argument");
+  std::string src, why;
+  std::vector<double> prm;
+  std::vector<int> off;
+  if (!jit_rop_generate(d, src, prm, off, why)) return fail(CKMI_ERR_UNSUPPORTED, why);
+  *len = (int64_t)src.size();
+  if (buf && cap > 0) {
+    const size_t k = std::min<size_t>((size_t)cap - 1, src.size());
+    std::memcpy(buf, src.data(), k);
+    buf[k] = 0;
+  }
+  return CKMI_OK;
+}
+
+int ckmi_rop_jit_compile(const ckmi_mech_desc* d, int64_t* code_bytes) {
+  if (!d || !code_bytes) return fail(CKMI_ERR_ARG, "null argument");
+  std::string src, why, log;
+  std::vector<double> prm;
+  std::vector<int> off;
+  if (!jit_rop_generate(d, src, prm, off, why)) return fail(CKMI_ERR_UNSUPPORTED, why);
+  std::vector<char> code;
+  if (jit_rop_compile(src, code, log)) return fail(CKMI_ERR_HIP, "hipRTC compilation failed: " + log.substr(0, 2000));
+  *code_bytes = (int64_t)code.size();
+  return CKMI_OK;
+}
+
+int ckmi_rop_jit_state(const ckmi_mech* m, int32_t* state) {
+  if (!m || !state) return fail(CKMI_ERR_ARG, "null argument");
+  *state = m->jit ? m->jit->state : -1;
+  if (m->jit && m->jit->state == -1) g_err = m->jit->why;
+  return CKMI_OK;
 }
 
 int ckmi_reaction_rates(const ckmi_mech* m, int32_t n, const double* T, const double* P, const double* Y, double* qf,

@@ -2,12 +2,30 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/ckmi.h"
 #include "ckmi_device.hpp"
 #include "ckmi_image.hpp"
+
+namespace ckmi {
+// mechanism-specialised ROP kernel (ckmi_jit.cpp): source generated at ckmi_mech_create, compiled
+// with hipRTC at the first call that selects it
+struct JitRop {
+  std::string src, why;
+  std::vector<int> lnA_off;  // original reaction -> offset of its ln A in the parameter block
+  double* prm = nullptr;     // device parameter block
+  int state = 0;             // 0 not compiled yet, 1 ready, -1 unsupported / compile failed (why)
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  std::mutex mu;
+};
+bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<double>& prm, std::vector<int>& lnA_off,
+                      std::string& why);
+int jit_rop_compile(const std::string& src, std::vector<char>& code, std::string& log);
+}  // namespace ckmi
 
 struct ckmi_mech {
   int device;
@@ -20,6 +38,7 @@ struct ckmi_mech {
   std::vector<int> rtype_orig;
   bool has_plog = false;
   std::vector<int> slot_of;  // original reaction -> device slot
+  ckmi::JitRop* jit = nullptr;
 };
 
 namespace ckmi {

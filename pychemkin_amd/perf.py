@@ -7,6 +7,8 @@ one add/multiply/divide/compare-free arithmetic op = 1 FLOP, and every transcend
 
   reactor  = sum over reactors of  nfe*F_rhs + nje*F_jac_extra + nlu*(F_build + F_lu) + nni*F_solve
   rop      = F_rhs_rop per state,  bytes = 8*(2 + KK) in + 8*(KK + 2) out per state
+  rop_jit  = the same for the specialised kernel (ckmi_jit.cpp): reactions with b = E = 0 take
+             k = A without the Arrhenius exp
 """
 from __future__ import annotations
 
@@ -32,6 +34,7 @@ def count_ops(tables: Dict[str, np.ndarray]) -> Dict[str, float]:
     f += 3 * KK                      # concentrations and total
     f += 2 * eff                     # third-body sums
     jac = 0.0
+    fj = f
     for i in range(II):
         slots = int(nr[i] + np_[i])
         powf = float(np.sum(rnu[i][: nr[i]]) + np.sum(pnu[i][: np_[i]]))
@@ -54,6 +57,8 @@ def count_ops(tables: Dict[str, np.ndarray]) -> Dict[str, float]:
         r += powf + 4                # concentration products and q
         r += 2 * slots               # production scatter
         f += r
+        arr = tables["arr"][i]
+        fj += r - ((4 + T) if (arr[1] == 0.0 and arr[2] == 0.0 and rtype[i] != 3) else 0)
         # Jacobian extra work for this reaction
         j = 2 * slots + 6 + 10 + 2 * slots
         for nsl in (int(nr[i]), int(np_[i])):
@@ -68,6 +73,7 @@ def count_ops(tables: Dict[str, np.ndarray]) -> Dict[str, float]:
         F_lu=(2.0 / 3.0) * n ** 3,
         F_solve=2.0 * n * n,
         F_rop=float(f),
+        F_rop_jit=float(fj + 2 * KK + 10 * KK + 10),
         bytes_rop=8.0 * (2 + KK) + 8.0 * (KK + 2),
         n=n,
     )
