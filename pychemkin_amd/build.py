@@ -31,7 +31,10 @@ LU_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-mcode-object-version=5", f"--offload
 # must stay in the unified VGPR + AGPR file, no scratch)
 BIG_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-munsafe-fp-atomics", "-mcode-object-version=5", f"--offload-arch={ARCH}",
              "-mllvm", "-disable-machine-licm", "-mllvm", "-disable-machine-sink",
-             "-mllvm", "-pragma-unroll-threshold=2000000"]
+             "-mllvm", "-pragma-unroll-threshold=2000000",
+             # the blocked Gauss-Jordan's MFMA accumulators are the register-resident matrix itself:
+             # VGPR-form MFMA (1249 -> 24 spilled VGPRs at NB = 11)
+             "-mllvm", "-amdgpu-mfma-vgpr-form"]
 KIN_FLAGS = ["-O2", "-std=c++17", "-fPIC", "-Wall", f"--offload-arch={ARCH}"]  # host code only
 
 

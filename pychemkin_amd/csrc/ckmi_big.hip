@@ -29,6 +29,8 @@
 // every setup; the oracle rounds J the same way).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -212,6 +214,7 @@ struct BigMatrix {
   static constexpr int NC = 16 * NB;
   static constexpr int NBP = (NB + 1) & ~1;  // LDS stride of the per-lane vectors (b128 pairs)
   double a[NB][NB];
+  __device__ __forceinline__ double entry(int r) const { return a[r][0]; }  // phase-timer probes
 
   __device__ __forceinline__ void build(const float* __restrict__ J, double gamma, int tid, int n) {
     const int t = opaque_lane(tid);
@@ -452,6 +455,272 @@ struct BigMatrix {
   }
 };
 
+// ------------------------------------------------------------------ blocked Gauss-Jordan on MFMA
+// Same factorisation as BigMatrix (explicit inverse of the row-permuted M, partial pivoting on
+// |a| rounded to fp32, ties to the lowest row, identical perm / rank / solve), reorganised in
+// panels of 4 steps.  The 4 columns of a panel sit in one wave (one per lane group q), which runs
+// the 4 pivot steps on them alone; GJ then gives every other column j
+//     a(:, j) <- a(:, j) + P'(:, 0:4) a(P, j)        (rows P = the 4 pivot rows, values before the panel)
+// with P' the processed panel columns minus the unit vectors e_p (the 4 elementary transforms
+// leave every vector that is zero at the pivot rows unchanged).  That rank-4 update is one
+// v_mfma_f64_16x16x4f64 per 16-row block and group of 4 register tiles: the thread layout
+// (row ti + 16 r, column 16 c + 4 w + q) is exactly the MFMA C/D map of a^T (col = lane & 15 = ti,
+// row = (lane >> 4) + 4 e = q + 4 e) when the 4 tiles c = 4 g + e form one accumulator, so the
+// registers are updated in place.  One workgroup barrier per panel instead of one per column.
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+struct PanHdr {
+  int p[4];
+  int ok;
+  int pad[3];
+};
+
+template <int NB>
+struct BigMatrixM {
+  static constexpr int NC = 16 * NB;
+  static constexpr int NG = (NB + 3) / 4;    // accumulator groups of 4 register tiles
+  static constexpr int NBP = (NB + 1) & ~1;  // LDS stride of the per-lane vectors (solve)
+  v4d a[NB][NG];
+  __device__ __forceinline__ double entry(int r) const { return a[r][0][0]; }  // phase-timer probes
+
+  __device__ __forceinline__ void build(const float* __restrict__ J, double gamma, int tid, int n) {
+    const int t = opaque_lane(tid);
+    const int lane = t & 63, w = t >> 6;
+    const int ti = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+#pragma unroll
+      for (int c = 0; c < 4 * NG; ++c) {
+        const int i = ti + 16 * r, j = 16 * c + 4 * w + q;
+        double v = 0.0;
+        if (c < NB) {
+          const double jv = (i < n && j < n) ? (double)J[(r * NB + c) * NT + t] : 0.0;
+          v = (i == j ? 1.0 : 0.0) - gamma * jv;
+        }
+        a[r][c >> 2][c & 3] = v;
+      }
+    }
+  }
+
+  // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo
+  template <int C>
+  __device__ __forceinline__ void panel(const BigLds& L, int wo, int par, uint32_t& pivmask, bool& ok, int t, int wid,
+                                        int lane
+#ifdef CKMI_PHASE_TIMERS
+                                        , unsigned long long (&fph)[3]
+#endif
+  ) {
+#ifdef CKMI_PHASE_TIMERS
+    unsigned long long ft = __builtin_amdgcn_s_memtime();
+#define PPH(i) do { const unsigned long long f2 = __builtin_amdgcn_s_memtime(); fph[i] += f2 - ft; ft = f2; } while (0)
+#else
+#define PPH(i) (void)0
+#endif
+    constexpr int G = C >> 2, E = C & 3;
+    const int ti = lane & 15, q = lane >> 4;
+    const int k0 = 16 * C + 4 * wo;
+    double* Pb = lds_at<double>(L.xpart) + par * 4 * NC;             // [4 s][NC] P of the panel
+    double* Rb = lds_at<double>(L.xpart) + 8 * NC + wid * 16 * NB;  // [4 s][NB c][4 q] pivot rows, per wave
+    PanHdr* hdr = lds_at<PanHdr>(L.phdr) + par;
+    if (wid == wo) {
+      double x[NB];
+#pragma unroll
+      for (int r = 0; r < NB; ++r) x[r] = a[r][G][E];
+      int ps[4];
+      // column / pivot-row exchange through LDS (one wave-local sync per step instead of ~26
+      // dependent ds_bpermute round trips): xc[r][ti] = column k0 + s, pvb[q] = pivot row
+      double* xc = lds_at<double>(L.gcol);
+      double* pvb = xc + 16 * NB;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (q == s) {
+#pragma unroll
+          for (int r = 0; r < NB; ++r) xc[r * 16 + ti] = x[r];
+        }
+        uint64_t key = 0;
+        if (q == s) {
+#pragma unroll
+          for (int r = 0; r < NB; ++r) {
+            const uint64_t kr =
+                ((uint64_t)__float_as_uint((float)fabs(x[r])) << 32) | (uint32_t)(0xffffffffu - (ti + 16 * r));
+            if (!((pivmask >> r) & 1u) && kr > key) key = kr;
+          }
+        }
+        key = row16_max_u64(key);
+        const uint32_t klo = __builtin_amdgcn_readlane((uint32_t)key, 16 * s);
+        const uint32_t khi = __builtin_amdgcn_readlane((uint32_t)(key >> 32), 16 * s);
+        if (khi == 0u) ok = false;
+        const int p = (int)(0xffffffffu - klo);
+        ps[s] = p;
+        const int tip = p & 15, rp = p >> 4;
+        const bool prow = ti == tip;
+        if (prow) {
+          double vr = x[0];
+#pragma unroll
+          for (int r = 1; r < NB; ++r) vr = r == rp ? x[r] : vr;  // the pivot row's entry of this column
+          pvb[q] = vr;
+        }
+        wave_lds_sync();
+        const double pvq = pvb[q];  // pivot row, this lane's column
+        const double piv = pvb[s];
+        double xs[NB];
+#pragma unroll
+        for (int r = 0; r < NB; ++r) xs[r] = xc[r * 16 + ti];  // column k0 + s, this lane's rows
+        const double rcp = rcp_nr(piv);
+#pragma unroll
+        for (int r = 0; r < NB; ++r) {
+          const double g = (prow && r == rp) ? (piv - 1.0) * rcp : xs[r] * rcp;
+          x[r] = q == s ? ((prow && r == rp) ? rcp : -g) : fma(-g, pvq, x[r]);
+        }
+        wave_lds_sync();  // the next step rewrites xc / pvb
+        if (prow) pivmask |= 1u << rp;
+      }
+      // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
+#pragma unroll
+      for (int r = 0; r < NB; ++r) Pb[q * NC + ti + 16 * r] = x[r];
+      if (lane < 4) {
+        const int pl = lane == 0 ? ps[0] : (lane == 1 ? ps[1] : (lane == 2 ? ps[2] : ps[3]));
+        lds_at<int>(L.perm)[k0 + lane] = pl;
+        lds_at<int>(L.rank)[pl] = k0 + lane;
+        hdr->p[lane] = pl;
+      }
+      if (lane == 0) hdr->ok = ok ? 1 : 0;
+    }
+    PPH(0);
+    __syncthreads();  // the panel's P' and pivots are published
+    PPH(1);
+    int pr[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) pr[s] = __builtin_amdgcn_readfirstlane(hdr->p[s]);
+    if (!__builtin_amdgcn_readfirstlane(hdr->ok)) ok = false;
+    // the 4 pivot rows' entries of this wave's columns (values before the panel), wave-locally
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int tip = pr[s] & 15, rp = pr[s] >> 4;
+      if (ti == tip) pivmask |= 1u << rp;
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        if (r == rp) {  // uniform: one scalar branch selects the register row
+          if (ti == tip) {
+#pragma unroll
+            for (int c = 0; c < NB; ++c) Rb[(s * NB + c) * 4 + q] = a[r][c >> 2][c & 3];
+          }
+          asm volatile("" ::: "memory");
+        }
+      }
+    }
+    wave_lds_sync();
+    // A = U^T (lane: column j = lane & 15 of the group, panel step lane >> 4), B = P'^T
+    double A[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const int j = lane & 15, c = 4 * g + (j >> 2);
+      A[g] = c < NB ? Rb[((lane >> 4) * NB + c) * 4 + (j & 3)] : 0.0;
+    }
+    const int sl = lane >> 4;
+    const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));  // pivot row of step sl
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+      const int i = 16 * rb + (lane & 15);
+      const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
+    }
+    if (wid == wo) {  // the panel columns keep their processed values
+#pragma unroll
+      for (int r = 0; r < NB; ++r) a[r][G][E] = Pb[q * NC + ti + 16 * r];
+    }
+#ifdef CKMI_PHASE_TIMERS
+    {  // the updates have landed before the stamp
+      double chk = 0.0;
+#pragma unroll
+      for (int r = 0; r < NB; ++r) chk += a[r][0][0];
+      if (chk == 12345.678) fph[2] += 1;
+    }
+#endif
+    PPH(2);
+#undef PPH
+  }
+
+#ifdef CKMI_PHASE_TIMERS
+#define FPH_ARG , fph
+#define FPH_PARAM , unsigned long long (&fph)[3]
+#else
+#define FPH_ARG
+#define FPH_PARAM
+#endif
+  template <int C>
+  __device__ __forceinline__ void panels(const BigLds& L, uint32_t& pivmask, bool& ok, int t, int wid, int lane FPH_PARAM) {
+    if constexpr (C < NB) {
+#pragma unroll 1
+      for (int wo = 0; wo < 4; ++wo) panel<C>(L, wo, (C * 4 + wo) & 1, pivmask, ok, t, wid, lane FPH_ARG);
+      panels<C + 1>(L, pivmask, ok, t, wid, lane FPH_ARG);
+    }
+  }
+
+  __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane
+#ifdef CKMI_PHASE_TIMERS
+                                         , unsigned long long (&fph)[3]
+#endif
+  ) {
+    (void)B;
+    const int t = opaque_lane(tid);
+    uint32_t pivmask = 0u;
+    bool ok = true;
+    panels<0>(L, pivmask, ok, t, wid, lane FPH_ARG);
+    return ok;
+  }
+
+  // x = M^-1 b (thread i: component i; b must be 0 for i >= n) -- as BigMatrix::solve
+  __device__ __forceinline__ double solve(double bv, const BigLds& L, int tid, int wid, int lane) const {
+    const int t = opaque_lane(tid);
+    const int ti = lane & 15, q = lane >> 4;
+    double* bp = lds_at<double>(L.bp);
+    double* xp = lds_at<double>(L.xpart);
+    const int* rank = lds_at<const int>(L.rank);
+    const int* perm = lds_at<const int>(L.perm);
+    if (t < NC) {
+      const int j = rank[t];
+      bp[(((j & 15) >> 2) * 4 + (j & 3)) * NBP + (j >> 4)] = bv;
+    }
+    __syncthreads();
+    double pv[NB];
+#pragma unroll
+    for (int c = 0; c < NB; ++c) pv[c] = bp[(wid * 4 + q) * NBP + c];
+    double* xo = xp + ((wid * 4 + q) * 16 + ti) * NBP;
+#pragma unroll
+    for (int r = 0; r < NB; ++r) {
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+      for (int c = 0; c < NB; c += 2) {
+        s0 = fma(a[r][c >> 2][c & 3], pv[c], s0);
+        if (c + 1 < NB) s1 = fma(a[r][(c + 1) >> 2][(c + 1) & 3], pv[c + 1], s1);
+      }
+      xo[r] = s0 + s1;
+    }
+    __syncthreads();
+    if (t >= NC) return 0.0;
+    const int i = perm[t];
+    const double* xi = xp + (i & 15) * NBP + (i >> 4);
+    double s[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+      s[w] = (xi[((w * 4 + 0) * 16) * NBP] + xi[((w * 4 + 1) * 16) * NBP]) +
+             (xi[((w * 4 + 2) * 16) * NBP] + xi[((w * 4 + 3) * 16) * NBP]);
+    return (s[0] + s[1]) + (s[2] + s[3]);
+  }
+};
+
+#ifdef CKMI_BIG_VALU
+template <int NB>
+using BigMat = BigMatrix<NB>;  // one workgroup barrier per column (VALU rank-1 updates)
+#else
+// NB = 12 (177..192 variables) keeps the per-column VALU factorisation: its MFMA form overflows
+// the register file (and crashes the ROCm 7.2 backend with the VGPR-form MFMA option)
+template <int NB>
+using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB>, BigMatrix<NB>>;
+#endif
+
 // ------------------------------------------------------------------ right-hand side
 // f(t, y) for this thread's component (thread 0 = T) and, if with_j, the Jacobian into the
 // workgroup's HBM slot Jg (FP32, column-major, leading dimension NT).  Same formulation as
@@ -688,7 +957,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
   Blk B;
   B.ored = L.red;
   B.phase = 0;
-  BigMatrix<NB> M;
+  BigMat<NB> M;
   BdfT<NT> b;
   b.zn.base = L.zn + tid * 8;
   BdfT<NT> b0;  // component 0 (T): its Nordsieck history, read by every thread
@@ -987,7 +1256,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             {  // s_memtime waits for nothing: force the loads to land before the stamp
               double chk = 0.0;
 #pragma unroll
-              for (int r2 = 0; r2 < NB; ++r2) chk += M.a[r2][0];
+              for (int r2 = 0; r2 < NB; ++r2) chk += M.entry(r2);
               if (chk == 12345.678) bph[5] += 1;
             }
 #endif
@@ -1392,7 +1661,7 @@ BigLds big_layout(const ckmi_mech* m, int NC, int lds_max) {
   const int NBP = (NC / 16 + 1) & ~1;
   L.prow = take(8 * BW * 4 * NBP);
   L.gcol = take(8 * 2 * 16 * NBP);
-  L.phdr = take(2 * 16);
+  L.phdr = take(2 * 32);  // [2] PivHdr (VALU factor) or PanHdr (MFMA factor)
   L.perm = take(4 * NT);
   L.rank = take(4 * NT);
   L.bp = take(8 * 16 * NBP);
@@ -1467,6 +1736,9 @@ int launch_big_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const React
     case 1:
     case 2:
     case 3:
+#ifdef CKMI_BIG_ONLY_NB  // diagnostics: compile one matrix size only (register-usage checks)
+    default: return launch_big_nc<CKMI_BIG_ONLY_NB, false>(m, n, dc, io, stream);
+#else
     case 4: return launch_big_nc<4, false>(m, n, dc, io, stream);
     case 5: return launch_big_nc<5, false>(m, n, dc, io, stream);
     case 6: return launch_big_nc<6, false>(m, n, dc, io, stream);
@@ -1476,6 +1748,7 @@ int launch_big_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const React
     case 10: return launch_big_nc<10, false>(m, n, dc, io, stream);
     case 11: return launch_big_nc<11, false>(m, n, dc, io, stream);
     default: return launch_big_nc<12, false>(m, n, dc, io, stream);
+#endif
   }
 }
 

@@ -48,8 +48,10 @@ def main():
             d["calls_per_step"] = calls[nm].sum() / st[:, 0].sum()
         out["phases"][nm] = d
     fac = ph[:, 3].sum()
-    out["factor_split"] = {"pivot_search_to_barrier1": ph[:, 6].sum() / fac, "publish_to_barrier2": ph[:, 7].sum() / fac,
-                           "update": 1.0 - (ph[:, 6].sum() + ph[:, 7].sum()) / fac,
+    # wave 0's view of the factorisation.  MFMA panels: [owner panel work, barrier wait, rest =
+    # pivot-row gather + MFMA update]; VALU build (CKMI_BIG_VALU): [pivot search, publish, update]
+    out["factor_split"] = {"part0": ph[:, 6].sum() / fac, "part1_barrier": ph[:, 7].sum() / fac,
+                           "rest_update": 1.0 - (ph[:, 6].sum() + ph[:, 7].sum()) / fac,
                            "cycles_per_gj_step": fac / max(calls["factor"].sum(), 1) / (16 * ((m.KK + 16) // 16))}
     other = tot - ph[:, :5].sum()
     out["phases"]["control"] = {"frac_of_total": other / tot, "cycles_per_step": other / st[:, 0].sum()}
