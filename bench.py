@@ -256,7 +256,7 @@ def rop_line(dev, mech, ops, ns, rank, world, cpu_sample, kernel_name="rop_kerne
     torch.cuda.synchronize()
     jit = dm.rop_jit_state() == 1
     if jit:
-        kernel_name, flops_key, traffic_key = "ckjit_rop", "F_rop_jit", traffic_key + "_jit"
+        kernel_name, flops_key, traffic_key = f"ckjit_rop_k{mech.KK}_i{mech.II}", "F_rop_jit", traffic_key + "_jit"
     else:
         flops_key = "F_rop"
     reps = 3

@@ -1272,7 +1272,8 @@ int jit_ready(ckmi_mech* m) {
     return fail(CKMI_ERR_HIP, J.why);
   }
   if (hipModuleLoadData(&J.mod, code.data()) != hipSuccess ||
-      hipModuleGetFunction(&J.fn, J.mod, "ckjit_rop") != hipSuccess) {
+      hipModuleGetFunction(&J.fn, J.mod, ("ckjit_rop_k" + std::to_string(m->KK) + "_i" + std::to_string(m->II)).c_str()) !=
+          hipSuccess) {
     J.state = -1;
     J.why = "hipModuleLoadData / hipModuleGetFunction failed";
     return fail(CKMI_ERR_HIP, J.why);

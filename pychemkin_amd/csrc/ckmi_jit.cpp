@@ -175,7 +175,7 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
   o << "#define CKJ_RU " << lit(1.3806504e-16 * 6.02214179e23) << "\n";  // = ckmi_device.hpp RU
   o << kPrelude;
   o << "extern \"C\" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(" << wpe << ", " << wpe
-    << "))) ckjit_rop(int n, const double* __restrict__ Tv, "
+    << "))) ckjit_rop_k" << KK << "_i" << II << "(int n, const double* __restrict__ Tv, "
        "const double* __restrict__ Pv, const double* __restrict__ Yv, double* __restrict__ wd, "
        "double* __restrict__ cpo, double* __restrict__ ho, const double* __restrict__ prm) {\n";
   o << "  const int s0 = blockIdx.x * 64 + threadIdx.x;\n  const bool live = s0 < n;\n"

@@ -19,7 +19,7 @@ stop_unless_ok() {  # $1 = status, $2 = step name, $3 = allowed non-fatal status
 
 if [[ $STEPS == all || $STEPS == *test* ]]; then
   echo "== pytest -m gpu"
-  timeout -k 10 900 python3 -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_$TAG.log 2>&1
+  timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1
   rc=$?; tail -25 gpurun_out/pytest_gpu_$TAG.log; stop_unless_ok $rc pytest 1
   echo "== smoke"
   timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1

@@ -35,6 +35,16 @@ def main():
     Y = rng.dirichlet(0.5 * np.ones(mech.KK), ns).T.copy()
     dm.rop_thermo(T, P, Y)
     torch.cuda.synchronize()
+    # configs[4] stand-in: a strided sample on the workgroup-per-reactor (MFMA) kernel
+    nb = int(os.environ.get("PMC_BIG_REACTORS", "2048"))
+    if nb > 0:
+        bm = bench.big_mechanism()
+        bdm = _native.DeviceMechanism(bm.to_tables(), device=0)
+        T5, P5, Y5, pr5 = bench.sweep_c5(bm, 1, 0)
+        j = np.arange(0, len(T5), max(1, len(T5) // nb))[:nb]
+        r5 = bdm.reactor_run(_native.make_cfg(**bench.RUN), pr5[j], T5[j], P5[j], np.ones(len(j)), Y5[j])
+        torch.cuda.synchronize()
+        print(f"big reactors {len(j)} failed {int((r5['stats'][:, 6] != 0).sum().item())}")
     print(f"reactors {len(idx)} mean steps {st[:, 0].mean():.1f} failed {(st[:, 6] != 0).sum()}; rop states {ns}")
 
 

@@ -17,7 +17,8 @@ def load(root):
     for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            short = "reactor" if "reactor_kernel" in k else ("rop" if "rop_kernel" in k else k[:40])
+            short = ("big_reactor" if "big_reactor_kernel" in k else "reactor" if "reactor_kernel" in k else
+                     "rop_jit" if "ckjit_rop" in k else "rop" if "rop_kernel" in k else k[:40])
             tot[short][row["Counter_Name"]] += float(row["Counter_Value"])
             disp[short].add((f, row["Dispatch_Id"]))
     return tot, disp
@@ -27,7 +28,7 @@ def main():
     root = sys.argv[1]
     tot, disp = load(root)
     out = {}
-    for k in ("reactor", "rop"):
+    for k in ("reactor", "big_reactor", "rop", "rop_jit"):
         if k not in tot:
             continue
         c = tot[k]
@@ -40,6 +41,8 @@ def main():
             d["valu_insts_per_wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
         f64 = c.get("SQ_INSTS_VALU_FMA_F64", 0) * 2 + c.get("SQ_INSTS_VALU_MUL_F64", 0) + c.get("SQ_INSTS_VALU_ADD_F64", 0)
         d["fp64_flops_counted"] = f64 * 64
+        if "SQ_INSTS_VALU_MFMA_F64" in c:  # every f64 MFMA here is 16x16x4: 1024 FMA = 2048 FLOP per wave instr
+            d["mfma_f64_flops_from_insts"] = c["SQ_INSTS_VALU_MFMA_F64"] * 2048
         if "FETCH_SIZE" in c:
             d["fetch_bytes_x2_calibrated"] = c["FETCH_SIZE"] * 1024 * 2
         if "WRITE_SIZE" in c:

@@ -1,5 +1,7 @@
 """Per-launch HBM bytes of the reactor and ROP kernels from scripts/pmc_traffic.sh output.
 
+    python scripts/traffic_summary.py gpurun_out/traffic_TAG [--c4]   (--c4: a run of the c4 line only)
+
 FETCH_SIZE (KiB) is doubled per the gfx950 calibration (MI355X_MICROARCH.md, HBM section: it
 tallies 128-B requests at 64 B); WRITE_SIZE (KiB) is taken as is.  Output: profiles/traffic.json
 format, {"reactor": {...}, "rop": {...}}, averaged over the dispatches of each kernel.
@@ -15,15 +17,20 @@ import sys
 
 def main():
     root = sys.argv[1]
+    # reactor_kernel dispatches of a run belong to one line: c3 (default) or c4 (--c4)
+    reactor_key = "reactor_c4" if "--c4" in sys.argv else "reactor"
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     grid = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         per = collections.defaultdict(float)
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
-            kind = ("reactor" if "reactor_kernel" in k else
-                    "rop" if re.search(r"rop_kernel<0, 1[,>]", k) else        # GRI-3.0 (KK <= 63)
-                    "rop_161sp" if re.search(r"rop_kernel<0, 3[,>]", k) else  # synthetic 161-species mechanism
+            kind = ("big_reactor" if "big_reactor_kernel" in k else            # configs[4] (c5 line)
+                    reactor_key if re.search(r"(^|[^_])reactor_kernel", k) else  # configs[2] / [3] (c3 / c4)
+                    "rop" if re.search(r"rop_kernel<0, 1[,>]", k) else        # GRI-3.0 (KK <= 63), generic
+                    "rop_161sp" if re.search(r"rop_kernel<0, 3[,>]", k) else  # synthetic 161-species, generic
+                    "rop_jit" if "ckjit_rop_k53_" in k else                   # specialised kernels
+                    "rop_161sp_jit" if "ckjit_rop_k161_" in k else
                     "lu" if "lu_factor_kernel" in k else None)
             if kind is None:
                 continue
@@ -32,17 +39,21 @@ def main():
             acc[kind][cname].append(v)
     out = {}
     for kind, c in acc.items():
+        if kind == "reactor_c4":  # the c4 run's tiny headline dispatches are dropped: largest dispatch only
+            fetch = 2.0 * 1024 * max(c["FETCH_SIZE"])
+            write = 1024 * max(c["WRITE_SIZE"])
+            out[kind] = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write, "dispatches": 1}
+            continue
         fetch = 2.0 * 1024 * sum(c["FETCH_SIZE"]) / max(len(c["FETCH_SIZE"]), 1)
         write = 1024 * sum(c["WRITE_SIZE"]) / max(len(c["WRITE_SIZE"]), 1)
         out[kind] = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
                      "dispatches": len(c["FETCH_SIZE"])}
     # units per launch of the bench workload (bench.py defaults)
-    if "reactor" in out:
-        out["reactor"]["units"] = 65536
-    if "rop" in out:
-        out["rop"]["units"] = 10_000_000
-    if "rop_161sp" in out:
-        out["rop_161sp"]["units"] = 1_000_000
+    units = {"reactor": 65536, "reactor_c4": 2 ** 20, "big_reactor": 262144, "rop": 10_000_000, "rop_jit": 10_000_000,
+             "rop_161sp": 1_000_000, "rop_161sp_jit": 1_000_000}
+    for k, u in units.items():
+        if k in out:
+            out[k]["units"] = u
     if "lu" in out:
         out["lu"]["units"] = 16384
     print(json.dumps(out, indent=1))

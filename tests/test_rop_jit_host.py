@@ -7,7 +7,7 @@ from pychemkin_amd import _native
 
 def test_generated_source_covers_every_reaction_and_species(tables, mech):
     src = _native.rop_jit_source(tables)
-    assert 'extern "C" __global__' in src and "ckjit_rop" in src
+    assert 'extern "C" __global__' in src and f"ckjit_rop_k{mech.KK}_i{mech.II}(" in src
     for i in range(mech.II):
         assert f"// reaction {i + 1}\n" in src
     for k in range(mech.KK):
