@@ -4,6 +4,7 @@ from __future__ import annotations
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "ckmi.hip")        # kinetics, thermo and reactor kernels + C ABI
@@ -70,22 +71,26 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     if not force and default and not needs_build():
         return OUT
     os.makedirs(OBJ_DIR, exist_ok=True)
+    jobs = []  # (src, obj, flags): independent translation units, compiled concurrently
     lu_obj = os.path.join(OBJ_DIR, "ckmi_lu.o")
     if force or _stale(lu_obj, [LU_SRC, DEPS[-1]]):
-        _compile(LU_SRC, lu_obj, LU_FLAGS, verbose)
+        jobs.append((LU_SRC, lu_obj, LU_FLAGS))
     big_obj = os.path.join(OBJ_DIR, "ckmi_big.o" if default else f"ckmi_big_{'prof' if prof else 'main'}.o")
     if force or _stale(big_obj, [BIG_SRC] + DEPS):
-        _compile(BIG_SRC, big_obj, BIG_FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []), verbose)
+        jobs.append((BIG_SRC, big_obj, BIG_FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else [])))
     kin_obj = os.path.join(OBJ_DIR, "ckmi_kin.o")
     if force or _stale(kin_obj, [KIN_SRC] + DEPS):
-        _compile(KIN_SRC, kin_obj, KIN_FLAGS, verbose)
+        jobs.append((KIN_SRC, kin_obj, KIN_FLAGS))
     jit_obj = os.path.join(OBJ_DIR, "ckmi_jit.o")
     if force or _stale(jit_obj, [JIT_SRC] + DEPS):
-        _compile(JIT_SRC, jit_obj, KIN_FLAGS, verbose)
+        jobs.append((JIT_SRC, jit_obj, KIN_FLAGS))
     tag = "main" if default else os.path.splitext(os.path.basename(out))[0]
     main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
     if force or (not default and not prof) or _stale(main_obj, [SRC] + DEPS):
-        _compile(SRC, main_obj, FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(extra), verbose)
+        jobs.append((SRC, main_obj, FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(extra)))
+    with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), os.cpu_count() or 1))) as pool:
+        for f in [pool.submit(_compile, s, o, fl, verbose) for s, o, fl in jobs]:
+            f.result()
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj, kin_obj, jit_obj,
            "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:

@@ -443,7 +443,11 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
           const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
           // each lane reads back only the J entries it wrote itself (same-address order)
+#if defined(CKMI_NEWTON_F32)
+          M.build(Jg, WAVE, S.gamma, lane, n, b.ewt, L.base + 32 * VL);
+#elif !defined(CKMI_NEWTON_F32S)
           M.build(Jg, WAVE, S.gamma, lane, n);
+#endif
 #ifdef CKMI_PHASE_TIMERS
           {
             // build (J reload from HBM) timed separately; s_memtime waits for the loads
@@ -454,8 +458,10 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
             if (lane == 0) phs[20] += __builtin_amdgcn_s_memtime() - t0;
           }
 #endif
-#ifdef CKMI_NEWTON_LU
+#if defined(CKMI_NEWTON_LU)
           const bool ok = M.factor(lane, n);
+#elif defined(CKMI_NEWTON_F32S)
+          const bool ok = M.build_factor(Jg, WAVE, S.gamma, lane, n, L.base + 32 * VL);
 #else
           const bool ok = M.factor(lane, n, L.base + 32 * VL);  // the dwdT row of the slice (free here)
 #endif

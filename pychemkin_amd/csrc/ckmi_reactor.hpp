@@ -354,7 +354,122 @@ __device__ __forceinline__ double bpermute(int src_lane, double v) {
   return __hiloint2double(hi, lo);
 }
 
-#ifndef CKMI_NEWTON_LU
+#if defined(CKMI_NEWTON_F32)
+// Gauss-Jordan inverse held in FP32 (N floats per lane instead of N doubles).  The modified
+// Newton iteration only needs an approximate M^-1 -- M is rebuilt from the FP32-parked Jacobian
+// and a gamma that lags by up to DGMAX -- so the factorisation runs in FP32 (half the VALU cost
+// and half the registers of the FP64 form); the right-hand side and the correction stay FP64.
+// M is equilibrated with the error weights first, M~ = D M D^-1 with D = diag(ewt): in the
+// weighted variables of the convergence test every entry has its natural scale (T against
+// trace species span ~1e14 unscaled), the pivot search compares like with like, and the FP32
+// rounding of M~^-1 is uniform in the norm the Newton iteration is judged in.
+template <int N>
+struct NewtonMatrix {
+  float a[N];
+  int permv;  // lane k: the lane whose row was the pivot of step k
+  float dl;   // this lane's scale d_i (ewt at factorisation time; 1 on inactive lanes)
+
+  // orow: LDS byte offset of an N-float scratch row of the calling wave (16-byte aligned)
+  __device__ __forceinline__ void build(const float* J, int ldj, double gamma, int lane_in, int n, double ewt,
+                                        int orow) {
+    const int lane = opaque_lane(lane_in);
+    dl = (lane < n && ewt > 0.0) ? (float)ewt : 1.0f;
+    float* rdv = lds_at<float>(__builtin_amdgcn_readfirstlane(opaque_lane(orow)));
+    if (lane < N) rdv[lane] = 1.0f / dl;
+    wave_lds_sync();
+    const float gf = (float)gamma;
+    constexpr int NQ = (N + 3) / 4;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const float4 r = reinterpret_cast<const float4*>(rdv)[q];
+      const float rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = 4 * q + u;
+        if (j < N) a[j] = ((j == lane ? 1.0f : 0.0f) - gf * J[j * ldj + lane]) * (dl * rv[u]);
+      }
+    }
+    wave_lds_sync();  // the scratch row is the pivot row of factor()
+  }
+
+  __device__ __forceinline__ bool factor(int lane_in, int n, int orow) {
+    const int lane = opaque_lane(lane_in);
+    bool pivoted = lane >= N;
+    permv = lane;
+    bool ok = true;
+    float4* row = lds_at<float4>(__builtin_amdgcn_readfirstlane(opaque_lane(orow)));
+    constexpr int NQ = (N + 3) / 4;  // float4 groups per row
+    uint32_t v0 = pivoted ? 0u : __float_as_uint(fabsf(a[0]));
+    uint32_t vmax = wave_max_u32(v0);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      if (vmax == 0u) ok = false;
+      const uint64_t mask = __ballot(!pivoted && v0 == vmax);
+      const int p = uni(mask ? (int)__ffsll((unsigned long long)mask) - 1 : 0);
+      const bool me = lane == p;
+      if (me) {
+#pragma unroll
+        for (int j = 0; j < NQ; ++j)
+          row[j] = make_float4(a[4 * j], 4 * j + 1 < N ? a[4 * j + 1] : 0.0f, 4 * j + 2 < N ? a[4 * j + 2] : 0.0f,
+                               4 * j + 3 < N ? a[4 * j + 3] : 0.0f);
+      }
+      wave_lds_sync();
+      const float piv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(a[k]), p));
+      float rp = __builtin_amdgcn_rcpf(piv);
+      rp = fmaf(rp, fmaf(-piv, rp, 1.0f), rp);
+      if (me) pivoted = true;
+      if (lane == k) permv = p;
+      const float g = me ? (piv - 1.0f) * rp : a[k] * rp;
+      const float ak = me ? rp : -g;
+      const int Q0 = (k + 1 < N ? k + 1 : k) / 4;  // the group holding column k+1 goes first
+      uint32_t w = 0u;
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) {
+        const int Q = (Q0 + t) % NQ;
+        const float4 r = row[Q];
+        const float rv[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int j = 4 * Q + u;
+          if (j < N && j != k) a[j] = fmaf(-g, rv[u], a[j]);
+        }
+        if (k + 1 < N) {
+          if (t == 0) {
+            v0 = pivoted ? 0u : __float_as_uint(fabsf(a[k + 1]));
+            w = v0;
+          }
+          if (t == 1) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_QUAD_1032, 0xf, 0xf, false));
+          if (t == 3) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_QUAD_2301, 0xf, 0xf, false));
+          if (t == 5) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false));
+          if (t == 7) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_ROW_MIRROR, 0xf, 0xf, false));
+          if (t == 9) {
+            const uint32_t r0 = __builtin_amdgcn_readlane(w, 0), r1 = __builtin_amdgcn_readlane(w, 16);
+            const uint32_t r2 = __builtin_amdgcn_readlane(w, 32), r3 = __builtin_amdgcn_readlane(w, 48);
+            vmax = max(max(r0, r1), max(r2, r3));
+          }
+        }
+        if (t % 2 == 1) asm volatile("" ::: "memory");
+      }
+      a[k] = ak;
+    }
+    return ok;
+  }
+
+  // x = M^-1 b = D^-1 M~^-1 D b (lane k: component k); FP64 accumulation of the FP32 inverse
+  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
+    const int lane = opaque_lane(lane_in);
+    if (lane >= n) b = 0.0;
+    const double bp = bpermute(permv, b * (double)dl);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      s0 = fma((double)a[j], bcast(bp, j), s0);
+      if (j + 1 < N) s1 = fma((double)a[j + 1], bcast(bp, j + 1), s1);
+    }
+    return bpermute(permv, s0 + s1) / (double)dl;
+  }
+};
+#elif !defined(CKMI_NEWTON_LU)
 #ifndef CKMI_GJ_BATCH
 #define CKMI_GJ_BATCH 4  // row pairs read per batch in the elimination
 #endif
@@ -366,7 +481,7 @@ __device__ __forceinline__ double bpermute(int src_lane, double v) {
 // FMAs at factor time, paid back within one solve (1.5 solves per factorisation on average
 // is the minimum; the bench workload does 11).
 template <int N>
-struct NewtonMatrix {
+struct NewtonMatrixGJ64 {
   double a[N];
   int permv;  // lane k: the lane whose row was the pivot of step k
 
@@ -461,6 +576,41 @@ struct NewtonMatrix {
     return bpermute(permv, s0 + s1);
   }
 };
+#ifdef CKMI_NEWTON_F32S
+// The FP64 Gauss-Jordan inverse above, stored in FP32 between factorisations: the factorisation
+// itself keeps FP64 (its N doubles are live only inside ST_SETUP), the inverse that stays in
+// registers across the RHS evaluations takes N VGPRs instead of 2N.
+template <int N>
+struct NewtonMatrix {
+  float a[N];
+  int permv;
+  template <typename TJ>
+  __device__ __forceinline__ bool build_factor(const TJ* J, int ldj, double gamma, int lane, int n, int orow) {
+    NewtonMatrixGJ64<N> m;
+    m.build(J, ldj, gamma, lane, n);
+    const bool ok = m.factor(lane, n, orow);
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = (float)m.a[j];
+    permv = m.permv;
+    return ok;
+  }
+  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
+    const int lane = opaque_lane(lane_in);
+    if (lane >= n) b = 0.0;
+    const double bp = bpermute(permv, b);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      s0 = fma((double)a[j], bcast(bp, j), s0);
+      if (j + 1 < N) s1 = fma((double)a[j + 1], bcast(bp, j + 1), s1);
+    }
+    return bpermute(permv, s0 + s1);
+  }
+};
+#else
+template <int N>
+using NewtonMatrix = NewtonMatrixGJ64<N>;
+#endif
 #else
 template <int N>
 struct NewtonMatrix {

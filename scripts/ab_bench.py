@@ -28,8 +28,16 @@ dm.reactor_run(cfg, *args); torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(); res = dm.reactor_run(cfg, *args); e1.record(); torch.cuda.synchronize()
 st = res["stats"].cpu().numpy()
-print(json.dumps({"ms": e0.elapsed_time(e1), "steps": float(st[:, 0].mean()), "fail": int((st[:, 6] != 0).sum()),
-                  "tau0": float(res["tau"][0].item())}))
+tau = res["tau"].cpu().numpy()
+ref = os.environ.get("AB_TAU_REF")
+d = {"ms": e0.elapsed_time(e1), "mean_stats": [round(float(x), 3) for x in st.mean(axis=0)],
+     "fail": int((st[:, 6] != 0).sum()), "tau0": float(tau[0])}
+if ref and os.path.exists(ref):
+    t0 = np.load(ref)
+    d["tau_max_rel_vs_ref"] = float(np.max(np.abs(tau - t0) / np.abs(t0)))
+elif ref:
+    np.save(ref, tau)
+print(json.dumps(d))
 """
 
 ROP_CHILD = r"""
@@ -66,7 +74,8 @@ def main():
     out = {lib: [] for lib in libs}
     for _ in range(reps):
         for lib in libs:
-            env = dict(os.environ, CKMI_LIB=os.path.abspath(lib))
+            env = dict(os.environ, CKMI_LIB=os.path.abspath(lib),
+                       AB_TAU_REF=os.path.join(ROOT, "gpurun_out", "ab_tau_%s.npy" % os.path.basename(libs[0])))
             r = subprocess.run([sys.executable, "-c", (ROP_CHILD if rop else CHILD) % (ROOT, n)], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
