@@ -84,6 +84,8 @@ typedef struct {
   const double* eff_val;  /* third-body efficiencies (absolute) */
   const int32_t* plog_ptr; /* [II+1] CSR into plog_par for CKMI_RXN_PLOG reactions (may be NULL if none) */
   const double* plog_par;  /* [npl][4] ln P (dyn/cm2), ln A (cgs), b, E/R (K); ascending, distinct P */
+  const double* ford;      /* [II][4] forward order of each reactant slot (FORD; = rnu without it), or NULL */
+  const double* rord;      /* [II][4] reverse order of each product slot (RORD; = pnu without it), or NULL */
 } ckmi_mech_desc;
 
 typedef struct ckmi_mech ckmi_mech; /* opaque: tables resident in HBM of one device */
@@ -216,8 +218,10 @@ int ckmi_reactor_run_ex(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int3
                         void* stream);
 
 /* Reactor kernel selection (diagnostic / testing): 0 = automatic (one wave per reactor for KK + 1 <= 64,
- * one 4-wave workgroup per reactor above, up to KK + 1 = 192), 1 = the workgroup-per-reactor kernel for
- * every mechanism (lets tests run both integrators on the same GRI-3.0 reactors).  Process-wide. */
+ * its Newton inverse stored in FP32 unless rtol < 1e-9; one 4-wave workgroup per reactor above, up to
+ * KK + 1 = 192), 1 = the workgroup-per-reactor kernel for every mechanism (lets tests run both
+ * integrators on the same GRI-3.0 reactors), 2 / 3 = the wave kernel with the FP64 / FP32-stored
+ * Newton inverse whatever the tolerances.  Process-wide. */
 int ckmi_set_reactor_path(int32_t path);
 
 /* Batched dense LU of Newton iteration matrices too large for one wave (mechanisms with more

@@ -35,11 +35,30 @@ void cko_thermo(const cko_mech* m, double T, double* cp_R, double* h_RT, double*
   }
 }
 
-static double powi_nu(double c, double nu) {
-  if (nu == 1.0) return c;
-  if (nu == 2.0) return c * c;
-  if (nu == 3.0) return c * c * c;
-  return pow(c, nu);
+/* C^o for a reaction order o (stoichiometric coefficient, or FORD / RORD): exact products for
+ * o = 0..3; otherwise pow(C, o) for C > 0 and 0 for C <= 0 (a real power of a negative
+ * concentration is undefined; the device kernels use the same rule) */
+static double conc_pow(double c, double o) {
+  if (o == 0.0) return 1.0;
+  if (o == 1.0) return c;
+  if (o == 2.0) return c * c;
+  if (o == 3.0) return c * c * c;
+  return c > 0.0 ? pow(c, o) : 0.0;
+}
+/* d C^o / dC under the same rule (0 for C <= 0 at a non-integral order) */
+static double dconc_pow(double c, double o) {
+  if (o == 0.0) return 0.0;
+  if (o == 1.0) return 1.0;
+  if (o == 2.0) return 2.0 * c;
+  if (o == 3.0) return 3.0 * c * c;
+  return c > 0.0 ? o * pow(c, o - 1.0) : 0.0;
+}
+/* order of reactant slot s / product slot s of reaction i */
+static double ford_of(const cko_mech* m, int i, int s) {
+  return m->ford ? m->ford[CKO_SLOTS * i + s] : m->rnu[CKO_SLOTS * i + s];
+}
+static double rord_of(const cko_mech* m, int i, int s) {
+  return m->rord ? m->rord[CKO_SLOTS * i + s] : m->pnu[CKO_SLOTS * i + s];
 }
 
 /* Per-reaction kinetics at (T, C[]).  Returns kf_eff (incl. falloff), kr_eff, the
@@ -145,8 +164,8 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
     }
   }
   double pf = 1.0, pr = 1.0;
-  for (int s = 0; s < m->nr[i]; ++s) pf *= powi_nu(C[m->rsp[CKO_SLOTS * i + s]], m->rnu[CKO_SLOTS * i + s]);
-  for (int s = 0; s < m->np[i]; ++s) pr *= powi_nu(C[m->psp[CKO_SLOTS * i + s]], m->pnu[CKO_SLOTS * i + s]);
+  for (int s = 0; s < m->nr[i]; ++s) pf *= conc_pow(C[m->rsp[CKO_SLOTS * i + s]], ford_of(m, i, s));
+  for (int s = 0; s < m->np[i]; ++s) pr *= conc_pow(C[m->psp[CKO_SLOTS * i + s]], rord_of(m, i, s));
   /* GFAC scales forward and reverse rates alike */
   e->kf = kf * gfac; e->kr = kr * gfac; e->mfac = mfac; e->pf = pf; e->pr = pr; e->dlkf = dlkf; e->dlkr = dlkr;
 }
@@ -302,8 +321,8 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
     double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
     if (conp) {
       double ordf = 0.0, ordr = 0.0;
-      for (int s = 0; s < m->nr[i]; ++s) ordf += rn[s];
-      for (int s = 0; s < m->np[i]; ++s) ordr += pn[s];
+      for (int s = 0; s < m->nr[i]; ++s) ordf += ford_of(m, i, s);
+      for (int s = 0; s < m->np[i]; ++s) ordr += rord_of(m, i, s);
       dqdT -= e.mfac * (ordf * e.kf * e.pf - ordr * e.kr * e.pr) * invT;
       if (m->rtype[i] == 1) dqdT -= q * invT;
     }
@@ -313,13 +332,14 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
     for (int side = 0; side < 2; ++side) {
       const int nsl = side == 0 ? m->nr[i] : m->np[i];
       const int* sp = side == 0 ? rs : ps;
-      const double* nu = side == 0 ? rn : pn;
+      double ord[CKO_SLOTS];
+      for (int s = 0; s < nsl; ++s) ord[s] = side == 0 ? ford_of(m, i, s) : rord_of(m, i, s);
       const double kk = side == 0 ? e.mfac * e.kf : -e.mfac * e.kr;
       if (kk == 0.0) continue;
       for (int s = 0; s < nsl; ++s) {
-        double d = nu[s] * powi_nu(C[sp[s]], nu[s] - 1.0);
+        double d = dconc_pow(C[sp[s]], ord[s]);
         for (int u = 0; u < nsl; ++u)
-          if (u != s) d *= powi_nu(C[sp[u]], nu[u]);
+          if (u != s) d *= conc_pow(C[sp[u]], ord[u]);
         const double dq = kk * d;
         const int j = sp[s];
         const double wj = 1.0 / m->wt[j];

@@ -39,6 +39,8 @@ typedef struct {
   const int* eff_ptr; const int* eff_sp; const double* eff_val;
   const int* plog_ptr;   /* [II+1] CSR into plog_par (rtype 3) */
   const double* plog_par;/* [npl][4]: ln P (dyn/cm2), ln A (cgs), b, E/R; ascending P per reaction */
+  const double* ford;    /* [II][4] forward order of each reactant slot (FORD; = rnu without it), or NULL */
+  const double* rord;    /* [II][4] reverse order of each product slot (RORD; = pnu without it), or NULL */
 } cko_mech;
 
 typedef struct {

@@ -16,6 +16,15 @@ RU = BOLTZMANN * AVOGADRO
 PATM = 1.01325e6
 
 
+def _cpow(C, o):
+    """C ** o elementwise; a non-integral order of a concentration <= 0 gives 0 (the rule of
+    oracle/ckoracle.c conc_pow and of the device kernels)."""
+    with np.errstate(invalid="ignore", divide="ignore"):
+        r = np.power(C, o)
+    frac = o != np.round(o)
+    return np.where(frac & (C <= 0.0), 0.0, r)
+
+
 class NumpyKinetics:
     def __init__(self, tables):
         t = tables
@@ -25,11 +34,18 @@ class NumpyKinetics:
         self.th = t["thermo"]
         self.nuf = np.zeros((II, KK))
         self.nur = np.zeros((II, KK))
+        # concentration exponents: FORD / RORD where given, else the stoichiometric coefficients
+        self.ordf = np.zeros((II, KK))
+        self.ordr = np.zeros((II, KK))
+        ford = t.get("ford", t["rnu"])
+        rord = t.get("rord", t["pnu"])
         for i in range(II):
             for s in range(int(t["nr"][i])):
                 self.nuf[i, t["rsp"][i, s]] += t["rnu"][i, s]
+                self.ordf[i, t["rsp"][i, s]] += ford[i, s]
             for s in range(int(t["np"][i])):
                 self.nur[i, t["psp"][i, s]] += t["pnu"][i, s]
+                self.ordr[i, t["psp"][i, s]] += rord[i, s]
         self.dnu_mat = self.nur - self.nuf
         self.arr = t["arr"]
         self.low = t["low"]
@@ -100,8 +116,8 @@ class NumpyKinetics:
         kr_rev = np.exp(self.revp[:, 0] + self.revp[:, 1] * np.log(T) - self.revp[:, 2] / T)
         kr_rev = np.where(fo, kr_rev * kf / kinf, kr_rev)
         kr = np.where(self.rev, np.where(self.has_rev, kr_rev, kf / Kc), 0.0)
-        pf = np.prod(C[None, :] ** self.nuf, axis=1)
-        pr = np.prod(C[None, :] ** self.nur, axis=1)
+        pf = np.prod(_cpow(C[None, :], self.ordf), axis=1)
+        pr = np.prod(_cpow(C[None, :], self.ordr), axis=1)
         qf = mfac * kf * pf
         qr = mfac * kr * pr
         wdot = self.dnu_mat.T @ (qf - qr)

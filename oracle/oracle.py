@@ -43,7 +43,7 @@ class _Mech(ct.Structure):
     _fields_ = [("KK", ct.c_int), ("II", ct.c_int)] + [
         (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
                           "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val",
-                          "plog_ptr", "plog_par")
+                          "plog_ptr", "plog_par", "ford", "rord")
     ]
 
 

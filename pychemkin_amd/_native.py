@@ -38,7 +38,7 @@ class MechDesc(ct.Structure):
     _fields_ = [("KK", ct.c_int32), ("II", ct.c_int32)] + [
         (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
                           "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val",
-                          "plog_ptr", "plog_par")
+                          "plog_ptr", "plog_par", "ford", "rord")
     ]
 
 
@@ -368,8 +368,10 @@ class DeviceMechanism:
 
 
 def set_reactor_path(path: int) -> None:
-    """0: automatic (wave per reactor for KK + 1 <= 64, workgroup per reactor above); 1: the
-    workgroup-per-reactor kernel for every mechanism (testing both integrators on one mechanism)."""
+    """0: automatic (wave per reactor for KK + 1 <= 64 -- Newton inverse stored in FP32 unless
+    rtol < 1e-9 -- workgroup per reactor above); 1: the workgroup-per-reactor kernel for every
+    mechanism (testing both integrators on one mechanism); 2 / 3: the wave kernel with the FP64 /
+    FP32-stored Newton inverse whatever the tolerances."""
     _check(lib().ckmi_set_reactor_path(int(path)), "ckmi_set_reactor_path")
 
 

@@ -93,12 +93,14 @@ __host__ __device__ constexpr int jscratch_bytes() {
 // to oracle/ckoracle.c) is written as a wave-uniform state machine whose only RHS evaluation,
 // LU factorisation and triangular solve each appear ONCE in the loop: the LU factors of
 // M = I - gamma J then stay in VGPRs for the life of the wave without spilling.
-#ifndef CKMI_RWAVES
-#define CKMI_RWAVES 8
-#endif
-constexpr int RWAVES = CKMI_RWAVES;
-template <int N, bool PL = false>  // PL: the mechanism has PLOG reactions
-__global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, const DevCfg* __restrict__ dcfg,
+// Waves per workgroup by Newton-matrix form: 12 (3 per SIMD) with the FP32-stored inverse, whose
+// 54 VGPRs leave room for a third wave per SIMD within 168 VGPRs (+16 % reactors/s on configs[2]
+// over 8 waves with the FP64 inverse, MI355X; the FP64 factorisation phase spills ~180 VGPRs to
+// scratch, outside the RHS); 8 (2 per SIMD) with the FP64 inverse (256 VGPRs).
+__host__ __device__ constexpr int rwaves(bool f64) { return f64 ? 8 : 12; }
+// PL: the mechanism has PLOG / chemically activated / general reactions; F64: FP64-stored inverse
+template <int N, bool PL = false, bool F64 = false>
+__global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage img, const DevCfg* __restrict__ dcfg,
                                                                int nreact, int* __restrict__ queue,
                                                                double* __restrict__ jws, ReactorIO io) {
   const ckmi_reactor_cfg* __restrict__ cfg = &dcfg->c;
@@ -119,6 +121,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
   // the wave's parked Jacobian, rounded to FP32: M = I - gamma J is rebuilt from it at every
   // setup (5.6 per J); the modified Newton iteration only needs an approximate M, and half
   // the bytes keep the slots of an XCD's 256 waves (3.5 MB) within its 4 MB L2
+  constexpr int RWAVES = rwaves(F64);
   float* Jg = reinterpret_cast<float*>(jws) + ((size_t)blockIdx.x * RWAVES + wid) * N * WAVE;
   const int KK = V.KK;
   const int n = KK + 1;
@@ -127,7 +130,7 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
   // per-reactor constants of the RHS: in LDS, not registers (the Newton matrix owns those)
   RunCtx& R = *lds_at<RunCtx>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)));
   R.cfg = cfg;
-  NewtonMatrix<N> M;
+  std::conditional_t<F64, NewtonMatrixGJ64<N>, NewtonMatrixF32S<N>> M;
   Bdf b;
   b.zn.base = oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)) +
               align16((int)sizeof(RunCtx)) + lane * 8;
@@ -442,29 +445,9 @@ __global__ __launch_bounds__(RWAVES* WAVE) void reactor_kernel(MechImage img, co
 #ifdef CKMI_PHASE_TIMERS
           const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-          // each lane reads back only the J entries it wrote itself (same-address order)
-#if defined(CKMI_NEWTON_F32)
-          M.build(Jg, WAVE, S.gamma, lane, n, b.ewt, L.base + 32 * VL);
-#elif !defined(CKMI_NEWTON_F32S)
-          M.build(Jg, WAVE, S.gamma, lane, n);
-#endif
-#ifdef CKMI_PHASE_TIMERS
-          {
-            // build (J reload from HBM) timed separately; s_memtime waits for the loads
-            double chk = 0.0;
-#pragma unroll
-            for (int j = 0; j < N; ++j) chk += M.a[j];
-            if (lane == 0 && chk == 12345.678) phs[21] += 1;
-            if (lane == 0) phs[20] += __builtin_amdgcn_s_memtime() - t0;
-          }
-#endif
-#if defined(CKMI_NEWTON_LU)
-          const bool ok = M.factor(lane, n);
-#elif defined(CKMI_NEWTON_F32S)
+          // each lane reads back only the J entries it wrote itself (same-address order); the
+          // dwdT row of the slice (free here) is the pivot-row scratch
           const bool ok = M.build_factor(Jg, WAVE, S.gamma, lane, n, L.base + 32 * VL);
-#else
-          const bool ok = M.factor(lane, n, L.base + 32 * VL);  // the dwdT row of the slice (free here)
-#endif
 #ifdef CKMI_PHASE_TIMERS
           ph[PH_LU] += __builtin_amdgcn_s_memtime() - t0;
 #endif
@@ -954,6 +937,23 @@ __global__ __launch_bounds__(rop_waves(NCH)* WAVE) void rop_kernel(MechImage img
         const int i = base + lane;
         const uint32_t inf = V.info()[i];
         const int nr = rx_nr(inf), np = rx_np(inf);
+        if constexpr (PL) {
+          if (inf & RX_GEN) {  // FORD / RORD / non-integral coefficients
+            const double* g;
+            const Rxn e = eval_gen_img(V, i, inf, T, lnT, invT, lnPRT, P, C, gRT, gRT, Mg, false, -1, 0.0, 1.0, g);
+            const double qf = e.mfac * e.kf * e.pf, qr = e.mfac * e.kr * e.pr;
+            if (MODE == 1) {
+              const int oi = orig[i];
+              o0[(size_t)oi * nstate + st] = qf;
+              o1[(size_t)oi * nstate + st] = qr;
+            } else {
+              const double q = qf - qr;
+              for (int u = 0; u < (int)g[0]; ++u) atomicAdd(&wdot[(int)g[2 + 3 * u]], -g[3 + 3 * u] * q);
+              for (int u = 0; u < (int)g[1]; ++u) atomicAdd(&wdot[(int)g[14 + 3 * u]], g[15 + 3 * u] * q);
+            }
+            continue;
+          }
+        }
         if (nr + np == 0) continue;
         const uint32_t rs = V.rsp()[i], ps = V.psp()[i];
         const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, 0u, T, lnT, invT, lnPRT, P, C, gRT, gRT, Mg, false);
@@ -1053,15 +1053,16 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     uint32_t a = 0, b = 0, nu = 0;
     const int* r4 = &rsp[s].x;
     const int* p4 = &psp[s].x;
+    const bool gen = (flags[s] & RX_GEN) != 0;  // real coefficients: no unit slots, aux stream
     // unit-coefficient slots: a species with coefficient c occupies c slots
     int ns_r = 0, ns_p = 0;
-    for (int u = 0; u < nr; ++u) {
+    for (int u = 0; u < nr && !gen; ++u) {
       const int c = (int)rnu[u * IIp + s];
       nu |= (uint32_t)std::min(c, 15) << (4 * u);
       for (int k = 0; k < c; ++k, ++ns_r)
         if (ns_r < 4) a |= (uint32_t)r4[u] << (8 * ns_r);
     }
-    for (int u = 0; u < np; ++u) {
+    for (int u = 0; u < np && !gen; ++u) {
       const int c = (int)pnu[u * IIp + s];
       nu |= (uint32_t)std::min(c, 15) << (16 + 4 * u);
       for (int k = 0; k < c; ++k, ++ns_p)
@@ -1076,7 +1077,8 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     unu[s] = nu;
     const int fl = flags[s];
     const int type = fl & 3;
-    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10) | (uint32_t)(fl & 0x2000);
+    uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10) | (uint32_t)(fl & 0x2000) |
+                   (uint32_t)(fl & RX_GEN);
     if (slots[s] >= 0 && type == CKMI_RXN_PLOG) {
       // PLOG stream: npts, then (ln P, ln A, b, E/R) per point, over ceil((1 + 4 npts) / AUXW) records
       const int i = slots[s], p0 = d->plog_ptr[i], n = d->plog_ptr[i + 1] - p0;
@@ -1086,7 +1088,7 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
       aux.insert(aux.end(), rec.begin(), rec.end());
       inf |= (uint32_t)naux << 16;
       naux += (int)rec.size() / AUXW;
-    } else if (slots[s] >= 0 && (type == 2 || (fl & 8))) {
+    } else if (slots[s] >= 0 && (type == 2 || (fl & 8) || gen)) {
       double rec[AUXW] = {lnA0[s], beta0[s], Ea0[s], fp[0 * IIp + s], fp[1 * IIp + s], fp[2 * IIp + s],
                           fp[3 * IIp + s], fp[4 * IIp + s], rlnA[s], rbeta[s], rEa[s], 0.0};
       const int ft = (fl >> 4) & 7;
@@ -1099,6 +1101,22 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
       aux.insert(aux.end(), rec, rec + AUXW);
       inf |= (uint32_t)naux << 16;
       ++naux;
+      if (gen) {  // records naux..: nr, np, (species, nu, order) x 4 reactant and x 4 product slots
+        const int i = slots[s];
+        double grec[GEN_RECORDS * AUXW] = {(double)nr, (double)np};
+        for (int u = 0; u < nr; ++u) {
+          grec[2 + 3 * u] = d->rsp[4 * i + u];
+          grec[3 + 3 * u] = d->rnu[4 * i + u];
+          grec[4 + 3 * u] = d->ford ? d->ford[4 * i + u] : d->rnu[4 * i + u];
+        }
+        for (int u = 0; u < np; ++u) {
+          grec[14 + 3 * u] = d->psp[4 * i + u];
+          grec[15 + 3 * u] = d->pnu[4 * i + u];
+          grec[16 + 3 * u] = d->rord ? d->rord[4 * i + u] : d->pnu[4 * i + u];
+        }
+        aux.insert(aux.end(), grec, grec + GEN_RECORDS * AUXW);
+        naux += GEN_RECORDS;
+      }
     }
     uinfo[s] = inf;
   }
@@ -1171,9 +1189,9 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   return CKMI_OK;
 }
 
-template <int N>
+template <int N, bool F64>
 size_t reactor_lds_bytes(const ckmi_mech* m) {
-  return (size_t)m->img.bytes + jscratch_bytes<N>() + (size_t)RWAVES * slice_bytes(m->G);
+  return (size_t)m->img.bytes + jscratch_bytes<N>() + (size_t)rwaves(F64) * slice_bytes(m->G);
 }
 // Grid = (CUs x resident workgroups per CU), capped by the batch; J workspace = one
 // column-major N x 64 matrix per wave slot, allocated stream-ordered (~55 MB for GRI-3.0).
@@ -1192,17 +1210,18 @@ int stage_cfg(const DevCfg& dc, DevCfg* dst, hipStream_t stream) {
   return CKMI_OK;
 }
 
-template <int N, bool PL = false>
+template <int N, bool PL = false, bool F64 = false>
 int launch_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO& io, hipStream_t stream) {
-  const size_t lds = reactor_lds_bytes<N>(m);
+  constexpr int RWAVES = rwaves(F64);
+  const size_t lds = reactor_lds_bytes<N, F64>(m);
   static thread_local std::map<int, int> max_lds_set;
   if (lds > 64 * 1024 && max_lds_set[m->device] < (int)lds) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)reactor_kernel<N, PL>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    HIP_CHECK(hipFuncSetAttribute((const void*)reactor_kernel<N, PL, F64>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     max_lds_set[m->device] = (int)lds;
   }
   int ncu = 0, per_cu = 0;
   HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
-  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reactor_kernel<N, PL>, RWAVES * WAVE, lds));
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reactor_kernel<N, PL, F64>, RWAVES * WAVE, lds));
   if (per_cu < 1) return fail(CKMI_ERR_SIZE, "reactor kernel does not fit on a CU (LDS " + std::to_string(lds) + " B)");
   const int want = (n + RWAVES - 1) / RWAVES;
   const int grid = std::max(1, std::min(ncu * per_cu, want));
@@ -1216,7 +1235,7 @@ int launch_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO
   int rc = stage_cfg(dc, dcfg, stream);
   if (rc == CKMI_OK) {
     HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(int), stream));
-    hipLaunchKernelGGL((reactor_kernel<N, PL>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, dcfg, n, queue,
+    hipLaunchKernelGGL((reactor_kernel<N, PL, F64>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, dcfg, n, queue,
                        (double*)ws, io);
     HIP_CHECK(hipGetLastError());
   }
@@ -1394,16 +1413,23 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     const int type = chemact ? CKMI_RXN_FALLOFF : d->rtype[i];
     flags[s] = type | (d->rev[i] ? 4 : 0) | (d->has_rev[i] ? 8 : 0) | ((d->ftype[i] & 7) << 4) | (chemact ? 0x2000 : 0);
     const int nr = d->nr[i], np = d->np[i];
-    for (int u = 0; u < nr; ++u)
-      if (d->rnu[i * SLOTS + u] != std::floor(d->rnu[i * SLOTS + u]) || d->rnu[i * SLOTS + u] < 1.0) {
+    if (rxn_general(d, i)) {  // FORD / RORD / non-integral: real coefficients, extended variants
+      if (type == CKMI_RXN_PLOG) {
         delete m;
-        return fail(CKMI_ERR_UNSUPPORTED, "non-integral stoichiometric coefficient");
+        return fail(CKMI_ERR_UNSUPPORTED, "FORD / RORD or non-integral coefficients on a PLOG reaction");
       }
-    for (int u = 0; u < np; ++u)
-      if (d->pnu[i * SLOTS + u] != std::floor(d->pnu[i * SLOTS + u]) || d->pnu[i * SLOTS + u] < 1.0) {
-        delete m;
-        return fail(CKMI_ERR_UNSUPPORTED, "non-integral stoichiometric coefficient");
-      }
+      for (int u = 0; u < nr; ++u)
+        if (!(d->rnu[i * SLOTS + u] > 0.0) || (d->ford && d->ford[i * SLOTS + u] < 0.0)) {
+          delete m;
+          return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficients must be > 0 and orders >= 0");
+        }
+      for (int u = 0; u < np; ++u)
+        if (!(d->pnu[i * SLOTS + u] > 0.0) || (d->rord && d->rord[i * SLOTS + u] < 0.0)) {
+          delete m;
+          return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficients must be > 0 and orders >= 0");
+        }
+      flags[s] |= RX_GEN;
+    }
     if (nr > SLOTS || np > SLOTS) {
       delete m;
       return fail(CKMI_ERR_UNSUPPORTED, "more than 4 species on a reaction side");
@@ -1444,6 +1470,8 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   // PLOG and chemically activated reactions are evaluated by the extended kernel variant
   m->has_plog = std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_PLOG) > 0 ||
                 std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_CHEMACT) > 0;
+  for (int i = 0; i < II; ++i) m->has_general = m->has_general || rxn_general(d, i);
+  m->has_plog = m->has_plog || m->has_general;
   m->lnA_orig.resize(II);
   m->b_orig.resize(II);
   m->E_orig.resize(II);
@@ -1695,19 +1723,28 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   const int nvar = m->KK + 1;
   int rc;
   // PLOG mechanisms use one (64-wide) reactor variant, so that the PLOG branch costs compile time once
-  // more than 63 species: one workgroup per reactor (ckmi_big.hip); else one wave per reactor
-  if (nvar > 64 || g_reactor_path == 1) rc = launch_big_reactors(m, n, dc, io, (hipStream_t)stream);
-  else if (m->has_plog) rc = launch_reactors<64, true>(m, n, dc, io, (hipStream_t)stream);
-  else if (nvar <= 32) rc = launch_reactors<32>(m, n, dc, io, (hipStream_t)stream);
-  else if (nvar <= 54) rc = launch_reactors<54>(m, n, dc, io, (hipStream_t)stream);
-  else rc = launch_reactors<64>(m, n, dc, io, (hipStream_t)stream);
+  // more than 63 species: one workgroup per reactor (ckmi_big.hip); else one wave per reactor, its
+  // Newton inverse stored in FP64 when the tolerances ask for more than its FP32 rounding resolves
+  // (rtol < 1e-9; measured: the FP32-stored inverse integrates the rtol = 1e-8 sweeps of configs[2]
+  // and [3] without a failure, and fails one of 55 reactors at rtol = 1e-10, atol = 1e-20), and for
+  // mechanisms with FORD / RORD / fractional orders, whose d C^o / dC = o C^(o-1) grows without
+  // bound as C -> 0 (the FP32-stored inverse of such a Newton matrix stalled one reactor of five)
+  const bool f64 = g_reactor_path == 2 || (g_reactor_path != 3 && (cfg->rtol < 1e-9 || m->has_general));
+  const hipStream_t st = (hipStream_t)stream;
+  if (nvar > 64 || g_reactor_path == 1) rc = launch_big_reactors(m, n, dc, io, st);
+  else if (m->has_plog) rc = f64 ? launch_reactors<64, true, true>(m, n, dc, io, st) : launch_reactors<64, true>(m, n, dc, io, st);
+  else if (nvar <= 32 && !f64) rc = launch_reactors<32>(m, n, dc, io, st);
+  else if (nvar <= 54) rc = f64 ? launch_reactors<54, false, true>(m, n, dc, io, st) : launch_reactors<54>(m, n, dc, io, st);
+  else rc = f64 ? launch_reactors<64, false, true>(m, n, dc, io, st) : launch_reactors<64>(m, n, dc, io, st);
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;
 }
 
 int ckmi_set_reactor_path(int32_t path) {
-  if (path != 0 && path != 1) return fail(CKMI_ERR_ARG, "reactor path must be 0 (automatic) or 1 (workgroup)");
+  if (path < 0 || path > 3)
+    return fail(CKMI_ERR_ARG, "reactor path must be 0 (automatic), 1 (workgroup), 2 (wave, FP64 inverse) or 3 (wave, "
+                              "FP32-stored inverse)");
   g_reactor_path = path;
   return CKMI_OK;
 }

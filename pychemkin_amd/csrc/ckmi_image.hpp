@@ -289,4 +289,75 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
   return e;
 }
 
+// ------------------------------------------------------------------ general reactions
+// FORD / RORD orders or non-integral stoichiometric coefficients (extended kernel variants only).
+// Such a reaction keeps empty unit slots (nr = np = 0, so the unit-slot code skips it), carries
+// info bit 14 and an aux stream after its own record (record rx_aux + 1 on):
+//   nr, np, then (species, nu, order) for 4 reactant slots and for 4 product slots.
+constexpr uint32_t RX_GEN = 0x4000u;
+constexpr int GEN_RECORDS = 3;  // 2 + 24 doubles
+
+// C^o for a reaction order o: exact products for o = 0..3, else exp(o ln C) for C > 0 and 0 for
+// C <= 0 (oracle/ckoracle.c conc_pow, same rule)
+__device__ __forceinline__ double conc_pow(double c, double o, const double* e2t) {
+  if (o == 1.0) return c;
+  if (o == 2.0) return c * c;
+  if (o == 0.0) return 1.0;
+  if (o == 3.0) return c * c * c;
+  return c > 0.0 ? fexp(o * log(c), e2t) : 0.0;
+}
+// d C^o / dC under the same rule (oracle dconc_pow)
+__device__ __forceinline__ double dconc_pow(double c, double o, const double* e2t) {
+  if (o == 1.0) return 1.0;
+  if (o == 2.0) return 2.0 * c;
+  if (o == 0.0) return 0.0;
+  if (o == 3.0) return 3.0 * c * c;
+  return c > 0.0 ? o * fexp((o - 1.0) * log(c), e2t) : 0.0;
+}
+
+// Rate coefficients and concentration products of general reaction slot i: the Arrhenius /
+// third-body / falloff / explicit-REV part from eval_rxn_img (dummy species slots, so its
+// products are 1), then K_c from the real coefficients and the products from the orders.
+// Same arithmetic as oracle/ckoracle.c eval_reaction() with ford / rord.
+__device__ __forceinline__ Rxn eval_gen_img(const MechView& V, int i, uint32_t inf, double T, double lnT, double invT,
+                                            double lnPRT, double P, const double* C, const double* gRT,
+                                            const double* hRT, const double* Mg, bool need_h, int pslot, double plnf,
+                                            double gfac, const double*& g) {
+  const uint32_t one = (uint32_t)(V.KKp - 1);
+  const uint32_t dummy = one | (one << 8) | (one << 16) | (one << 24);
+  const uint32_t inf2 = rx_hasrev(inf) ? inf : (inf & ~4u);  // K_c-based reverse rate: below
+  Rxn e = eval_rxn_img<true>(V, i, inf2, dummy, dummy, 0u, T, lnT, invT, lnPRT, P, C, gRT, hRT, Mg, false, pslot, plnf,
+                             gfac);
+  g = V.aux() + AUXW * (rx_aux(inf) + 1);
+  const double* e2t = V.e2t();
+  const int nr = (int)g[0], np = (int)g[1];
+  double pf = 1.0, pr = 1.0, dG = 0.0, dH = 0.0, dnu = 0.0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (u < nr) {
+      const int k = (int)g[2 + 3 * u];
+      const double nu = g[3 + 3 * u];
+      pf *= conc_pow(C[k], g[4 + 3 * u], e2t);
+      dG -= nu * gRT[k];
+      if (need_h) dH -= nu * hRT[k];
+      dnu -= nu;
+    }
+    if (u < np) {
+      const int k = (int)g[14 + 3 * u];
+      const double nu = g[15 + 3 * u];
+      pr *= conc_pow(C[k], g[16 + 3 * u], e2t);
+      dG += nu * gRT[k];
+      if (need_h) dH += nu * hRT[k];
+      dnu += nu;
+    }
+  }
+  if (rx_rev(inf) && !rx_hasrev(inf)) {
+    e.kr = e.kf * fexp(dG - dnu * lnPRT, e2t);  // e.kf carries GFAC already
+    e.dlkr = need_h ? e.dlkf - (dH - dnu) * invT : 0.0;
+  }
+  e.pf = pf;
+  e.pr = pr;
+  return e;
+}
+
 }  // namespace ckmi

@@ -22,6 +22,25 @@ struct JitRop {
   hipFunction_t fn = nullptr;
   std::mutex mu;
 };
+// A reaction the unit-coefficient slots cannot express: a non-integral (or < 1) stoichiometric
+// coefficient, a FORD / RORD order that differs from the coefficient, or more than 4 molecules
+// on a side.  Evaluated by the extended kernel variants (ckmi_image.hpp eval_gen_img).
+inline bool rxn_general(const ckmi_mech_desc* d, int i) {
+  int mr = 0, mp = 0;
+  for (int u = 0; u < d->nr[i]; ++u) {
+    const double nu = d->rnu[4 * i + u];
+    if (nu != (double)(int)nu || nu < 1.0) return true;
+    if (d->ford && d->ford[4 * i + u] != nu) return true;
+    mr += (int)nu;
+  }
+  for (int u = 0; u < d->np[i]; ++u) {
+    const double nu = d->pnu[4 * i + u];
+    if (nu != (double)(int)nu || nu < 1.0) return true;
+    if (d->rord && d->rord[4 * i + u] != nu) return true;
+    mp += (int)nu;
+  }
+  return mr > 4 || mp > 4;
+}
 bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<double>& prm, std::vector<int>& lnA_off,
                       std::string& why);
 int jit_rop_compile(const std::string& src, std::vector<char>& code, std::string& log);
@@ -36,7 +55,8 @@ struct ckmi_mech {
   // host copies of the forward Arrhenius (original order) for get/set
   std::vector<double> lnA_orig, b_orig, E_orig;
   std::vector<int> rtype_orig;
-  bool has_plog = false;
+  bool has_plog = false;     // PLOG / chemically activated / general reactions: extended kernel variants
+  bool has_general = false;  // FORD / RORD / non-integral coefficients (rxn_general)
   std::vector<int> slot_of;  // original reaction -> device slot
   ckmi::JitRop* jit = nullptr;
 };

@@ -119,6 +119,10 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
       why = "PLOG / chemically activated reactions";
       return false;
     }
+    if (rxn_general(d, i)) {
+      why = "FORD / RORD orders or non-integral stoichiometric coefficients";
+      return false;
+    }
     if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_FALLOFF) {
       why = "reaction type";
       return false;

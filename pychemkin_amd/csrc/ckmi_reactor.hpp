@@ -114,6 +114,45 @@ __device__ __forceinline__ void jac_scatter(const MechView& V, int oJ, int nr, i
   }
 }
 
+// Jacobian terms of a general reaction (FORD / RORD / non-integral coefficients): dwdot/dT and
+// dq/dC_j through the orders, scattered with the real coefficients (oracle reactor_rhs).
+__device__ __noinline__ void gen_jac_terms(const MechView& V, const RunCtx& R, int i, uint32_t inf, double T,
+                                           double lnT, double invT, double lnPRT, double P, const double* C,
+                                           const WaveLds& L, int oJ, int conp) {
+  const double* g;
+  const Rxn e = eval_gen_img(V, i, inf, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), true, R.pslot, R.plnf,
+                             R.gfac, g);
+  const double* e2t = V.e2t();
+  const int nr = (int)g[0], np = (int)g[1];
+  const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
+  double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
+  if (conp) {
+    double of = 0.0, orr = 0.0;
+    for (int u = 0; u < nr; ++u) of += g[4 + 3 * u];
+    for (int u = 0; u < np; ++u) orr += g[16 + 3 * u];
+    dqdT -= e.mfac * (of * e.kf * e.pf - orr * e.kr * e.pr) * invT;
+    if (rx_type(inf) == 1) dqdT -= q * invT;
+  }
+  for (int u = 0; u < nr; ++u) atomicAdd(&L.dwdT()[(int)g[2 + 3 * u]], -g[3 + 3 * u] * dqdT);
+  for (int u = 0; u < np; ++u) atomicAdd(&L.dwdT()[(int)g[14 + 3 * u]], g[15 + 3 * u] * dqdT);
+  for (int side = 0; side < 2; ++side) {
+    const int ns = side == 0 ? nr : np;
+    const double* sl = g + (side == 0 ? 2 : 14);
+    const double kk = side == 0 ? e.mfac * e.kf : -e.mfac * e.kr;
+    if (kk == 0.0) continue;
+    for (int s = 0; s < ns; ++s) {
+      const int j = (int)sl[3 * s];
+      double d = dconc_pow(C[j], sl[3 * s + 2], e2t);
+      for (int u = 0; u < ns; ++u)
+        if (u != s) d *= conc_pow(C[(int)sl[3 * u]], sl[3 * u + 2], e2t);
+      const double dqw = kk * d * V.rwt()[j];
+      double* col = lds_at<double>(oJ) + (1 + j) * LDJ + 1;
+      for (int u = 0; u < nr; ++u) atomicAdd(&col[(int)g[2 + 3 * u]], -g[3 + 3 * u] * dqw * V.wt()[(int)g[2 + 3 * u]]);
+      for (int u = 0; u < np; ++u) atomicAdd(&col[(int)g[14 + 3 * u]], g[15 + 3 * u] * dqw * V.wt()[(int)g[14 + 3 * u]]);
+    }
+  }
+}
+
 // Right-hand side f(t, y) (one component per lane, lane 0 = T) and, if with_j, the
 // approximate analytic Jacobian into the workgroup's shared J scratch (column-major, the
 // caller holds its lock).  Same formulation as oracle/ckoracle.c reactor_rhs().  with_j is a
@@ -210,6 +249,19 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     const int i = base + lane;
     const uint32_t inf = V.info()[i];
     const int nr = rx_nr(inf), np = rx_np(inf);
+    if constexpr (PL) {
+      if (inf & RX_GEN) {  // FORD / RORD / non-integral coefficients: real nu and orders
+        const double* g;
+        const Rxn e = eval_gen_img(V, i, inf, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), false, R.pslot,
+                                   R.plnf, R.gfac, g);
+        const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (u < (int)g[0]) atomicAdd(&L.wdot()[(int)g[2 + 3 * u]], -g[3 + 3 * u] * q);
+          if (u < (int)g[1]) atomicAdd(&L.wdot()[(int)g[14 + 3 * u]], g[15 + 3 * u] * q);
+        }
+      }
+    }
     if (nr + np != 0) {
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
       const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), false,
@@ -242,6 +294,12 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       const int i = base + lane;
       const uint32_t inf = V.info()[i];
       const int nr = rx_nr(inf), np = rx_np(inf);
+      if constexpr (PL) {
+        if (inf & RX_GEN) {
+          gen_jac_terms(V, R, i, inf, T, lnT, invT, lnPRT, P, C, L, oJ, conp);
+          continue;
+        }
+      }
       if (nr + np == 0) continue;
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
       const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), true,
@@ -354,122 +412,15 @@ __device__ __forceinline__ double bpermute(int src_lane, double v) {
   return __hiloint2double(hi, lo);
 }
 
-#if defined(CKMI_NEWTON_F32)
-// Gauss-Jordan inverse held in FP32 (N floats per lane instead of N doubles).  The modified
-// Newton iteration only needs an approximate M^-1 -- M is rebuilt from the FP32-parked Jacobian
-// and a gamma that lags by up to DGMAX -- so the factorisation runs in FP32 (half the VALU cost
-// and half the registers of the FP64 form); the right-hand side and the correction stay FP64.
-// M is equilibrated with the error weights first, M~ = D M D^-1 with D = diag(ewt): in the
-// weighted variables of the convergence test every entry has its natural scale (T against
-// trace species span ~1e14 unscaled), the pivot search compares like with like, and the FP32
-// rounding of M~^-1 is uniform in the norm the Newton iteration is judged in.
-template <int N>
-struct NewtonMatrix {
-  float a[N];
-  int permv;  // lane k: the lane whose row was the pivot of step k
-  float dl;   // this lane's scale d_i (ewt at factorisation time; 1 on inactive lanes)
-
-  // orow: LDS byte offset of an N-float scratch row of the calling wave (16-byte aligned)
-  __device__ __forceinline__ void build(const float* J, int ldj, double gamma, int lane_in, int n, double ewt,
-                                        int orow) {
-    const int lane = opaque_lane(lane_in);
-    dl = (lane < n && ewt > 0.0) ? (float)ewt : 1.0f;
-    float* rdv = lds_at<float>(__builtin_amdgcn_readfirstlane(opaque_lane(orow)));
-    if (lane < N) rdv[lane] = 1.0f / dl;
-    wave_lds_sync();
-    const float gf = (float)gamma;
-    constexpr int NQ = (N + 3) / 4;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const float4 r = reinterpret_cast<const float4*>(rdv)[q];
-      const float rv[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = 4 * q + u;
-        if (j < N) a[j] = ((j == lane ? 1.0f : 0.0f) - gf * J[j * ldj + lane]) * (dl * rv[u]);
-      }
-    }
-    wave_lds_sync();  // the scratch row is the pivot row of factor()
-  }
-
-  __device__ __forceinline__ bool factor(int lane_in, int n, int orow) {
-    const int lane = opaque_lane(lane_in);
-    bool pivoted = lane >= N;
-    permv = lane;
-    bool ok = true;
-    float4* row = lds_at<float4>(__builtin_amdgcn_readfirstlane(opaque_lane(orow)));
-    constexpr int NQ = (N + 3) / 4;  // float4 groups per row
-    uint32_t v0 = pivoted ? 0u : __float_as_uint(fabsf(a[0]));
-    uint32_t vmax = wave_max_u32(v0);
-#pragma unroll
-    for (int k = 0; k < N; ++k) {
-      if (vmax == 0u) ok = false;
-      const uint64_t mask = __ballot(!pivoted && v0 == vmax);
-      const int p = uni(mask ? (int)__ffsll((unsigned long long)mask) - 1 : 0);
-      const bool me = lane == p;
-      if (me) {
-#pragma unroll
-        for (int j = 0; j < NQ; ++j)
-          row[j] = make_float4(a[4 * j], 4 * j + 1 < N ? a[4 * j + 1] : 0.0f, 4 * j + 2 < N ? a[4 * j + 2] : 0.0f,
-                               4 * j + 3 < N ? a[4 * j + 3] : 0.0f);
-      }
-      wave_lds_sync();
-      const float piv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(a[k]), p));
-      float rp = __builtin_amdgcn_rcpf(piv);
-      rp = fmaf(rp, fmaf(-piv, rp, 1.0f), rp);
-      if (me) pivoted = true;
-      if (lane == k) permv = p;
-      const float g = me ? (piv - 1.0f) * rp : a[k] * rp;
-      const float ak = me ? rp : -g;
-      const int Q0 = (k + 1 < N ? k + 1 : k) / 4;  // the group holding column k+1 goes first
-      uint32_t w = 0u;
-#pragma unroll
-      for (int t = 0; t < NQ; ++t) {
-        const int Q = (Q0 + t) % NQ;
-        const float4 r = row[Q];
-        const float rv[4] = {r.x, r.y, r.z, r.w};
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int j = 4 * Q + u;
-          if (j < N && j != k) a[j] = fmaf(-g, rv[u], a[j]);
-        }
-        if (k + 1 < N) {
-          if (t == 0) {
-            v0 = pivoted ? 0u : __float_as_uint(fabsf(a[k + 1]));
-            w = v0;
-          }
-          if (t == 1) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_QUAD_1032, 0xf, 0xf, false));
-          if (t == 3) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_QUAD_2301, 0xf, 0xf, false));
-          if (t == 5) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_ROW_HALF_MIRROR, 0xf, 0xf, false));
-          if (t == 7) w = max(w, (uint32_t)__builtin_amdgcn_mov_dpp((int)w, DPP_ROW_MIRROR, 0xf, 0xf, false));
-          if (t == 9) {
-            const uint32_t r0 = __builtin_amdgcn_readlane(w, 0), r1 = __builtin_amdgcn_readlane(w, 16);
-            const uint32_t r2 = __builtin_amdgcn_readlane(w, 32), r3 = __builtin_amdgcn_readlane(w, 48);
-            vmax = max(max(r0, r1), max(r2, r3));
-          }
-        }
-        if (t % 2 == 1) asm volatile("" ::: "memory");
-      }
-      a[k] = ak;
-    }
-    return ok;
-  }
-
-  // x = M^-1 b = D^-1 M~^-1 D b (lane k: component k); FP64 accumulation of the FP32 inverse
-  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
-    const int lane = opaque_lane(lane_in);
-    if (lane >= n) b = 0.0;
-    const double bp = bpermute(permv, b * (double)dl);
-    double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; j += 2) {
-      s0 = fma((double)a[j], bcast(bp, j), s0);
-      if (j + 1 < N) s1 = fma((double)a[j + 1], bcast(bp, j + 1), s1);
-    }
-    return bpermute(permv, s0 + s1) / (double)dl;
-  }
-};
-#elif !defined(CKMI_NEWTON_LU)
+// Two forms of the Newton matrix (kernel template parameter F64 of reactor_kernel):
+//   NewtonMatrixF32S  FP64 Gauss-Jordan, inverse stored in FP32 between factorisations (N VGPRs:
+//                     3 waves per SIMD); the default
+//   NewtonMatrixGJ64  the same inverse kept in FP64 (2N VGPRs: 2 waves per SIMD), for tolerances
+//                     tighter than an FP32-rounded inverse resolves (rtol < 1e-9, ckmi.hip)
+// A factorisation in FP32 (tried, with error-weight equilibration) fails on ~6 % of the bench
+// reactors (Newton convergence / error-test failures): the elimination needs FP64, the stored
+// inverse does not.  CKMI_NEWTON_LU selects the older LU form of the FP64 matrix.
+#if !defined(CKMI_NEWTON_LU)
 #ifndef CKMI_GJ_BATCH
 #define CKMI_GJ_BATCH 4  // row pairs read per batch in the elimination
 #endif
@@ -561,6 +512,12 @@ struct NewtonMatrixGJ64 {
     return ok;
   }
 
+  template <typename TJ>
+  __device__ __forceinline__ bool build_factor(const TJ* J, int ldj, double gamma, int lane, int n, int orow) {
+    build(J, ldj, gamma, lane, n);
+    return factor(lane, n, orow);
+  }
+
   // x = M^-1 b (lane k: component k)
   __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
     const int lane = opaque_lane(lane_in);
@@ -576,44 +533,9 @@ struct NewtonMatrixGJ64 {
     return bpermute(permv, s0 + s1);
   }
 };
-#ifdef CKMI_NEWTON_F32S
-// The FP64 Gauss-Jordan inverse above, stored in FP32 between factorisations: the factorisation
-// itself keeps FP64 (its N doubles are live only inside ST_SETUP), the inverse that stays in
-// registers across the RHS evaluations takes N VGPRs instead of 2N.
-template <int N>
-struct NewtonMatrix {
-  float a[N];
-  int permv;
-  template <typename TJ>
-  __device__ __forceinline__ bool build_factor(const TJ* J, int ldj, double gamma, int lane, int n, int orow) {
-    NewtonMatrixGJ64<N> m;
-    m.build(J, ldj, gamma, lane, n);
-    const bool ok = m.factor(lane, n, orow);
-#pragma unroll
-    for (int j = 0; j < N; ++j) a[j] = (float)m.a[j];
-    permv = m.permv;
-    return ok;
-  }
-  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
-    const int lane = opaque_lane(lane_in);
-    if (lane >= n) b = 0.0;
-    const double bp = bpermute(permv, b);
-    double s0 = 0.0, s1 = 0.0;
-#pragma unroll
-    for (int j = 0; j < N; j += 2) {
-      s0 = fma((double)a[j], bcast(bp, j), s0);
-      if (j + 1 < N) s1 = fma((double)a[j + 1], bcast(bp, j + 1), s1);
-    }
-    return bpermute(permv, s0 + s1);
-  }
-};
 #else
 template <int N>
-using NewtonMatrix = NewtonMatrixGJ64<N>;
-#endif
-#else
-template <int N>
-struct NewtonMatrix {
+struct NewtonMatrixGJ64 {  // LU form (CKMI_NEWTON_LU experiment)
   double a[N];
   int permv;     // lane k: the lane whose row was the pivot of step k
   double rdiag;  // 1 / u_kk of this lane's (permuted) row
@@ -627,6 +549,11 @@ struct NewtonMatrix {
     for (int j = 0; j < N; ++j) a[j] = (j == lane ? 1.0 : 0.0) - gamma * J[j * ldj + lane];
   }
 
+  template <typename TJ>
+  __device__ __forceinline__ bool build_factor(const TJ* J, int ldj, double gamma, int lane, int n, int) {
+    build(J, ldj, gamma, lane, n);
+    return factor(lane, n);
+  }
   __device__ __forceinline__ bool factor(int lane_in, int n) {
     const int lane = opaque_lane(lane_in);
     bool pivoted = lane >= n;
@@ -681,6 +608,36 @@ struct NewtonMatrix {
 };
 
 #endif
+
+// The FP64 Gauss-Jordan inverse above, stored in FP32 between factorisations: the factorisation
+// itself keeps FP64 (its N doubles are live only inside ST_SETUP), the inverse that stays in
+// registers across the RHS evaluations takes N VGPRs instead of 2N.
+template <int N>
+struct NewtonMatrixF32S {
+  float a[N];
+  int permv;
+  template <typename TJ>
+  __device__ __forceinline__ bool build_factor(const TJ* J, int ldj, double gamma, int lane, int n, int orow) {
+    NewtonMatrixGJ64<N> m;
+    const bool ok = m.build_factor(J, ldj, gamma, lane, n, orow);
+#pragma unroll
+    for (int j = 0; j < N; ++j) a[j] = (float)m.a[j];
+    permv = m.permv;
+    return ok;
+  }
+  __device__ __forceinline__ double solve(double b, int lane_in, int n) const {
+    const int lane = opaque_lane(lane_in);
+    if (lane >= n) b = 0.0;
+    const double bp = bpermute(permv, b);
+    double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < N; j += 2) {
+      s0 = fma((double)a[j], bcast(bp, j), s0);
+      if (j + 1 < N) s1 = fma((double)a[j + 1], bcast(bp, j + 1), s1);
+    }
+    return bpermute(permv, s0 + s1);
+  }
+};
 
 // uniform small-array access with runtime index (keeps the arrays in SGPRs)
 template <int S>

@@ -11,7 +11,7 @@ flattened once into the fixed-slot, struct-of-arrays layout declared in
 Supported syntax (Chemkin-II gas phase): ELEMENTS (with optional /weight/), SPECIES,
 optional THERMO block, REACTIONS with unit keywords, ``=``/``<=>``/``=>``, ``+M``,
 ``(+M)``/``(+species)`` falloff, LOW, TROE (3 or 4 parameters), SRI (3 or 5), REV,
-DUPLICATE, third-body efficiencies, FORD/RORD (parsed, rejected by the device path),
+DUPLICATE, third-body efficiencies, FORD/RORD and non-integral stoichiometric coefficients,
 PLOG (elementary reactions; ln k interpolated in ln P, clamped outside the table).
 """
 from __future__ import annotations
@@ -380,7 +380,8 @@ class Mechanism:
             k = key.upper()
             if not k:
                 continue
-            nums = [_to_float(v) for v in vals.split()] if vals else []
+            # FORD / RORD carry "species order"; every other keyword numbers only
+            nums = [_to_float(v) for v in vals.split()] if vals and k not in ("FORD", "RORD") else []
             if k in ("DUP", "DUPLICATE"):
                 current.duplicate = True
             elif k == "LOW":
@@ -399,12 +400,12 @@ class Mechanism:
                 current.sri = tuple(nums)
             elif k == "REV":
                 current.rev = tuple(nums[:3])
-            elif k == "FORD":
-                sp = vals.split()[0]
-                current.ford[self._species_index_upper()[sp.upper()]] = _to_float(vals.split()[1])
-            elif k == "RORD":
-                sp = vals.split()[0]
-                current.rord[self._species_index_upper()[sp.upper()]] = _to_float(vals.split()[1])
+            elif k in ("FORD", "RORD"):
+                parts = vals.split() if vals else []
+                names = self._species_index_upper()
+                if len(parts) != 2 or parts[0].upper() not in names:
+                    raise MechanismError(f"{k} needs /species order/: {s!r}")
+                (current.ford if k == "FORD" else current.rord)[names[parts[0].upper()]] = _to_float(parts[1])
             elif k == "PLOG":
                 current.plog.append(tuple(nums[:4]))
             elif k == "UNITS":
@@ -430,8 +431,16 @@ class Mechanism:
                 self.ncf[self.elements.index(el), k] = n
         self.wt = (np.asarray(self.awt, dtype=np.float64)[:, None] * self.ncf).sum(axis=0)
         for rx in self.reactions:
-            if rx.ford or rx.rord:
-                pass  # kept on the host object; device path rejects (see to_tables)
+            # FORD / RORD change the order of a species already on that side (Chemkin: the
+            # concentration exponent of that reactant / product in the forward / reverse rate)
+            for sp in rx.ford:
+                if sp not in [r for r, _ in rx.reactants]:
+                    raise MechanismError(f"FORD species {sp} is not a reactant of {rx.equation}")
+            for sp in rx.rord:
+                if sp not in [p for p, _ in rx.products]:
+                    raise MechanismError(f"RORD species {sp} is not a product of {rx.equation}")
+            if rx.rord and not rx.reversible:
+                raise MechanismError(f"RORD on an irreversible reaction {rx.equation}")
             # element balance check
             bal = np.zeros(MM)
             for sp, nu in rx.products:
@@ -500,6 +509,8 @@ class Mechanism:
         psp = np.zeros((II, S), np.int32)
         rnu = np.zeros((II, S), np.float64)
         pnu = np.zeros((II, S), np.float64)
+        ford = np.zeros((II, S), np.float64)     # forward order of each reactant slot (FORD, else nu)
+        rord = np.zeros((II, S), np.float64)     # reverse order of each product slot (RORD, else nu)
         arr = np.zeros((II, 3), np.float64)      # ln A, b, E/R  (forward / high-pressure)
         low = np.zeros((II, 3), np.float64)      # ln A0, b0, E0/R
         revp = np.zeros((II, 3), np.float64)     # explicit REV: ln Ar, br, Er/R
@@ -513,8 +524,6 @@ class Mechanism:
         plog_ptr = np.zeros(II + 1, np.int32)     # CSR into plog_par (rtype TAB_PLOG)
         plog_par: List[Tuple[float, float, float, float]] = []  # ln P [dyn/cm2], ln A [cgs], b, E/R
         for i, rx in enumerate(self.reactions):
-            if rx.ford or rx.rord:
-                raise MechanismError(f"FORD/RORD not supported on the device path ({rx.equation})")
             if rx.plog:
                 if rx.kind != RXN_ELEMENTARY or rx.rev is not None:
                     raise MechanismError(f"PLOG on a third-body/falloff reaction or with REV ({rx.equation})")
@@ -534,9 +543,11 @@ class Mechanism:
             for j, (sp, nu) in enumerate(rx.reactants):
                 rsp[i, j] = idx[sp]
                 rnu[i, j] = nu
+                ford[i, j] = rx.ford.get(sp, nu)
             for j, (sp, nu) in enumerate(rx.products):
                 psp[i, j] = idx[sp]
                 pnu[i, j] = nu
+                rord[i, j] = rx.rord.get(sp, nu)
             extra = 1 if rx.kind == RXN_THIRDBODY else 0
             A = self.A_cgs(i)
             arr[i] = (math.log(A) if A > 0 else -1e300, rx.b, rx.E * rx.E_scale)
@@ -589,7 +600,7 @@ class Mechanism:
             thermo[k, 10:17] = th.high
         return dict(
             KK=np.int32(KK), II=np.int32(II), wt=self.wt.astype(np.float64), thermo=thermo,
-            rtype=rtype, rev=rev, nr=nr, np=np_, rsp=rsp, psp=psp, rnu=rnu, pnu=pnu,
+            rtype=rtype, rev=rev, nr=nr, np=np_, rsp=rsp, psp=psp, rnu=rnu, pnu=pnu, ford=ford, rord=rord,
             arr=arr, low=low, revp=revp, has_rev=has_rev, ftype=ftype, fpar=fpar, tbsp=tbsp,
             eff_ptr=np.asarray(eff_ptr, np.int32), eff_sp=np.asarray(eff_sp, np.int32),
             eff_val=np.asarray(eff_val, np.float64),

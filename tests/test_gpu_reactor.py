@@ -68,6 +68,21 @@ def test_conp_conv_energy_tifp(dm, oracle, mech):
     assert np.all(np.abs(ratio - 1) < 0.25) and abs(np.mean(ratio) - 1) < 0.1
 
 
+@pytest.mark.parametrize("path", [2, 3])
+def test_newton_inverse_forms_match_oracle(dm, oracle, mech, path):
+    """Both forms of the wave kernel's Newton inverse -- FP64 (path 2, 8 waves per workgroup) and
+    FP32-stored (path 3, 12 waves; the automatic choice for rtol >= 1e-9) -- against the oracle
+    (FP64 LU) at the north_star bars."""
+    from pychemkin_amd import _native
+
+    _native.set_reactor_path(path)
+    try:
+        res, ref = _run_both(dm, oracle, mech, CASES, energy=1, t_end=1.0, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
+    finally:
+        _native.set_reactor_path(0)
+    _check(res, ref, mech)
+
+
 def test_given_temperature(dm, oracle, mech):
     res, ref = _run_both(dm, oracle, mech, CASES[:4], energy=2, t_end=2e-3, atol=1e-12, rtol=1e-7)
     _check(res, ref, mech)
