@@ -121,6 +121,9 @@ typedef struct {
   int32_t prof2_kind;  /* 1 QPRO heat loss rate [cal/s] (replaces QLOS), 2 AEXT area [cm2] (replaces AREAQ) */
   double prof2_t[64];
   double prof2_v[64];
+  int32_t nprof3;      /* AEXT area profile [cm2] beside a QPRO in the second slot (prof2_kind 1): the */
+  double prof3_t[64];  /* heat loss is then QPRO(t) + HTC AEXT(t) (T - TAMB) (batchreactor.py:2005-2067); */
+  double prof3_v[64];  /* 0 = none (<= 64) */
 } ckmi_reactor_cfg;
 
 /* Optional per-reactor inputs / outputs of ckmi_reactor_run_ex (any pointer may be NULL). */

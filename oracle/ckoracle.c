@@ -267,8 +267,12 @@ static void profile_eval(const cko_cfg* c, double t, double tsel, double base, d
 #define ERG_PER_CAL 4.184e7
 
 static double prof2_value(const cko_cfg* c, double t, double tsel, double base, int kind) {
-  if (c->nprof2 <= 0 || c->prof2_kind != kind) return base;
   double v, d;
+  if (kind == 2 && c->nprof3 > 0 && c->nprof2 > 0 && c->prof2_kind == 1) { /* AEXT beside QPRO */
+    pwl_eval(c->prof3_t, c->prof3_v, c->nprof3, t, tsel, &v, &d);
+    return v;
+  }
+  if (c->nprof2 <= 0 || c->prof2_kind != kind) return base;
   pwl_eval(c->prof2_t, c->prof2_v, c->nprof2, t, tsel, &v, &d);
   return v;
 }
@@ -986,12 +990,14 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   y[0] = T0;
   for (int k = 0; k < KK; ++k) y[1 + k] = Y0[k];
   /* profile breakpoints are integration stop points (derivative discontinuities) */
-  double tcrit[130];
+  double tcrit[194];
   int ncrit = 0;
   for (int i = 0; i < cfg->nprof && ncrit < 64; ++i)
     if (cfg->prof_t[i] > 0.0 && cfg->prof_t[i] < tend) tcrit[ncrit++] = cfg->prof_t[i];
   for (int i = 0; i < cfg->nprof2 && ncrit < 128; ++i)
     if (cfg->prof2_t[i] > 0.0 && cfg->prof2_t[i] < tend) tcrit[ncrit++] = cfg->prof2_t[i];
+  for (int i = 0; i < cfg->nprof3 && ncrit < 192; ++i)
+    if (cfg->prof3_t[i] > 0.0 && cfg->prof3_t[i] < tend) tcrit[ncrit++] = cfg->prof3_t[i];
   /* sorted union of both profiles' breakpoints */
   for (int i = 1; i < ncrit; ++i)
     for (int j = i; j > 0 && tcrit[j - 1] > tcrit[j]; --j) {

@@ -71,6 +71,9 @@ typedef struct {
   int prof2_kind;
   const double* prof2_t;
   const double* prof2_v;
+  int nprof3;       /* AEXT [cm2] beside a QPRO second profile (prof2_kind 1), 0 = none */
+  const double* prof3_t;
+  const double* prof3_v;
 } cko_cfg;
 
 typedef struct {

@@ -55,7 +55,8 @@ class _Cfg(ct.Structure):
         ("max_steps", ct.c_int), ("nprof", ct.c_int), ("prof_t", _P), ("prof_v", _P), ("prof_kind", ct.c_int),
         ("gfac", ct.c_double), ("qloss", ct.c_double), ("htc", ct.c_double), ("areaq", ct.c_double),
         ("tamb", ct.c_double), ("pert_rxn", ct.c_int), ("pert_fac", ct.c_double), ("nprof2", ct.c_int),
-        ("prof2_kind", ct.c_int), ("prof2_t", _P), ("prof2_v", _P),
+        ("prof2_kind", ct.c_int), ("prof2_t", _P), ("prof2_v", _P), ("nprof3", ct.c_int), ("prof3_t", _P),
+        ("prof3_v", _P),
     ]
 
 
@@ -136,7 +137,7 @@ class Oracle:
     def make_cfg(problem=1, energy=1, t_end=1.0, atol=1e-12, rtol=1e-6, h0=0.0, hmax=0.0, nneg=False,
                  ign_mode=None, ign_val=0.0, ign_species=0, ign_stop=False, max_steps=0, profile=None,
                  prof_kind=0, gfac=1.0, qloss=0.0, htc=0.0, areaq=0.0, tamb=300.0, asteps=0, pert_rxn=-1,
-                 pert_fac=1.0, profile2=None, prof2_kind=0, avar=-1, avalue=0.0):
+                 pert_fac=1.0, profile2=None, prof2_kind=0, avar=-1, avalue=0.0, profile3=None):
         """asteps / avar / avalue (adaptive output points) do not change the integration and are
         accepted for signature parity with pychemkin_amd._native.make_cfg."""
         c = _Cfg()
@@ -153,6 +154,12 @@ class Oracle:
             v2 = np.ascontiguousarray(profile2[1], np.float64)
             c.nprof2, c.prof2_t, c.prof2_v = len(x2), _ptr(x2), _ptr(v2)
             keep = [(x2, v2)]
+        c.nprof3 = 0
+        if profile3 is not None:  # AEXT beside a QPRO profile2
+            x3 = np.ascontiguousarray(profile3[0], np.float64)
+            v3 = np.ascontiguousarray(profile3[1], np.float64)
+            c.nprof3, c.prof3_t, c.prof3_v = len(x3), _ptr(x3), _ptr(v3)
+            keep = (keep or []) + [(x3, v3)]
         if profile is not None:
             x = np.ascontiguousarray(profile[0], np.float64)
             v = np.ascontiguousarray(profile[1], np.float64)

@@ -51,7 +51,8 @@ class ReactorCfg(ct.Structure):
         ("prof_kind", ct.c_int32), ("gfac", ct.c_double), ("qloss", ct.c_double), ("htc", ct.c_double),
         ("areaq", ct.c_double), ("tamb", ct.c_double), ("asteps", ct.c_int32), ("avar", ct.c_int32),
         ("avalue", ct.c_double), ("nprof2", ct.c_int32), ("prof2_kind", ct.c_int32), ("prof2_t", ct.c_double * 64),
-        ("prof2_v", ct.c_double * 64),
+        ("prof2_v", ct.c_double * 64), ("nprof3", ct.c_int32), ("prof3_t", ct.c_double * 64),
+        ("prof3_v", ct.c_double * 64),
     ]
 
 
@@ -131,11 +132,12 @@ def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: flo
              hmax: float = 0.0, nneg: bool = False, ign_mode=None, ign_val: float = 0.0, ign_species: int = 0,
              ign_stop: bool = False, max_steps: int = 0, profile=None, prof_kind: int = 0, gfac: float = 1.0,
              qloss: float = 0.0, htc: float = 0.0, areaq: float = 0.0, tamb: float = 300.0,
-             asteps: int = 0, avar: int = -1, avalue: float = 0.0, profile2=None, prof2_kind: int = 0) -> ReactorCfg:
+             asteps: int = 0, avar: int = -1, avalue: float = 0.0, profile2=None, prof2_kind: int = 0,
+             profile3=None) -> ReactorCfg:
     """Typed form of the reactor keywords (see include/ckmi.h ckmi_reactor_cfg).
 
     profile: (x, v) VPRO/PPRO (prof_kind 0) or TPRO (prof_kind 1); profile2: (x, v) QPRO
-    (prof2_kind 1) or AEXT (prof2_kind 2)."""
+    (prof2_kind 1) or AEXT (prof2_kind 2); profile3: (x, v) AEXT beside a QPRO profile2."""
     c = ReactorCfg()
     c.avar, c.avalue = int(avar), float(avalue)
     c.nprof2, c.prof2_kind = 0, int(prof2_kind)
@@ -147,6 +149,15 @@ def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: flo
         for i in range(len(x2)):
             c.prof2_t[i] = x2[i]
             c.prof2_v[i] = v2[i]
+    c.nprof3 = 0
+    if profile3 is not None:
+        x3, v3 = np.asarray(profile3[0], np.float64), np.asarray(profile3[1], np.float64)
+        if len(x3) != len(v3) or len(x3) > 64 or len(x3) == 0:
+            raise ValueError("profile3 must have matching lengths in [1, 64]")
+        c.nprof3 = len(x3)
+        for i in range(len(x3)):
+            c.prof3_t[i] = x3[i]
+            c.prof3_v[i] = v3[i]
     c.prof_kind, c.gfac, c.qloss, c.htc, c.areaq, c.tamb = int(prof_kind), float(gfac), float(qloss), float(htc), \
         float(areaq), float(tamb)
     c.asteps = int(asteps)

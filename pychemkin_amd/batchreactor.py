@@ -284,10 +284,10 @@ class BatchReactors(ReactorModel):
                         htc=self.heat_transfer_coefficient, areaq=self.heat_transfer_area,
                         tamb=self.ambient_temperature)
             qp, ap = self.getprofile("QPRO"), self.getprofile("AEXT")
-            if qp is not None and ap is not None:
-                raise ReactorError("QPRO together with AEXT is not supported on the device path yet")
             if qp is not None:
                 heat.update(profile2=(qp.x, qp.y), prof2_kind=1)
+                if ap is not None:  # both: QPRO(t) + HTC AEXT(t) (T - TAMB)
+                    heat.update(profile3=(ap.x, ap.y))
             elif ap is not None:
                 heat.update(profile2=(ap.x, ap.y), prof2_kind=2)
         adap = {}

@@ -206,7 +206,9 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           R.areaq = cfg->areaq;
           R.tamb = cfg->tamb;
           R.nq = cfg->prof2_kind == 1 ? cfg->nprof2 : 0;
-          R.na = cfg->prof2_kind == 2 ? cfg->nprof2 : 0;
+          R.na = cfg->prof2_kind == 2 ? cfg->nprof2 : cfg->nprof3;
+          R.a_t = cfg->prof2_kind == 2 ? cfg->prof2_t : cfg->prof3_t;
+          R.a_v = cfg->prof2_kind == 2 ? cfg->prof2_v : cfg->prof3_v;
           {
             const int ar = io.afac_rxn ? io.afac_rxn[r] : -1;
             R.pslot = (ar >= 0 && ar < img.II) ? img.slot_of[ar] : -1;
@@ -1700,6 +1702,9 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   if (cfg->nprof2 > 0 && cfg->prof2_kind != 1 && cfg->prof2_kind != 2)
     return fail(CKMI_ERR_ARG, "prof2_kind must be 1 (QPRO) or 2 (AEXT)");
   if (cfg->nprof2 > 0 && cfg->energy != 1) return fail(CKMI_ERR_ARG, "QPRO / AEXT need an energy-equation run");
+  if (cfg->nprof3 < 0 || cfg->nprof3 > 64) return fail(CKMI_ERR_ARG, "nprof3 must be in [0, 64]");
+  if (cfg->nprof3 > 0 && !(cfg->nprof2 > 0 && cfg->prof2_kind == 1))
+    return fail(CKMI_ERR_ARG, "the third profile (AEXT) needs a QPRO second profile");
   if (cfg->avar > m->KK || cfg->avar < -1) return fail(CKMI_ERR_ARG, "avar must be -1, 0 (T) or 1 + species index");
   if (n == 0) return CKMI_OK;
   DevCfg dc;  // this call's configuration (staged per launch: no state shared between calls)
@@ -1711,6 +1716,8 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
       if (cfg->prof_t[i] > 0.0 && cfg->prof_t[i] < cfg->t_end) tc.push_back(cfg->prof_t[i]);
     for (int i = 0; i < cfg->nprof2; ++i)
       if (cfg->prof2_t[i] > 0.0 && cfg->prof2_t[i] < cfg->t_end) tc.push_back(cfg->prof2_t[i]);
+    for (int i = 0; i < cfg->nprof3; ++i)
+      if (cfg->prof3_t[i] > 0.0 && cfg->prof3_t[i] < cfg->t_end) tc.push_back(cfg->prof3_t[i]);
     std::sort(tc.begin(), tc.end());
     tc.erase(std::unique(tc.begin(), tc.end()), tc.end());
     dc.ncrit = (int)tc.size();

@@ -846,7 +846,7 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
     else fT -= P * dVdt / (V_ * rho * cpm);
     double qloss = R.qloss, area = R.areaq, dummy;
     if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
-    if (R.na > 0) profile2_eval(R.cfg, R.na, t, R.tsel, area, dummy);
+    if (R.na > 0) pwl_eval(R.a_t, R.a_v, R.na, t, R.tsel, area, dummy);
     mcp = R.mass * cpm;
     q1 = R.htc * area * ERG_PER_CAL;
     fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
@@ -1032,7 +1032,9 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           R.areaq = cfg->areaq;
           R.tamb = cfg->tamb;
           R.nq = cfg->prof2_kind == 1 ? cfg->nprof2 : 0;
-          R.na = cfg->prof2_kind == 2 ? cfg->nprof2 : 0;
+          R.na = cfg->prof2_kind == 2 ? cfg->nprof2 : cfg->nprof3;
+          R.a_t = cfg->prof2_kind == 2 ? cfg->prof2_t : cfg->prof3_t;
+          R.a_v = cfg->prof2_kind == 2 ? cfg->prof2_v : cfg->prof3_v;
           {
             const int ar = io.afac_rxn ? io.afac_rxn[r] : -1;
             R.pslot = (ar >= 0 && ar < img.II) ? img.slot_of[ar] : -1;

@@ -228,9 +228,22 @@ int apply_profiles(ckmi_reactor_cfg& c) {
       std::copy(p.x.begin(), p.x.end(), c.prof_t);
       std::copy(p.y.begin(), p.y.end(), c.prof_v);
     } else if (p.key == "QPRO" || p.key == "AEXT") {
-      if (c.nprof2 > 0) return fail(CKMI_ERR_UNSUPPORTED, "QPRO together with AEXT");
+      // QPRO takes the second slot; AEXT the second alone, or the third beside a QPRO
+      const bool q = p.key == "QPRO";
+      if (q && c.nprof2 > 0 && c.prof2_kind == 2) {  // AEXT came first: move it to the third slot
+        c.nprof3 = c.nprof2;
+        std::copy(c.prof2_t, c.prof2_t + c.nprof2, c.prof3_t);
+        std::copy(c.prof2_v, c.prof2_v + c.nprof2, c.prof3_v);
+        c.nprof2 = 0;
+      }
+      if (!q && c.nprof2 > 0 && c.prof2_kind == 1) {
+        c.nprof3 = np;
+        std::copy(p.x.begin(), p.x.end(), c.prof3_t);
+        std::copy(p.y.begin(), p.y.end(), c.prof3_v);
+        continue;
+      }
       c.nprof2 = np;
-      c.prof2_kind = p.key == "QPRO" ? 1 : 2;
+      c.prof2_kind = q ? 1 : 2;
       std::copy(p.x.begin(), p.x.end(), c.prof2_t);
       std::copy(p.y.begin(), p.y.end(), c.prof2_v);
     } else {

@@ -54,7 +54,9 @@ struct RunCtx {
   double rho0, V0, P0;
   double mass;                       // rho0 V0 [g]
   double qloss, htc, areaq, tamb;    // QLOS [cal/s], HTC, AREAQ, TAMB
-  int nq, na;                        // QPRO / AEXT profile points (prof2), 0 = constant
+  int nq, na;                        // QPRO / AEXT profile points, 0 = constant
+  const double* a_t;                 // the AEXT profile: prof2 (alone) or prof3 (beside QPRO)
+  const double* a_v;
   double tsel;                       // midpoint of the current integration segment (pwl_eval)
   const ckmi_reactor_cfg* cfg;
 };
@@ -356,7 +358,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     // per unit heat capacity of the reactor contents
     double qloss = R.qloss, area = R.areaq, dummy;
     if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
-    if (R.na > 0) profile2_eval(R.cfg, R.na, t, R.tsel, area, dummy);
+    if (R.na > 0) pwl_eval(R.a_t, R.a_v, R.na, t, R.tsel, area, dummy);
     const double mcp = R.mass * cpm;
     const double q1 = R.htc * area * ERG_PER_CAL;
     fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;

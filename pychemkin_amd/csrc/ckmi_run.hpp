@@ -56,7 +56,7 @@ __device__ __forceinline__ double ign_peak_time(const Ign& g) {
 struct DevCfg {
   ckmi_reactor_cfg c;
   int ncrit;
-  double tcrit[128];
+  double tcrit[192];  // breakpoints of the three profiles (64 each)
 };
 __device__ __forceinline__ int n_crit(const DevCfg* d) { return d->ncrit + 1; }
 __device__ __forceinline__ double crit_time(const DevCfg* d, double tend, int idx) {

@@ -106,8 +106,8 @@ def test_volume_profile_cfg(chem):
     cfg = r.reactor_cfg()
     assert cfg.prof2_kind == 1 and cfg.nprof2 == 2 and cfg.nprof == 3
     r.set_heat_transfer_area_profile([0.0, 0.05], [1.0, 2.0])
-    with pytest.raises(ReactorError):  # QPRO together with AEXT is not on the device path yet
-        r.reactor_cfg()
+    cfg = r.reactor_cfg()  # QPRO with AEXT: QPRO in the second slot, AEXT in the third
+    assert cfg.prof2_kind == 1 and cfg.nprof2 == 2 and cfg.nprof3 == 2 and list(cfg.prof3_v[:2]) == [1.0, 2.0]
 
 
 def test_temperature_profile_cfg(chem):

@@ -49,7 +49,10 @@ def test_gfac_and_heat_loss_vs_oracle(dm, oracle, mech):
     Y0 = ch4_air_Y(mech, 1.0)
     cases = [dict(gfac=2.0), dict(qloss=0.5), dict(htc=2e-3, areaq=5.0, tamb=400.0),
              dict(profile2=([0.0, 0.02], [0.0, 1.0]), prof2_kind=1),
-             dict(htc=2e-3, areaq=5.0, tamb=400.0, profile2=([0.0, 0.01, 0.02], [2.0, 8.0, 8.0]), prof2_kind=2)]
+             dict(htc=2e-3, areaq=5.0, tamb=400.0, profile2=([0.0, 0.01, 0.02], [2.0, 8.0, 8.0]), prof2_kind=2),
+             # QPRO together with AEXT (batchreactor.py:2005-2067)
+             dict(htc=2e-3, tamb=400.0, profile2=([0.0, 0.02], [0.0, 1.0]), prof2_kind=1,
+                  profile3=([0.0, 0.01, 0.03], [2.0, 8.0, 6.0]))]
     for kw in cases:
         cfg = dict(energy=1, t_end=0.05, atol=1e-10, rtol=1e-8, ign_mode="TIFP", **kw)
         res = dm.reactor_run(_native.make_cfg(**cfg), np.array([1, 2], np.int32), [1250.0, 1250.0],

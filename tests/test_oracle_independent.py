@@ -102,6 +102,17 @@ def test_heat_loss_energy_balance_inert(oracle, mech):
     r3, _ = oracle.reactor(T0, P_ATM, V0, Y, energy=1, t_end=tend, atol=1e-12, rtol=1e-10,
                            profile2=([0.0, tend], [0.0, 2 * Q]), prof2_kind=1)
     assert abs(r3.T / T_exact - 1) < 1e-7
+    # QPRO together with AEXT (batchreactor.py:2005-2067): heat loss QPRO(t) + HTC AEXT(t) (T - TAMB).
+    # A constant AEXT profile equals AREAQ; wall transfer from TAMB = T0 gives back part of the loss
+    kw = dict(energy=1, t_end=tend, atol=1e-12, rtol=1e-10, htc=1e-3, profile2=([0.0, tend], [0.0, 2 * Q]),
+              prof2_kind=1)
+    r4, _ = oracle.reactor(T0, P_ATM, V0, Y, tamb=T0, profile3=([0.0, tend], [20.0, 20.0]), **kw)
+    r5, _ = oracle.reactor(T0, P_ATM, V0, Y, tamb=T0, areaq=20.0, **kw)
+    assert r4.status == 0 and abs(r4.T / r5.T - 1) < 1e-12
+    assert T_exact + 1.0 < r4.T < T0
+    r6, _ = oracle.reactor(T0, P_ATM, V0, Y, tamb=T0, profile3=([0.0, tend], [0.0, 40.0]), **kw)
+    # the ramp's area (mean 20) weighs the late times, when the charge is furthest below TAMB
+    assert r4.T + 1.0 < r6.T < T0
 
 
 def test_temperature_profile_given_T(oracle, mech):
