@@ -1167,7 +1167,11 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   I.o_geff = geff.empty() ? put(&dzero, 8) : put(geff.data(), geff.size() * 8);
   // dense efficiency rows: only the reactor kernel's CKMI_MG_DENSE variant reads them, and only for
   // KK <= 63; larger mechanisms get a one-row stub so that the image fits in LDS (G x KKp grows fast)
+#ifdef CKMI_MG_DENSE
   const bool dense = KK <= SP_ONE;
+#else
+  const bool dense = false;  // only the CKMI_MG_DENSE reactor variant reads the dense rows
+#endif
   std::vector<double> geffd(dense ? (size_t)std::max(G, 1) * KKp : (size_t)2, 0.0);
   for (int g = 0; dense && g < G; ++g)
     for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)g * KKp + gsp[e]] = geff[e];
