@@ -234,3 +234,32 @@ def test_reaction_rates_golden_through_kin_call(K, mech):
     order = nz[np.argsort(-net[nz], kind="stable")]
     assert order.tolist() == g["state-order_1800"]
     assert np.all(within(net[order], g["rate-net_reaction_rate_1800"], *g["tolerance-ROP"]))
+
+
+def test_qpro_with_aext_through_kin_calls(K, mech, oracle):
+    """set_heat_loss_profile + set_heat_transfer_area_profile together (batchreactor.py:2005-2067,
+    QPRO and AEXT through KINAll0D_SetProfileParameter, either order) with HTC / TAMB keywords:
+    the heat loss is QPRO(t) + HTC AEXT(t) (T - TAMB); against the oracle."""
+    from conftest import ch4_air_Y
+
+    L, cs = K
+    Y0 = ch4_air_Y(mech, 1.0)[0]
+    xq, vq = np.array([0.0, 0.02]), np.array([0.0, 1.0])
+    xa, va = np.array([0.0, 0.01, 0.03]), np.array([2.0, 8.0, 6.0])
+    ref, _ = oracle.reactor(1250.0, 2 * P_ATM, 3.0, Y0, problem=1, energy=1, t_end=0.05, atol=1e-10, rtol=1e-8,
+                            ign_mode="TIFP", htc=2e-3, tamb=400.0, profile2=(xq, vq), prof2_kind=1,
+                            profile3=(xa, va))
+    assert ref.status == 0  # the heat loss holds this charge below ignition (tau = -1 on both sides)
+    for order in (("QPRO", "AEXT"), ("AEXT", "QPRO")):
+        _setup(L, cs, 1, 1, 0.05, 1250.0, 2 * P_ATM, 3.0, Y0)
+        for key in order:
+            x, v = (xq, vq) if key == "QPRO" else (xa, va)
+            assert L.KINAll0D_SetProfileParameter(key.encode(), ct.byref(ct.c_int(len(x))), x, v) == 0
+        for line in ("ATOL    1e-10", "RTOL    1e-08", "TIFP", "HTC    2e-3", "TAMB    400"):
+            assert L.KINAll0D_SetUserKeyword(line.encode()) == 0, line
+        assert L.KINAll0D_Calculate(ct.byref(cs)) == 0, L.ckmi_kin_last_error()
+        tau = ct.c_double(0.0)
+        assert L.KINAll0D_GetIgnitionDelay(ct.byref(tau)) == 0
+        assert (abs(tau.value / ref.tau - 1) < 1e-4) if ref.tau > 0 else tau.value == ref.tau, order
+        t, T, P, V, Y = _solution(L, mech.KK)
+        assert abs(T[-1] / ref.T - 1) < 1e-5, order
