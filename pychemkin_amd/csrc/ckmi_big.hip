@@ -1733,7 +1733,8 @@ int launch_big_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const React
                                                " species are not supported (the ROP/thermo kernels are)");
   if (m->has_plog)
     return set_error(CKMI_ERR_UNSUPPORTED,
-                     "PLOG / chemically activated reactions in batch reactors with more than 63 species");
+                     "PLOG / chemically activated / FORD-RORD-fractional-order reactions in batch reactors with "
+                     "more than 63 species");
   switch ((nvar + 15) / 16) {  // NB: register blocks per dimension (NC = 16 NB >= n)
     case 1:
     case 2:

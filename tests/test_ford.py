@@ -197,8 +197,8 @@ def fdm(fmech):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 17, 1000])
-def test_ford_gpu_rop(fmech, forc, fdm, n):
+@pytest.mark.parametrize("n", [1, 17, 1000, 20000])  # 20,000: the automatic path falls back from the
+def test_ford_gpu_rop(fmech, forc, fdm, n):          # specialised kernel (which declines FORD) to the generic one
     T, P, Y = _states(fmech.KK, n, seed=n)
     Y[3, :] = 0.0  # CH2 absent: a non-integral order of a zero concentration
     w, cp, h = (x.cpu().numpy() for x in fdm.rop_thermo(T, P, Y))
