@@ -966,8 +966,10 @@ __global__ __launch_bounds__(rop_waves(NCH)* WAVE) void rop_kernel(MechImage img
           o1[(size_t)oi * nstate + st] = qr;
         } else {
           const double q = qf - qr;
+          const bool s23 = __ballot(nr > 2 || np > 2) != 0;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
+            if (u >= 2 && !s23) break;
             if (u < nr) atomicAdd(&wdot[sp_of(rs, u)], -q);
             if (u < np) atomicAdd(&wdot[sp_of(ps, u)], q);
           }
@@ -1347,9 +1349,19 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   // ---- order reactions: elementary, then third-body, then falloff
   std::vector<int> ordr;
   // strips stay type-uniform: chemically activated reactions run in the falloff strips
+  // within a type, reactions with at most 2 unit slots per side first: the strips that hold only
+  // those skip the slot-2/3 gathers wave-uniformly (eval_rxn_img); general reactions last
+  auto slot_class = [&](int i) -> int {
+    if (rxn_general(d, i)) return 2;
+    double ur = 0.0, up = 0.0;
+    for (int u = 0; u < d->nr[i]; ++u) ur += d->rnu[4 * i + u];
+    for (int u = 0; u < d->np[i]; ++u) up += d->pnu[4 * i + u];
+    return (ur > 2.0 || up > 2.0) ? 1 : 0;
+  };
   for (int t : {CKMI_RXN_ELEMENTARY, CKMI_RXN_THIRDBODY, CKMI_RXN_FALLOFF, CKMI_RXN_CHEMACT, CKMI_RXN_PLOG})
-    for (int i = 0; i < II; ++i)
-      if (d->rtype[i] == t) ordr.push_back(i);
+    for (int cls = 0; cls < 3; ++cls)
+      for (int i = 0; i < II; ++i)
+        if (d->rtype[i] == t && slot_class(i) == cls) ordr.push_back(i);
   for (int i = 0; i < II; ++i) {
     if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_CHEMACT) {
       delete m;

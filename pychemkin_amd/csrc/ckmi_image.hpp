@@ -260,6 +260,10 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
   double kr = 0.0, dlkr = 0.0;
   const int r0 = sp_of(rs, 0), r1 = sp_of(rs, 1), r2 = sp_of(rs, 2), r3 = sp_of(rs, 3);
   const int p0 = sp_of(ps, 0), p1 = sp_of(ps, 1), p2 = sp_of(ps, 2), p3 = sp_of(ps, 3);
+  // slots 2 and 3 hold the dummy species (C = 1, g = h = 0) unless some lane of the wave has a
+  // third molecule on a side: reactions are ordered so that most strips have none, and those
+  // skip 8 gathers as a wave; the results are bitwise those of the full four-slot forms
+  const bool s23 = __ballot(rx_nr(inf) > 2 || rx_np(inf) > 2) != 0;
   if (rx_rev(inf)) {
     if (rx_hasrev(inf)) {
       kr = fexp(ax[8] + ax[9] * lnT - ax[10] * invT, e2t);
@@ -267,7 +271,12 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
       dlkr = (ax[9] + ax[10] * invT) * invT;
     } else {
       // unit-coefficient slots: sum_products g - sum_reactants g, dnu = np - nr
-      const double dG = (gRT[p0] + gRT[p1]) + (gRT[p2] + gRT[p3]) - ((gRT[r0] + gRT[r1]) + (gRT[r2] + gRT[r3]));
+      double gp = gRT[p0] + gRT[p1], gr = gRT[r0] + gRT[r1];
+      if (s23) {
+        gp += gRT[p2] + gRT[p3];
+        gr += gRT[r2] + gRT[r3];
+      }
+      const double dG = gp - gr;
       const int dnu = rx_np(inf) - rx_nr(inf);
       kr = kf * fexp(dG - dnu * lnPRT, e2t);
       if (need_h) {
@@ -276,8 +285,11 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
       }
     }
   }
-  const double pf = (C[r0] * C[r1]) * (C[r2] * C[r3]);
-  const double pr = (C[p0] * C[p1]) * (C[p2] * C[p3]);
+  double pf = C[r0] * C[r1], pr = C[p0] * C[p1];
+  if (s23) {
+    pf *= C[r2] * C[r3];
+    pr *= C[p2] * C[p3];
+  }
   Rxn e;
   e.kf = kf * gfac;  // GFAC scales forward and reverse rates alike
   e.kr = kr * gfac;

@@ -276,8 +276,10 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
         if (u < np) L.wdot()[sp_of(ps, u)] = q;
       }
 #else
+      const bool s23 = __ballot(nr > 2 || np > 2) != 0;  // wave-uniform: slots 2, 3 in use anywhere
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+        if (u >= 2 && !s23) break;
         if (u < nr) atomicAdd(&L.wdot()[sp_of(rs, u)], -q);
         if (u < np) atomicAdd(&L.wdot()[sp_of(ps, u)], q);
       }
