@@ -91,12 +91,12 @@ __host__ __device__ constexpr int jscratch_bytes() {
 //
 // The integrator (CVODE-style variable-order BDF with modified Newton, control flow identical
 // to oracle/ckoracle.c) is written as a wave-uniform state machine whose only RHS evaluation,
-// LU factorisation and triangular solve each appear ONCE in the loop: the LU factors of
-// M = I - gamma J then stay in VGPRs for the life of the wave without spilling.
+// factorisation and solve each appear ONCE in the loop: the explicit inverse of M = I - gamma J
+// then stays in VGPRs for the life of the wave.
 // Waves per workgroup by Newton-matrix form: 12 (3 per SIMD) with the FP32-stored inverse, whose
 // 54 VGPRs leave room for a third wave per SIMD within 168 VGPRs (+16 % reactors/s on configs[2]
-// over 8 waves with the FP64 inverse, MI355X; the FP64 factorisation phase spills ~180 VGPRs to
-// scratch, outside the RHS); 8 (2 per SIMD) with the FP64 inverse (256 VGPRs).
+// over 8 waves with the FP64 inverse, MI355X, although the 168-VGPR allocation spills ~28 values
+// per step to scratch); 8 (2 per SIMD) with the FP64 inverse (256 VGPRs).
 __host__ __device__ constexpr int rwaves(bool f64) { return f64 ? 8 : 12; }
 // PL: the mechanism has PLOG / chemically activated / general reactions; F64: FP64-stored inverse
 template <int N, bool PL = false, bool F64 = false>

@@ -8,10 +8,11 @@
 //
 // Per wave (= reactor):
 //   lanes 0..n-1  one state component each (lane 0 = T, lane k = Y_{k-1}),
-//   VGPRs         the LU factors of M = I - gamma J (row-per-lane, N doubles per lane) and the
-//                 Nordsieck history,
+//   VGPRs         the explicit inverse of M = I - gamma J (row-per-lane: N floats per lane, or
+//                 N doubles in the FP64 form) and the per-lane BDF vectors,
 //   LDS           the workgroup's mechanism image (shared), a per-wave slice of species
-//                 vectors and integrator scalars, and one J assembly scratch per workgroup
+//                 vectors, the Nordsieck history and the integrator scalars, and one J assembly
+//                 scratch per workgroup
 //                 (lock-protected; Jacobian evaluations are ~2 % of the RHS calls),
 //   HBM           the wave's last Jacobian (column-major), reloaded when only gamma changes.
 #pragma once
