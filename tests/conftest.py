@@ -85,6 +85,27 @@ def h2_air_Y(mech):
     return Y / Y.sum()
 
 
+def check_h2_golden(g, mech, t, T, Y, wdot_h2o, min_ok=101):
+    """All five columns of closed_homogeneous__transient.baseline, each point within the golden's
+    own per-column tolerance (closed_homogeneous__transient.py:195-207).  ``Y`` is the saved
+    mass-fraction trajectory [npts, KK]; X_H2O and the density follow from it as the reference's
+    solution mixtures compute them; ``wdot_h2o`` is the caller's ROP()[H2O] at each point."""
+    R = 1.3806504e-16 * 6.02214179e23
+    P = P_ATM
+    Y = np.asarray(Y, dtype=np.float64)
+    k = mech.species.index("H2O")
+    X = Y[:, k] / mech.wt[k] / np.sum(Y / mech.wt, axis=1)
+    rho = P / (R * np.asarray(T)) / np.sum(Y / mech.wt, axis=1)
+    assert np.asarray(t).tolist() == g["state-time"]
+    cols = {"state-temperature": (T, "tolerance-var"), "species-H2O_mole_fraction": (X, "tolerance-frac"),
+            "rate-H2O_production_rate": (wdot_h2o, "tolerance-ROP"), "state-density": (rho, "tolerance-var")}
+    counts = {}
+    for key, (v, tol) in cols.items():
+        counts[key] = int(within(v, g[key], *g[tol]).sum())
+    assert all(c >= min_ok for c in counts.values()), counts
+    return counts
+
+
 def sensitivity_mixture(chem):
     """sensitivity.py:66-86: C3H8:CH4:H2 = 0.1:0.8:0.1 fuel, O2:N2 = 1:3.76, phi = 1.1, 900 K, 1 atm."""
     import pychemkin_amd as ck

@@ -8,7 +8,7 @@ import ctypes as ct
 import numpy as np
 import pytest
 
-from conftest import P_ATM, golden, h2_air_Y, within
+from conftest import P_ATM, check_h2_golden, golden, h2_air_Y, within
 
 pytestmark = pytest.mark.gpu
 
@@ -163,15 +163,20 @@ def test_h2_golden_through_kin_calls(K, mech):
     tau = ct.c_double(0.0)
     assert L.KINAll0D_GetIgnitionDelay(ct.byref(tau)) == 0
     t, T, P, V, Y = _solution(L, mech.KK)
-    assert t.tolist() == g["state-time"]
     Tg = np.asarray(g["state-temperature"])
-    assert within(T, Tg, *g["tolerance-var"]).sum() >= 90
-    assert abs(T[-1] / Tg[-1] - 1) < 2e-5
-    assert abs(tau.value / np.interp(1400.0, Tg, t) - 1) < 2e-3
     assert np.allclose(P, P_ATM, rtol=1e-14)
-    rho = P / (RU * T * (Y / mech.wt[:, None]).sum(axis=0))
-    assert np.all(np.abs(rho / np.asarray(g["state-density"]) - 1) < 2e-3)
     assert np.allclose(Y.sum(axis=0), 1.0, atol=1e-10)
+    # closed_homogeneous__transient.py:176-181: ROP()[H2O] of each solution mixture, via KINGetGasROP
+    k = mech.species.index("H2O")
+    wdot = np.zeros(mech.KK)
+    rop = np.zeros(len(t))
+    for i in range(len(t)):
+        assert L.KINGetGasROP(ct.byref(cs), ct.byref(ct.c_double(T[i])), ct.byref(ct.c_double(P[i])),
+                              np.ascontiguousarray(Y[:, i]), wdot) == 0
+        rop[i] = wdot[k]
+    check_h2_golden(g, mech, t, T, Y.T, rop, min_ok=99)
+    assert abs(T[-1] / Tg[-1] - 1) < 1e-6
+    assert abs(tau.value / np.interp(1400.0, Tg, t) - 1) < 1e-4
 
 
 def test_conv_volume_profile_golden_through_kin_calls(K, mech, chem, oracle):

@@ -8,7 +8,7 @@ tests assert the north_star bar plus a tighter "same algorithm" bar on tau (1e-4
 import numpy as np
 import pytest
 
-from conftest import P_ATM, ch4_air_Y, golden, h2_air_Y, within
+from conftest import P_ATM, ch4_air_Y, check_h2_golden, golden, h2_air_Y, within
 
 pytestmark = pytest.mark.gpu
 
@@ -104,7 +104,7 @@ def test_ignition_definitions(dm, oracle, mech, mode, val, target, stop):
         assert np.all(res["stats"][:, 0] < np.array([r.nst for r, _ in ref]) * 1.5 + 50)
 
 
-def test_h2_air_golden_through_drop_in_api(chem):
+def test_h2_air_golden_through_drop_in_api(chem, mech):
     """closed_homogeneous__transient.py:61-131 through the PyChemkin-style API on the GPU."""
     import pychemkin_amd as ck
 
@@ -123,14 +123,17 @@ def test_h2_air_golden_through_drop_in_api(chem):
     r.process_solution()
     t = r.get_solution_variable_profile("time")
     T = r.get_solution_variable_profile("temperature")
-    assert t.tolist() == g["state-time"]
     Tg = np.asarray(g["state-temperature"])
-    assert within(T, Tg, *g["tolerance-var"]).sum() >= 90
-    assert abs(T[-1] / Tg[-1] - 1) < 2e-5
+    mixes = [r.get_solution_mixture_at_index(i) for i in range(len(t))]
+    k = chem.get_specindex("H2O")
+    Y = np.stack([mx.Y for mx in mixes])
+    wdot = np.array([mx.ROP()[k] for mx in mixes])  # closed_homogeneous__transient.py:176-181
+    rho = np.array([mx.RHO for mx in mixes])
+    check_h2_golden(g, mech, t, T, Y, wdot, min_ok=99)
+    assert np.all(within(rho, g["state-density"], *g["tolerance-var"]))
+    assert abs(T[-1] / Tg[-1] - 1) < 1e-6
     tg = np.interp(1400.0, Tg, t)
-    assert abs(r.get_ignition_delay() * 1e-3 / tg - 1) < 2e-3
-    rho = np.array([r.get_solution_mixture_at_index(i).RHO for i in range(len(t))])
-    assert np.all(np.abs(rho / np.asarray(g["state-density"]) - 1) < 2e-3)
+    assert abs(r.get_ignition_delay() * 1e-3 / tg - 1) < 1e-4
 
 
 def test_rcm_conv_volume_profile_golden(chem, oracle, mech):

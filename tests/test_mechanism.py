@@ -53,9 +53,9 @@ def test_tables_layout(tables):
     assert tables["rsp"].shape == (325, 4) and tables["arr"].shape == (325, 3)
     assert tables["thermo"].shape == (53, 17)
     assert tables["eff_ptr"].shape == (326,)
-    # E/R of H+O2<=>O+OH: 17041 cal/mol / R [cal/mol-K]
-    from pychemkin_amd.constants import R_GAS_CAL
-    assert abs(tables["arr"][37, 2] / (17041.0 / R_GAS_CAL) - 1) < 1e-14
+    # E/R of H+O2<=>O+OH: 17041 cal/mol / RUC, Chemkin's activation-energy gas constant
+    # (8.314510e7 / 4.184e7 cal/mol-K, mechanism.RU_ACT), not constants.R_GAS_CAL
+    assert abs(tables["arr"][37, 2] / (17041.0 / (8.314510e7 / 4.184e7)) - 1) < 1e-14
 
 
 CHEM_MINI = """ELEMENTS H O N END

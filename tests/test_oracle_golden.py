@@ -2,8 +2,8 @@
 import numpy as np
 import pytest
 
-from conftest import (P_ATM, SENS_FACTOR, SENS_RUN, ch4_air_Y, golden, h2_air_Y, sensitivity_mixture, top5,
-                      within)
+from conftest import (P_ATM, SENS_FACTOR, SENS_RUN, ch4_air_Y, check_h2_golden, golden, h2_air_Y,
+                      sensitivity_mixture, top5, within)
 
 R = 1.3806504e-16 * 6.02214179e23
 
@@ -35,26 +35,25 @@ def test_n2_cv_speciesproperties_baseline(oracle, mech):
 
 
 def test_h2_air_conp_trajectory(oracle, mech):
-    """closed_homogeneous__transient.py:61-131: CONP, 1000 K, 1 atm, t_end 0.5 ms, 1e-20/1e-8, NNEG, DTIGN 400."""
+    """closed_homogeneous__transient.py:61-131: CONP, 1000 K, 1 atm, t_end 0.5 ms, 1e-20/1e-8, NNEG, DTIGN 400.
+
+    All five golden columns on all 101 points, the ignition front included.  Round 2 held X_H2O on
+    53/101 and wdot_H2O on 82/101: the radical pool grew 1e-4 slower than Chemkin's because E [cal/mol]
+    was converted with R_GAS_CAL instead of Chemkin's RUC = 8.314510e7 / 4.184e7 (mechanism.RU_ACT)."""
     g = golden("closed_homogeneous__transient")
     ts = np.asarray(g["state-time"])
     Y0 = h2_air_Y(mech)
     res, Yend, (ts, ys, ps, vs) = oracle.reactor(1000.0, P_ATM, 1.0, Y0, t_save=ts, problem=1, energy=1, t_end=5e-4,
                                                  atol=1e-20, rtol=1e-8, nneg=True, ign_mode="T_rise", ign_val=400.0)
     assert res.status == 0
-    T = ys[:, 0]
+    k = mech.species.index("H2O")
+    rop = np.array([oracle.rates(ys[i, 0], ps[i], ys[i, 1:])[2][k] for i in range(len(ts))])
+    check_h2_golden(g, mech, ts, ys[:, 0], ys[:, 1:], rop, min_ok=101)
     Tg = np.asarray(g["state-temperature"])
-    ok = within(T, Tg, *g["tolerance-var"])
-    # every point but the steepest few (ignition front, |dT/dt| ~ 6e7 K/s) within the golden tolerance
-    assert ok.sum() >= 90
-    assert abs(T[-1] / Tg[-1] - 1) < 2e-5
-    assert np.max(np.abs(T / Tg - 1)) < 2e-3
+    assert np.max(np.abs(ys[:, 0] / Tg - 1)) < 1e-6  # measured 3.6e-7, at the ignition front
+    assert abs(ys[-1, 0] / Tg[-1] - 1) < 1e-7
     # ignition time (T0 + 400 K) from the golden trajectory by interpolation
-    tg = np.interp(1400.0, Tg, ts)
-    assert abs(res.tau / tg - 1) < 2e-3
-    # density column
-    rho = P_ATM / (R * T) / np.sum(ys[:, 1:] / mech.wt, axis=1)
-    assert np.all(within(rho, g["state-density"], *g["tolerance-var"]) | (np.abs(rho / np.asarray(g["state-density"]) - 1) < 2e-3))
+    assert abs(res.tau / np.interp(1400.0, Tg, ts) - 1) < 2e-5
 
 
 def test_ch4_air_rcm_conv_with_volume_profile(oracle, mech):
@@ -87,6 +86,7 @@ def test_reaction_rates_1800K_ordering(oracle, mech):
     CKKFKR(P, T, X) convention).  The golden rates are those of the state whose mole fractions
     equal the mixture's mass fractions: reproduced to <= 1.4e-5 that way (3 of 5 to 1e-14), while
     reading the array as mass fractions misses by 0.85-1.82x (the round-1 "parity partial").
+    With Chemkin's activation-energy gas constant (mechanism.RU_ACT) all 5 agree to ~1e-14.
     """
     g = golden("reactionrates")
     Y0 = ch4_air_Y(mech, 1.0)[0]
@@ -103,7 +103,7 @@ def test_reaction_rates_1800K_ordering(oracle, mech):
     order, net = net_order(y_as_x)
     assert order.tolist() == g["state-order_1800"]
     assert np.all(within(net, gold, *g["tolerance-ROP"]))
-    assert np.max(np.abs(net / gold - 1)) < 2e-5
+    assert np.max(np.abs(net / gold - 1)) < 1e-12
     # the same rates read as mass fractions: same ordering, magnitudes off by up to 1.8x
     order_m, net_m = net_order(Y0)
     assert order_m.tolist() == g["state-order_1800"]
