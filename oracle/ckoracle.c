@@ -35,22 +35,36 @@ void cko_thermo(const cko_mech* m, double T, double* cp_R, double* h_RT, double*
   }
 }
 
-/* C^o for a reaction order o (stoichiometric coefficient, or FORD / RORD): exact products for
- * o = 0..3; otherwise pow(C, o) for C > 0 and 0 for C <= 0 (a real power of a negative
- * concentration is undefined; the device kernels use the same rule) */
+/* C^o for a reaction order o (stoichiometric coefficient, or FORD / RORD) -- one rule on every
+ * implementation (oracle/numpy_ref.py _cpow, pychemkin_amd/csrc/ckmi_image.hpp conc_pow):
+ *   o in {0, 1, 2, 3}: exact products;
+ *   0 < o < 1 (non-integral): C^o for C >= CFLOOR, and the chord CFLOOR^(o-1) C below it (negative
+ *     concentrations included), so the rate is Lipschitz at C = 0.  Without this the rate of a species
+ *     that runs out is non-Lipschitz there (d C^o/dC unbounded, flat for C <= 0): the BDF corrector
+ *     then settles into a period-2 cycle at C ~ 0 with the step size locked, and at some tolerances
+ *     the integration hits max steps (case 1 of tests/test_ford.py at rtol 0.97e-8).
+ *     The chord changes the rate only below 1e-14 mol/cm3 (this implementation's choice: the
+ *     reference holds no FORD golden, parity unpinned);
+ *   any other o: pow(C, o) for C > 0 and 0 for C <= 0. */
+#define CFLOOR 1e-14
 static double conc_pow(double c, double o) {
   if (o == 0.0) return 1.0;
   if (o == 1.0) return c;
   if (o == 2.0) return c * c;
   if (o == 3.0) return c * c * c;
+  if (o < 1.0 && c < CFLOOR) return pow(CFLOOR, o - 1.0) * c;
   return c > 0.0 ? pow(c, o) : 0.0;
 }
-/* d C^o / dC under the same rule (0 for C <= 0 at a non-integral order) */
+/* the Jacobian's d C^o / dC under the same rule.  For 0 < o < 1 it is the chord slope
+ * max(C, CFLOOR)^(o-1) (exact below CFLOOR, >= the tangent o C^(o-1) above it): C^o is concave, so
+ * the tangent lets the modified Newton iteration overshoot past C = 0 and cycle; the chord damps it
+ * (only the Newton matrix changes, not the rates). */
 static double dconc_pow(double c, double o) {
   if (o == 0.0) return 0.0;
   if (o == 1.0) return 1.0;
   if (o == 2.0) return 2.0 * c;
   if (o == 3.0) return 3.0 * c * c;
+  if (o < 1.0) return pow(fmax(c, CFLOOR), o - 1.0);
   return c > 0.0 ? o * pow(c, o - 1.0) : 0.0;
 }
 /* order of reactant slot s / product slot s of reaction i */

@@ -16,13 +16,20 @@ RU = BOLTZMANN * AVOGADRO
 PATM = 1.01325e6
 
 
+CFLOOR = 1e-14  # oracle/ckoracle.c CFLOOR
+
+
 def _cpow(C, o):
-    """C ** o elementwise; a non-integral order of a concentration <= 0 gives 0 (the rule of
-    oracle/ckoracle.c conc_pow and of the device kernels)."""
-    with np.errstate(invalid="ignore", divide="ignore"):
+    """C ** o elementwise under the rule of oracle/ckoracle.c conc_pow and the device kernels:
+    exact for o in {0, 1, 2, 3}; for 0 < o < 1 the chord CFLOOR^(o-1) C below CFLOOR (negative C
+    included); otherwise 0 for C <= 0."""
+    C, o = np.broadcast_arrays(np.asarray(C, dtype=np.float64), np.asarray(o, dtype=np.float64))
+    with np.errstate(invalid="ignore", divide="ignore", over="ignore"):
         r = np.power(C, o)
-    frac = o != np.round(o)
-    return np.where(frac & (C <= 0.0), 0.0, r)
+        chord = np.power(CFLOOR, o - 1.0) * C
+    exact = (o == 0.0) | (o == 1.0) | (o == 2.0) | (o == 3.0)
+    r = np.where(~exact & (C <= 0.0), 0.0, r)
+    return np.where(~exact & (o < 1.0) & (C < CFLOOR), chord, r)
 
 
 class NumpyKinetics:

@@ -309,21 +309,27 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
 constexpr uint32_t RX_GEN = 0x4000u;
 constexpr int GEN_RECORDS = 3;  // 2 + 24 doubles
 
-// C^o for a reaction order o: exact products for o = 0..3, else exp(o ln C) for C > 0 and 0 for
-// C <= 0 (oracle/ckoracle.c conc_pow, same rule)
+// C^o for a reaction order o, the rule of oracle/ckoracle.c conc_pow: exact products for
+// o = 0..3; for 0 < o < 1 C^o above CONC_FLOOR and the chord CONC_FLOOR^(o-1) C below it (negative
+// C included: Lipschitz through C = 0); otherwise exp(o ln C) for C > 0 and 0 for C <= 0
+constexpr double CONC_FLOOR = 1e-14;       // [mol/cm3]
+constexpr double LN_CONC_FLOOR = -32.236191301916641;  // ln(1e-14)
 __device__ __forceinline__ double conc_pow(double c, double o, const double* e2t) {
   if (o == 1.0) return c;
   if (o == 2.0) return c * c;
   if (o == 0.0) return 1.0;
   if (o == 3.0) return c * c * c;
+  if (o < 1.0 && c < CONC_FLOOR) return fexp((o - 1.0) * LN_CONC_FLOOR, e2t) * c;
   return c > 0.0 ? fexp(o * log(c), e2t) : 0.0;
 }
-// d C^o / dC under the same rule (oracle dconc_pow)
+// The Jacobian's d C^o / dC (oracle dconc_pow): the chord slope max(C, CONC_FLOOR)^(o-1) for
+// 0 < o < 1 (damps the modified Newton iteration where C^o is concave), the tangent otherwise
 __device__ __forceinline__ double dconc_pow(double c, double o, const double* e2t) {
   if (o == 1.0) return 1.0;
   if (o == 2.0) return 2.0 * c;
   if (o == 0.0) return 0.0;
   if (o == 3.0) return 3.0 * c * c;
+  if (o < 1.0) return fexp((o - 1.0) * (c > CONC_FLOOR ? log(c) : LN_CONC_FLOOR), e2t);
   return c > 0.0 ? o * fexp((o - 1.0) * log(c), e2t) : 0.0;
 }
 
