@@ -87,6 +87,14 @@ PROTOTYPES = {
     "ckmi_lu_factor_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
     "ckmi_lu_solve_batched": (ct.c_int, [ct.c_int32, ct.c_int32, _P, _P, _P, _P]),
     "ckmi_lu_last_error": (ct.c_char_p, []),
+    "ckmi_parse_mechanism": (ct.c_int, [ct.c_char_p, ct.c_char_p, ct.POINTER(_P)]),
+    "ckmi_parse_files": (ct.c_int, [ct.c_char_p, ct.c_char_p, ct.POINTER(_P)]),
+    "ckmi_parse_last_error": (ct.c_char_p, []),
+    "ckmi_parsed_free": (None, [_P]),
+    "ckmi_parsed_sizes": (ct.c_int, [_P, ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32), ct.POINTER(ct.c_int32)]),
+    "ckmi_parsed_desc": (ct.c_int, [_P, ct.POINTER(MechDesc)]),
+    "ckmi_parsed_symbols": (ct.c_int, [_P, _P, _P, _P, _P]),
+    "ckmi_parsed_equation": (ct.c_int, [_P, ct.c_int32, ct.c_char_p, ct.c_int32, ct.POINTER(ct.c_int32)]),
 }
 LU_NMAX = 192
 
@@ -110,6 +118,67 @@ def _check(rc: int, what: str) -> None:
     if rc != 0:
         msg = lib().ckmi_last_error().decode(errors="replace")
         raise NativeError(f"{what} failed (code {rc}): {msg}")
+
+
+# ckmi_mech_desc fields -> (dtype, shape given KK, II, npl)
+_DESC_LAYOUT = {
+    "wt": (np.float64, lambda K, I, n: (K,)), "thermo": (np.float64, lambda K, I, n: (K, 17)),
+    "rtype": (np.int32, lambda K, I, n: (I,)), "rev": (np.int32, lambda K, I, n: (I,)),
+    "nr": (np.int32, lambda K, I, n: (I,)), "np": (np.int32, lambda K, I, n: (I,)),
+    "rsp": (np.int32, lambda K, I, n: (I, 4)), "psp": (np.int32, lambda K, I, n: (I, 4)),
+    "rnu": (np.float64, lambda K, I, n: (I, 4)), "pnu": (np.float64, lambda K, I, n: (I, 4)),
+    "arr": (np.float64, lambda K, I, n: (I, 3)), "low": (np.float64, lambda K, I, n: (I, 3)),
+    "revp": (np.float64, lambda K, I, n: (I, 3)), "has_rev": (np.int32, lambda K, I, n: (I,)),
+    "ftype": (np.int32, lambda K, I, n: (I,)), "fpar": (np.float64, lambda K, I, n: (I, 5)),
+    "tbsp": (np.int32, lambda K, I, n: (I,)), "eff_ptr": (np.int32, lambda K, I, n: (I + 1,)),
+    "plog_ptr": (np.int32, lambda K, I, n: (I + 1,)),
+    "ford": (np.float64, lambda K, I, n: (I, 4)), "rord": (np.float64, lambda K, I, n: (I, 4)),
+}
+
+
+def parse_mechanism(chem_text: str, therm_text: str = ""):
+    """Run libckmi's native Chemkin interpreter (the parse half of KINPreProcess; host only, no GPU).
+
+    Returns (tables, species, elements, awt, ncf, equations) with ``tables`` in the layout of
+    ``Mechanism.to_tables()``; raises NativeError with the interpreter's message on a bad file."""
+    L = lib()
+    h = _P()
+    rc = L.ckmi_parse_mechanism(chem_text.encode(), (therm_text or "").encode(), ct.byref(h))
+    if rc != 0:
+        raise NativeError(f"ckmi_parse_mechanism failed (code {rc}): "
+                          f"{L.ckmi_parse_last_error().decode(errors='replace')}")
+    try:
+        MM, KK, II = ct.c_int32(), ct.c_int32(), ct.c_int32()
+        L.ckmi_parsed_sizes(h, ct.byref(MM), ct.byref(KK), ct.byref(II))
+        MM, KK, II = MM.value, KK.value, II.value
+        d = MechDesc()
+        L.ckmi_parsed_desc(h, ct.byref(d))
+        ne = int(np.ctypeslib.as_array(ct.cast(d.eff_ptr, ct.POINTER(ct.c_int32)), (II + 1,))[-1])
+        npl = int(np.ctypeslib.as_array(ct.cast(d.plog_ptr, ct.POINTER(ct.c_int32)), (II + 1,))[-1])
+        t = {"KK": np.int32(KK), "II": np.int32(II)}
+        for name, (dt, shp) in _DESC_LAYOUT.items():
+            cty = ct.c_double if dt == np.float64 else ct.c_int32
+            t[name] = np.ctypeslib.as_array(ct.cast(getattr(d, name), ct.POINTER(cty)), shp(KK, II, npl)).copy()
+        t["eff_sp"] = np.ctypeslib.as_array(ct.cast(d.eff_sp, ct.POINTER(ct.c_int32)), (max(ne, 1),))[:ne].copy()
+        t["eff_val"] = np.ctypeslib.as_array(ct.cast(d.eff_val, ct.POINTER(ct.c_double)), (max(ne, 1),))[:ne].copy()
+        t["plog_par"] = np.ctypeslib.as_array(ct.cast(d.plog_par, ct.POINTER(ct.c_double)),
+                                              (max(npl, 1), 4)).copy()
+        sp = ct.create_string_buffer(16 * KK + 1)
+        el = ct.create_string_buffer(16 * MM + 1)
+        awt = np.zeros(MM)
+        ncf = np.zeros((MM, KK), np.int32)
+        L.ckmi_parsed_symbols(h, ct.addressof(sp), ct.addressof(el), awt.ctypes.data, ncf.ctypes.data)
+        species = [sp.raw[16 * k:16 * k + 16].rstrip(b"\0").decode() for k in range(KK)]
+        elements = [el.raw[16 * m:16 * m + 16].rstrip(b"\0").decode() for m in range(MM)]
+        eqs = []
+        buf = ct.create_string_buffer(4096)
+        n = ct.c_int32()
+        for i in range(II):
+            L.ckmi_parsed_equation(h, i, buf, 4096, ct.byref(n))
+            eqs.append(buf.value.decode())
+        return t, species, elements, awt, ncf, eqs
+    finally:
+        L.ckmi_parsed_free(h)
 
 
 def _ptr(t) -> Optional[int]:
@@ -274,8 +343,9 @@ class DeviceMechanism:
         T = self._dev(T).reshape(-1)
         n = T.numel()
         cp, h, s = (torch.empty((self.KK, n), dtype=torch.float64, device=self.device) for _ in range(3))
-        _check(lib().ckmi_species_thermo(self._h, n, _ptr(T), _ptr(cp), _ptr(h), _ptr(s), _stream_ptr(self.device)),
-               "ckmi_species_thermo")
+        with torch.cuda.device(self.device):
+            _check(lib().ckmi_species_thermo(self._h, n, _ptr(T), _ptr(cp), _ptr(h), _ptr(s),
+                                             _stream_ptr(self.device)), "ckmi_species_thermo")
         return cp, h, s
 
     def rop_thermo(self, T, P, Y_soa, wdot=None, cp=None, h=None):
@@ -292,8 +362,9 @@ class DeviceMechanism:
             cp = torch.empty(n, dtype=torch.float64, device=self.device)
         if h is None:
             h = torch.empty(n, dtype=torch.float64, device=self.device)
-        _check(lib().ckmi_rop_thermo(self._h, n, _ptr(T), _ptr(P), _ptr(Y), _ptr(wdot), _ptr(cp), _ptr(h),
-                                     _stream_ptr(self.device)), "ckmi_rop_thermo")
+        with torch.cuda.device(self.device):  # the specialised kernel's module lives on this device
+            _check(lib().ckmi_rop_thermo(self._h, n, _ptr(T), _ptr(P), _ptr(Y), _ptr(wdot), _ptr(cp), _ptr(h),
+                                         _stream_ptr(self.device)), "ckmi_rop_thermo")
         return wdot, cp, h
 
     def reaction_rates(self, T, P, Y_soa):
@@ -303,8 +374,9 @@ class DeviceMechanism:
         n = T.numel()
         qf = torch.empty((self.II, n), dtype=torch.float64, device=self.device)
         qr = torch.empty((self.II, n), dtype=torch.float64, device=self.device)
-        _check(lib().ckmi_reaction_rates(self._h, n, _ptr(T), _ptr(P), _ptr(Y), _ptr(qf), _ptr(qr),
-                                         _stream_ptr(self.device)), "ckmi_reaction_rates")
+        with torch.cuda.device(self.device):
+            _check(lib().ckmi_reaction_rates(self._h, n, _ptr(T), _ptr(P), _ptr(Y), _ptr(qf), _ptr(qr),
+                                             _stream_ptr(self.device)), "ckmi_reaction_rates")
         return qf, qr
 
     def reactor_run(self, cfg: ReactorCfg, problem, T0, P0, V0, Y0, t_save=None, out=None, afac_rxn=None, afac=None,

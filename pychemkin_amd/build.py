@@ -12,6 +12,7 @@ LU_SRC = os.path.join(HERE, "csrc", "ckmi_lu.hip")  # batched MFMA LU (large mec
 BIG_SRC = os.path.join(HERE, "csrc", "ckmi_big.hip")  # workgroup-per-reactor integrator (64 <= KK + 1 <= 192)
 KIN_SRC = os.path.join(HERE, "csrc", "ckmi_kin.cpp")  # KIN-compatible host shims (include/ckmi_kin.h)
 JIT_SRC = os.path.join(HERE, "csrc", "ckmi_jit.cpp")  # mechanism-specialised ROP kernel generator (hipRTC)
+PARSE_SRC = os.path.join(HERE, "csrc", "ckmi_parse.cpp")  # native Chemkin-II interpreter (KINPreProcess)
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp", "ckmi_image.hpp",
                                                 "ckmi_run.hpp", "ckmi_internal.hpp")] + [
     os.path.join(HERE, "..", "include", "ckmi.h"), os.path.join(HERE, "..", "include", "ckmi_kin.h")]
@@ -47,7 +48,7 @@ def _stale(target: str, sources) -> bool:
 
 
 def needs_build() -> bool:
-    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC, JIT_SRC] + DEPS)
+    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC, JIT_SRC, PARSE_SRC] + DEPS)
 
 
 PROF_OUT = os.path.join(HERE, "_lib", "libckmi_prof.so")  # diagnostic phase-timer build
@@ -63,9 +64,9 @@ def _compile(src: str, obj: str, flags, verbose: bool) -> None:
 def build(force: bool = False, verbose: bool = False, prof: bool = False, out: str = None, extra=()) -> str:
     """Build libckmi.so (or the phase-timer build, or an A/B variant at `out` with `extra` flags).
 
-    Four translation units, compiled separately (the reactor kernel alone takes ~2 min) and linked
-    into one shared library: ckmi.hip, ckmi_lu.hip, ckmi_big.hip and the host-only ckmi_kin.cpp and
-    ckmi_jit.cpp (linked with libhiprtc)."""
+    Separately compiled translation units (the reactor kernel alone takes ~2 min) linked into one
+    shared library: ckmi.hip, ckmi_lu.hip, ckmi_big.hip and the host-only ckmi_kin.cpp,
+    ckmi_parse.cpp and ckmi_jit.cpp (linked with libhiprtc)."""
     default = out is None and not prof and not extra
     out = out or (PROF_OUT if prof else OUT)
     if not force and default and not needs_build():
@@ -84,6 +85,9 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     jit_obj = os.path.join(OBJ_DIR, "ckmi_jit.o")
     if force or _stale(jit_obj, [JIT_SRC] + DEPS):
         jobs.append((JIT_SRC, jit_obj, KIN_FLAGS))
+    parse_obj = os.path.join(OBJ_DIR, "ckmi_parse.o")
+    if force or _stale(parse_obj, [PARSE_SRC] + DEPS):
+        jobs.append((PARSE_SRC, parse_obj, KIN_FLAGS))
     tag = "main" if default else os.path.splitext(os.path.basename(out))[0]
     main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
     if force or (not default and not prof) or _stale(main_obj, [SRC] + DEPS):
@@ -92,6 +96,7 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
         for f in [pool.submit(_compile, s, o, fl, verbose) for s, o, fl in jobs]:
             f.result()
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj, kin_obj, jit_obj,
+           parse_obj,
            "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

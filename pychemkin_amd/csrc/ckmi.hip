@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -20,8 +21,10 @@ using namespace ckmi;
 namespace {
 
 thread_local std::string g_err;
-int g_reactor_path = 0;  // ckmi_set_reactor_path
-int g_rop_path = 0;      // ckmi_set_rop_path
+// Kernel-path overrides (ckmi_set_reactor_path / ckmi_set_rop_path): process-wide test and A/B
+// knobs, not per thread or per stream; each launch reads its selector once.
+std::atomic<int> g_reactor_path{0};
+std::atomic<int> g_rop_path{0};
 constexpr int JIT_MIN_STATES = 16384;  // automatic choice: the specialised kernel from this batch size up
 
 int fail(int code, const std::string& msg) {
@@ -1289,29 +1292,46 @@ int launch_rop(const ckmi_mech* m, int n, const double* T, const double* P, cons
   }
 }
 
-// compile and load the specialised ROP kernel of m once (thread-safe); CKMI_OK when it can run
+// Makes m's device current for the scope and restores the caller's device afterwards: the
+// specialised kernel's module belongs to the device it was loaded on.
+struct DeviceScope {
+  int prev = -1;
+  explicit DeviceScope(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceScope() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+// compile and load the specialised ROP kernel of m once (thread-safe), on m's device; CKMI_OK when
+// it can run
 int jit_ready(ckmi_mech* m) {
   if (!m->jit) return fail(CKMI_ERR_UNSUPPORTED, "no specialised ROP kernel");
   JitRop& J = *m->jit;
+  if (J.state.load() == 1) return CKMI_OK;
   std::lock_guard<std::mutex> lk(J.mu);
-  if (J.state == 1) return CKMI_OK;
-  if (J.state == -1) return fail(CKMI_ERR_UNSUPPORTED, "specialised ROP kernel unavailable: " + J.why);
+  if (J.state.load() == 1) return CKMI_OK;
+  if (J.state.load() == -1) return fail(CKMI_ERR_UNSUPPORTED, "specialised ROP kernel unavailable: " + J.why);
   std::vector<char> code;
   std::string log;
   const int rc = jit_rop_compile(J.src, code, log);
   if (rc) {
-    J.state = -1;
     J.why = "hipRTC compilation failed: " + log.substr(0, 2000);
+    J.state.store(-1);
     return fail(CKMI_ERR_HIP, J.why);
   }
+  DeviceScope on(m->device);
   if (hipModuleLoadData(&J.mod, code.data()) != hipSuccess ||
       hipModuleGetFunction(&J.fn, J.mod, ("ckjit_rop_k" + std::to_string(m->KK) + "_i" + std::to_string(m->II)).c_str()) !=
           hipSuccess) {
-    J.state = -1;
     J.why = "hipModuleLoadData / hipModuleGetFunction failed";
+    J.state.store(-1);
     return fail(CKMI_ERR_HIP, J.why);
   }
-  J.state = 1;
+  J.state.store(1);
   return CKMI_OK;
 }
 
@@ -1337,6 +1357,9 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   const int KK = d->KK, II = d->II;
   if (KK <= 0 || II < 0) return fail(CKMI_ERR_SIZE, "bad sizes");
   if (KK > KK_IMAGE_MAX) return fail(CKMI_ERR_UNSUPPORTED, "more than 255 species not supported by this build");
+  // slot counts and species indices first: everything below (rxn_general, the slot classes, the
+  // image) reads [4 i + u] for u < nr[i] / np[i]
+  if (const char* bad = ckmi::check_slots(d)) return fail(CKMI_ERR_ARG, bad);
   auto* m = new ckmi_mech();
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) {
@@ -1632,10 +1655,11 @@ int ckmi_rop_thermo(const ckmi_mech* m, int32_t n, const double* T, const double
                     double* cp, double* h, void* stream) {
   if (!m || n < 0 || !wdot) return fail(CKMI_ERR_ARG, "bad argument");
   if (n == 0) return CKMI_OK;
-  const int path = g_rop_path;
+  const int path = g_rop_path.load();
   if (path == 2 || (path == 0 && n >= JIT_MIN_STATES)) {
     const int rc = jit_ready(const_cast<ckmi_mech*>(m));
     if (rc == CKMI_OK) {
+      DeviceScope on(m->device);
       void* args[] = {&n, (void*)&T, (void*)&P, (void*)&Y, &wdot, &cp, &h, &m->jit->prm};
       HIP_CHECK(hipModuleLaunchKernel(m->jit->fn, (unsigned)((n + 63) / 64), 1, 1, 64, 1, 1, 0, (hipStream_t)stream,
                                       args, nullptr));
@@ -1681,8 +1705,11 @@ int ckmi_rop_jit_compile(const ckmi_mech_desc* d, int64_t* code_bytes) {
 
 int ckmi_rop_jit_state(const ckmi_mech* m, int32_t* state) {
   if (!m || !state) return fail(CKMI_ERR_ARG, "null argument");
-  *state = m->jit ? m->jit->state : -1;
-  if (m->jit && m->jit->state == -1) g_err = m->jit->why;
+  *state = m->jit ? m->jit->state.load() : -1;
+  if (*state == -1 && m->jit) {
+    std::lock_guard<std::mutex> lk(m->jit->mu);
+    g_err = m->jit->why;
+  }
   return CKMI_OK;
 }
 
@@ -1752,9 +1779,10 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   // and [3] without a failure, and fails one of 55 reactors at rtol = 1e-10, atol = 1e-20), and for
   // mechanisms with FORD / RORD / fractional orders, whose d C^o / dC = o C^(o-1) grows without
   // bound as C -> 0 (the FP32-stored inverse of such a Newton matrix stalled one reactor of five)
-  const bool f64 = g_reactor_path == 2 || (g_reactor_path != 3 && (cfg->rtol < 1e-9 || m->has_general));
+  const int rpath = g_reactor_path.load();
+  const bool f64 = rpath == 2 || (rpath != 3 && (cfg->rtol < 1e-9 || m->has_general));
   const hipStream_t st = (hipStream_t)stream;
-  if (nvar > 64 || g_reactor_path == 1) rc = launch_big_reactors(m, n, dc, io, st);
+  if (nvar > 64 || rpath == 1) rc = launch_big_reactors(m, n, dc, io, st);
   else if (m->has_plog) rc = f64 ? launch_reactors<64, true, true>(m, n, dc, io, st) : launch_reactors<64, true>(m, n, dc, io, st);
   else if (nvar <= 32 && !f64) rc = launch_reactors<32>(m, n, dc, io, st);
   else if (nvar <= 54) rc = f64 ? launch_reactors<54, false, true>(m, n, dc, io, st) : launch_reactors<54>(m, n, dc, io, st);

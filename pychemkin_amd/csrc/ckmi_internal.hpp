@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -17,7 +18,7 @@ struct JitRop {
   std::string src, why;
   std::vector<int> lnA_off;  // original reaction -> offset of its ln A in the parameter block
   double* prm = nullptr;     // device parameter block
-  int state = 0;             // 0 not compiled yet, 1 ready, -1 unsupported / compile failed (why)
+  std::atomic<int> state{0};  // 0 not compiled yet, 1 ready, -1 unsupported / compile failed (why, under mu)
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr;
   std::mutex mu;
@@ -25,6 +26,20 @@ struct JitRop {
 // A reaction the unit-coefficient slots cannot express: a non-integral (or < 1) stoichiometric
 // coefficient, a FORD / RORD order that differs from the coefficient, or more than 4 molecules
 // on a side.  Evaluated by the extended kernel variants (ckmi_image.hpp eval_gen_img).
+// Slot counts within 0..CKMI_SLOTS and species indices within 0..KK-1 for every reaction, checked
+// before any table walk (a descriptor from the C ABI is untrusted); nullptr when valid.
+inline const char* check_slots(const ckmi_mech_desc* d) {
+  if (!d->nr || !d->np || !d->rsp || !d->psp || !d->rnu || !d->pnu) return "null reaction tables";
+  for (int i = 0; i < d->II; ++i) {
+    if (d->nr[i] < 0 || d->nr[i] > CKMI_SLOTS || d->np[i] < 0 || d->np[i] > CKMI_SLOTS)
+      return "more than 4 species on one side of a reaction (nr / np outside 0..4)";
+    for (int u = 0; u < d->nr[i]; ++u)
+      if (d->rsp[CKMI_SLOTS * i + u] < 0 || d->rsp[CKMI_SLOTS * i + u] >= d->KK) return "reactant species index out of range";
+    for (int u = 0; u < d->np[i]; ++u)
+      if (d->psp[CKMI_SLOTS * i + u] < 0 || d->psp[CKMI_SLOTS * i + u] >= d->KK) return "product species index out of range";
+  }
+  return nullptr;
+}
 inline bool rxn_general(const ckmi_mech_desc* d, int i) {
   int mr = 0, mp = 0;
   for (int u = 0; u < d->nr[i]; ++u) {

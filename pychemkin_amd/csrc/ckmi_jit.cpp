@@ -102,6 +102,10 @@ __device__ __forceinline__ double jrcp(double x) {
 bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<double>& prm, std::vector<int>& lnA_off,
                       std::string& why) {
   const int KK = d->KK, II = d->II;
+  if (const char* bad = ckmi::check_slots(d)) {
+    why = bad;
+    return false;
+  }
   std::vector<int> aonly_off;
   // tuning knobs (defaults measured on MI355X, scripts/rop_jit_ab.py, profiles/r02h_jit_ab*.log):
   // reactions per basic block (8), and eg = 0: g_k in registers and one exp per reversible reaction,

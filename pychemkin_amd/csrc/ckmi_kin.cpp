@@ -43,6 +43,7 @@ struct ChemSet {
   std::vector<double> wt, awt, thermo;  // thermo [KK][17] for the per-mass conversions
   std::vector<int32_t> ncf;             // [MM][KK] row-major
   std::vector<std::string> names, elements;
+  std::vector<std::string> equations;   // reaction strings (KINPreProcess sets; KINGetGasReactionString)
   double* dbuf = nullptr;               // device scratch for single-state calls
   size_t dbuf_n = 0;
 };
@@ -392,15 +393,8 @@ int run_reactor(ChemSet* s) {
   return CKMI_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-const char* ckmi_kin_last_error(void) { return g_err.c_str(); }
-
-int ckmi_kin_register(const ckmi_mech_desc* desc, int32_t MM, const char* names, const char* elements,
-                      const double* awt, const int32_t* ncf, int32_t* chemset) {
-  std::lock_guard<std::recursive_mutex> lk(g_mu);
+int register_set(const ckmi_mech_desc* desc, int32_t MM, const char* names, const char* elements,
+                 const double* awt, const int32_t* ncf, int32_t* chemset, ChemSet** out) {
   if (!desc || !chemset || MM < 0) return fail(CKMI_ERR_ARG, "null argument");
   auto* s = new ChemSet();
   int rc = ckmi_mech_create(desc, &s->mech);
@@ -418,13 +412,27 @@ int ckmi_kin_register(const ckmi_mech_desc* desc, int32_t MM, const char* names,
     s->awt.assign(awt, awt + MM);
     s->ncf.assign(ncf, ncf + (size_t)MM * desc->KK);
   }
-  for (int k = 0; names && k < s->KK; ++k) s->names.emplace_back(trim(std::string(names + NAME_LEN * k, strnlen(names + NAME_LEN * k, NAME_LEN))));
+  for (int k = 0; names && k < s->KK; ++k)
+    s->names.emplace_back(trim(std::string(names + NAME_LEN * k, strnlen(names + NAME_LEN * k, NAME_LEN))));
   for (int m = 0; elements && m < MM; ++m)
     s->elements.emplace_back(trim(std::string(elements + NAME_LEN * m, strnlen(elements + NAME_LEN * m, NAME_LEN))));
   g_sets.push_back(s);
   *chemset = (int32_t)g_sets.size();
   g_active = *chemset;
+  if (out) *out = s;
   return CKMI_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ckmi_kin_last_error(void) { return g_err.c_str(); }
+
+int ckmi_kin_register(const ckmi_mech_desc* desc, int32_t MM, const char* names, const char* elements,
+                      const double* awt, const int32_t* ncf, int32_t* chemset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return register_set(desc, MM, names, elements, awt, ncf, chemset, nullptr);
 }
 
 int ckmi_kin_release(int32_t chemset) {
@@ -752,5 +760,355 @@ int KINAll0D_GetGasSolnResponse(int* nreac, int* npts, int* KK, double* t, doubl
   }
   return CKMI_OK;
 }
+
+
+// ---------------------------------------------------------------- mechanism preprocessing
+// KINPreProcess (chemkin_wrapper.py:303-316, chemistry.py:675-687): parse chem.inp + therm.dat with
+// the native interpreter (ckmi_parse.cpp), build the device tables and return the chemistry-set
+// index.  Surface chemistry is out of scope (isurf must be 0).  With itran = 1 the transport file
+// must exist and is kept for reference (transport properties are not computed on this path).  The
+// summary file, when named, receives the element / species / reaction listing; the link files of
+// the closed library are not written (the tables stay in this process).
+int KINPreProcess(int* isurf, int* itran, char* chem, char* surf, char* therm, char* tran, char* gaslink,
+                  char* surflink, char* tranlink, char* summary, int* chemset) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)surf, (void)gaslink, (void)surflink, (void)tranlink;
+  if (!chem || !chemset) return fail(CKMI_ERR_ARG, "KINPreProcess: null mechanism file or chemistry-set pointer");
+  if (isurf && *isurf != 0) return fail(CKMI_ERR_UNSUPPORTED, "surface chemistry is not supported on this path");
+  if (itran && *itran != 0) {
+    if (!tran || !*tran) return fail(CKMI_ERR_ARG, "KINPreProcess: transport requested without a transport file");
+    FILE* f = std::fopen(tran, "r");
+    if (!f) return fail(CKMI_ERR_ARG, std::string("cannot read transport file ") + tran);
+    std::fclose(f);
+  }
+  ckmi_parsed* p = nullptr;
+  int rc = ckmi_parse_files(chem, therm, &p);
+  if (rc) return fail(rc, std::string("KINPreProcess: ") + ckmi_parse_last_error());
+  int32_t MM = 0, KK = 0, II = 0;
+  ckmi_parsed_sizes(p, &MM, &KK, &II);
+  ckmi_mech_desc d;
+  ckmi_parsed_desc(p, &d);
+  std::vector<char> names((size_t)KK * NAME_LEN + 1), elems((size_t)MM * NAME_LEN + 1);
+  std::vector<double> awt(MM);
+  std::vector<int32_t> ncf((size_t)MM * KK);
+  ckmi_parsed_symbols(p, names.data(), elems.data(), awt.data(), ncf.data());
+  ChemSet* s = nullptr;
+  int32_t cs = 0;
+  rc = register_set(&d, MM, names.data(), elems.data(), awt.data(), ncf.data(), &cs, &s);
+  if (!rc) {
+    for (int i = 0; i < II; ++i) {
+      int32_t len = 0;
+      ckmi_parsed_equation(p, i, nullptr, 0, &len);
+      std::vector<char> b((size_t)len + 1);
+      ckmi_parsed_equation(p, i, b.data(), len + 1, nullptr);
+      s->equations.emplace_back(b.data());
+    }
+  }
+  ckmi_parsed_free(p);
+  if (rc) return rc;
+  *chemset = cs;
+  if (summary && *summary) {
+    FILE* f = std::fopen(summary, "w");
+    if (f) {
+      std::fprintf(f, "ckmi mechanism summary: %s\n  thermo: %s\n  elements %d, species %d, reactions %d\n\n", chem,
+                   therm ? therm : "(inline)", MM, KK, II);
+      for (int m = 0; m < MM; ++m) std::fprintf(f, "  element %3d %-16s %12.5f\n", m + 1, s->elements[m].c_str(), s->awt[m]);
+      for (int k = 0; k < KK; ++k) std::fprintf(f, "  species %3d %-16s %12.5f\n", k + 1, s->names[k].c_str(), s->wt[k]);
+      for (int i = 0; i < II; ++i) std::fprintf(f, "  reaction %4d %s\n", i + 1, s->equations[i].c_str());
+      std::fclose(f);
+    }
+  }
+  return CKMI_OK;
+}
+
+// KINGetGasReactionString (chemkin_wrapper.py:365-371, chemistry.py:1759-1781): 1-based reaction index
+int KINGetGasReactionString(int* chemset, int* irxn, int* len, char* buf) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !irxn || !len || !buf) return fail(CKMI_ERR_ARG, "bad argument");
+  if (*irxn < 1 || *irxn > s->II) return fail(CKMI_ERR_ARG, "reaction index out of range");
+  if ((int)s->equations.size() != s->II)
+    return fail(CKMI_ERR_UNSUPPORTED, "reaction strings are only kept for chemistry sets made by KINPreProcess");
+  const std::string& e = s->equations[*irxn - 1];
+  std::memcpy(buf, e.data(), e.size());  // the caller's buffer is 1024 bytes (chemistry.py:1761)
+  *len = (int)e.size();
+  return CKMI_OK;
+}
+
+// KINGetReactionStringLength (:372-373): the longest reaction string of the active chemistry set
+int KINGetReactionStringLength(int* len) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(&g_active);
+  if (!len || !s) return fail(CKMI_ERR_ARG, "no active chemistry set");
+  size_t n = 0;
+  for (const auto& e : s->equations) n = std::max(n, e.size());
+  *len = (int)n;
+  return CKMI_OK;
+}
+
+// ---------------------------------------------------------------- real-gas EOS: ideal gas only
+// (chemkin_wrapper.py:545-581; chemistry.py:755-792 and realgaseos.py:30-52 read mode 0 as "ideal")
+int KINRealGas_GetEOSMode(int* chemset, int* mode, char* name) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!get_set(chemset) || !mode) return fail(CKMI_ERR_ARG, "bad argument");
+  *mode = 0;
+  if (name) std::memcpy(name, "IDEAL", 6);  // the caller's buffer is MAX_SPECIES_LENGTH (17) bytes
+  return CKMI_OK;
+}
+int KINRealGas_CheckRealGasStatus(int* chemset, int* mode) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!get_set(chemset) || !mode) return fail(CKMI_ERR_ARG, "bad argument");
+  *mode = 0;
+  return CKMI_OK;
+}
+int KINRealGas_UseIdealGasLaw(int* chemset, int* flag) {
+  (void)flag;
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return get_set(chemset) ? CKMI_OK : fail(CKMI_ERR_ARG, "unknown chemistry set");
+}
+int KINRealGas_SetCurrentPressure(int* chemset, double* P) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!get_set(chemset) || !P || !(*P > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  return CKMI_OK;  // the ideal-gas EOS does not depend on it
+}
+int KINRealGas_UseCubicEOS(int* chemset, int* mode) {
+  (void)chemset, (void)mode;
+  return fail(CKMI_ERR_UNSUPPORTED, "real-gas cubic EOS is not supported on this path (ideal gas only)");
+}
+int KINRealGas_SetMixingRule(int* chemset, int* rule, int* flag) {
+  (void)chemset, (void)rule, (void)flag;
+  return fail(CKMI_ERR_UNSUPPORTED, "real-gas mixing rules are not supported on this path (ideal gas only)");
+}
+int KINRealGas_SetParameter(char* key, double* value) {
+  (void)key, (void)value;
+  return fail(CKMI_ERR_UNSUPPORTED, "real-gas parameters are not supported on this path (ideal gas only)");
+}
+
+// ---------------------------------------------------------------- small host utilities
+// KINGetGamma (:582-588): cp / cv of the mixture (ideal gas: cv = cp - R / W)
+int KINGetGamma(int* chemset, double* T, double* Y, double* gamma) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !Y || !gamma || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  double cp = 0.0;
+  int rc = rop_state(s, *T, 1.01325e6, Y, nullptr, &cp, nullptr);
+  if (rc) return rc;
+  double sw = 0.0;
+  for (int k = 0; k < s->KK; ++k) sw += Y[k] / s->wt[k];
+  *gamma = cp / (cp - RU * sw);
+  return CKMI_OK;
+}
+// KINGetMassFractionFromMoleFraction / KINGetMoleFractionFromMassFraction (:855-867)
+int KINGetMassFractionFromMoleFraction(int* chemset, double* X, double* Y) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !X || !Y) return fail(CKMI_ERR_ARG, "bad argument");
+  double sum = 0.0;
+  for (int k = 0; k < s->KK; ++k) sum += X[k] * s->wt[k];
+  if (!(sum > 0.0)) return fail(CKMI_ERR_ARG, "composition sums to zero");
+  for (int k = 0; k < s->KK; ++k) Y[k] = X[k] * s->wt[k] / sum;
+  return CKMI_OK;
+}
+int KINGetMoleFractionFromMassFraction(int* chemset, double* Y, double* X) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !X || !Y) return fail(CKMI_ERR_ARG, "bad argument");
+  double sum = 0.0;
+  for (int k = 0; k < s->KK; ++k) sum += Y[k] / s->wt[k];
+  if (!(sum > 0.0)) return fail(CKMI_ERR_ARG, "composition sums to zero");
+  for (int k = 0; k < s->KK; ++k) X[k] = Y[k] / s->wt[k] / sum;
+  return CKMI_OK;
+}
+
+// ---------------------------------------------------------------- 0-D reactor: API-mode setters
+// Declared by the reference (:702-743) but reached only as keyword text there; each maps onto the
+// keyword it stands for, so both spellings end in the same ckmi_reactor_cfg field.
+static int add_kw(const char* key, double v) {
+  if (!g_r.inputs) return fail(CKMI_ERR_ARG, "KINAll0D_SetupBatchInputs first");
+  char b[64];
+  std::snprintf(b, sizeof(b), "%.17g", v);
+  g_r.kw.push_back({key, b});
+  return CKMI_OK;
+}
+int KINAll0D_SetHeatTransfer(double* htc, double* tamb) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!htc || !tamb) return fail(CKMI_ERR_ARG, "bad argument");
+  int rc = add_kw("HTC", *htc);
+  return rc ? rc : add_kw("TAMB", *tamb);
+}
+int KINAll0D_SetHeatTransferArea(double* area) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return area ? add_kw("AREAQ", *area) : fail(CKMI_ERR_ARG, "bad argument");
+}
+int KINAll0D_SetSolverInitialStepTime(double* h0) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return h0 ? add_kw("HO", *h0) : fail(CKMI_ERR_ARG, "bad argument");
+}
+int KINAll0D_SetSolverMaximumStepTime(double* hmax) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return hmax ? add_kw("STPT", *hmax) : fail(CKMI_ERR_ARG, "bad argument");
+}
+int KINAll0D_SetSolverMaximumIteration(int* n) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  return n ? add_kw("MAXIT", (double)*n) : fail(CKMI_ERR_ARG, "bad argument");
+}
+int KINAll0D_SetRelaxIteration(void) {
+  return fail(CKMI_ERR_UNSUPPORTED, "relaxation iterations (steady-state solvers) are not on this path");
+}
+int KINAll0D_SetMinimumSpeciesBound(double* v) {
+  (void)v;
+  return fail(CKMI_ERR_UNSUPPORTED, "a species lower bound other than NNEG is not supported on this path");
+}
+int KINAll0D_SetProfileKeyword(int* a, int* b, char* key, int* n, double* x, double* y) {
+  (void)a, (void)b;
+  return KINAll0D_SetProfileParameter(key, n, x, y);
+}
+
+// KINAll0D_GetSolution (:739-744, PSR.py:818): the final state (T, P, mass fractions)
+int KINAll0D_GetSolution(double* T, double* P, double* Y) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_r.done || g_r.t.empty()) return fail(CKMI_ERR_ARG, "no completed run");
+  ChemSet* s = get_set(&g_r.chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  const size_t last = g_r.t.size() - 1;
+  if (T) *T = g_r.T[last];
+  if (P) *P = g_r.P[last];
+  if (Y) std::copy(g_r.Y.begin() + last * s->KK, g_r.Y.begin() + (last + 1) * s->KK, Y);
+  return CKMI_OK;
+}
+
+// KINAll0D_CalculateInput (:690-697; batchreactor.py:944-978): the full-keyword mode.  The keyword
+// block is one string cut by linelen[]; the lines are those of __process_keywords_withFullInputs
+// (batchreactor.py:822-925): TRAN, CONP|CONV, ENRG|TGIV, PRES [atm], TEMP, TIME, REAC sp x (mole
+// fractions), VOL, profile points "VPRO t v" (PPRO in atm), QRGEQ, END, and the solver / output /
+// ignition keywords of API mode.  They override what KINAll0D_Setup / SetupBatchInputs gave.
+int KINAll0D_CalculateInput(int* lout, int* chemset, char* lines, int* nlines, int32_t* linelen) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)lout;
+  ChemSet* s = get_set(chemset);
+  if (!s || !lines || !nlines || *nlines < 0 || (*nlines > 0 && !linelen)) return fail(CKMI_ERR_ARG, "bad argument");
+  if (!g_r.setup || g_r.chemset != *chemset) return fail(CKMI_ERR_ARG, "KINAll0D_Setup first");
+  if (!g_r.inputs) {  // everything may come from the keyword block
+    g_r.Y0.assign(s->KK, 0.0);
+    g_r.kw.clear();
+    g_r.prof.clear();
+    g_r.inputs = true;
+  }
+  std::vector<double> X(s->KK, 0.0);
+  bool have_x = false;
+  size_t off = 0;
+  for (int i = 0; i < *nlines; ++i) {
+    if (linelen[i] < 0) return fail(CKMI_ERR_ARG, "negative keyword line length");
+    const std::string line = trim(std::string(lines + off, (size_t)linelen[i]));
+    off += (size_t)linelen[i];
+    if (line.empty() || line[0] == '!') continue;
+    std::istringstream is(line);
+    std::string key;
+    is >> key;
+    key = upper(key);
+    std::vector<std::string> v;
+    for (std::string t; is >> t;) v.push_back(t);
+    bool ok = true;
+    auto val = [&](size_t j) {
+      bool o = false;
+      const double x = j < v.size() ? value_of(v[j], &o) : 0.0;
+      ok = ok && o;
+      return x;
+    };
+    if (key == "END") break;
+    if (key == "TRAN" || key == "QRGEQ") continue;
+    if (key == "STST") return fail(CKMI_ERR_UNSUPPORTED, "steady-state solver (STST) is not on this path");
+    if (key == "CONP" || key == "CONV") g_r.problem = key == "CONP" ? 1 : 2;
+    else if (key == "ENRG" || key == "TGIV") g_r.energy = key == "ENRG" ? 1 : 2;
+    else if (key == "PRES") g_r.P0 = val(0) * 1.01325e6;
+    else if (key == "TEMP") g_r.T0 = val(0);
+    else if (key == "TIME") g_r.t_end = val(0);
+    else if (key == "VOL") g_r.V0 = val(0);
+    else if (key == "QLOS") g_r.qloss = val(0);
+    else if (key == "REAC") {
+      const int k = v.empty() ? -1 : species_index(s, v[0]);
+      if (k < 0) return fail(CKMI_ERR_ARG, "REAC: unknown species in '" + line + "'");
+      X[k] = val(1);
+      have_x = true;
+    } else if (key == "VPRO" || key == "PPRO" || key == "TPRO" || key == "QPRO" || key == "AEXT") {
+      const double t = val(0), y = val(1) * (key == "PPRO" ? 1.01325e6 : 1.0);
+      if (!ok) return fail(CKMI_ERR_ARG, "bad profile line '" + line + "'");
+      Profile* p = nullptr;
+      for (auto& q : g_r.prof)
+        if (q.key == key) p = &q;
+      if (!p) {
+        g_r.prof.push_back(Profile{key, {}, {}});
+        p = &g_r.prof.back();
+      }
+      p->x.push_back(t);
+      p->y.push_back(y);
+    } else {
+      std::string rest;
+      for (size_t j = 0; j < v.size(); ++j) rest += (j ? " " : "") + v[j];
+      g_r.kw.push_back({key, rest});
+    }
+    if (!ok) return fail(CKMI_ERR_ARG, "bad value in keyword line '" + line + "'");
+  }
+  if (have_x) {  // REAC mole fractions, normalised, -> mass fractions
+    double sx = 0.0, sxw = 0.0;
+    for (int k = 0; k < s->KK; ++k) sx += X[k];
+    for (int k = 0; k < s->KK; ++k) sxw += X[k] / sx * s->wt[k];
+    for (int k = 0; k < s->KK; ++k) g_r.Y0[k] = X[k] / sx * s->wt[k] / sxw;
+  }
+  if (!(g_r.t_end > 0.0) || !(g_r.T0 > 0.0) || !(g_r.P0 > 0.0))
+    return fail(CKMI_ERR_ARG, "TIME, TEMP and PRES must be given and > 0");
+  double sy = 0.0;
+  for (double y : g_r.Y0) sy += y;
+  if (!(sy > 0.0)) return fail(CKMI_ERR_ARG, "no initial composition (REAC)");
+  g_r.done = false;
+  return run_reactor(s);
+}
+
+// ---------------------------------------------------------------- declared, out of scope
+// The reference declares these at import (chemkin_wrapper.py:300-867), so a drop-in library must
+// export them; they belong to models outside the batch-reactor path (transport, equilibrium, PSR,
+// PFR, engines, flames) and return CKMI_ERR_UNSUPPORTED with a message.
+#define CKMI_OUT_OF_SCOPE(name, what, ...) \
+  int name(__VA_ARGS__) { return fail(CKMI_ERR_UNSUPPORTED, #name ": " what " is not on this path"); }
+CKMI_OUT_OF_SCOPE(KINGetViscosity, "transport", int*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetConductivity, "transport", int*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetDiffusionCoeffs, "transport", int*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetMixtureViscosity, "transport", int*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetMixtureConductivity, "transport", int*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetMixtureDiffusionCoeffs, "transport", int*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetOrdinaryDiffusionCoeffs, "transport", int*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINGetThermalDiffusionCoeffs, "transport", int*, double*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINCalculateEquil, "the equilibrium solver", int*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINCalculateEquilWithOption, "the equilibrium solver", int*, int*, double*, double*, double*,
+                  double*)
+CKMI_OUT_OF_SCOPE(KINCalculateEqGasWithOption, "the equilibrium solver", int*, int*, int*, double*, double*,
+                  double*, double*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_SetupPSRReactorInputs, "the PSR model", int*, int*, double*, double*, double*, double*,
+                  double*, double*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_SetupPSRInletInputs, "the PSR model", int*, int*, int*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_SetupPFRInputs, "the PFR model", int*, double*, double*, double*, double*, double*,
+                  double*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_SetupHCCIInputs, "the HCCI engine model", int*, double*, double*, double*, double*,
+                  double*, double*, double*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_SetupHCCIZoneInputs, "the HCCI engine model", int*, int*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_SetupSIInputs, "the SI engine model", int*, double*, double*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_GetHeatRelease, "QRGEQ heat-release output", double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_GetEngineHeatRelease, "engine heat release", double*, double*, double*, double*,
+                  double*, double*)
+CKMI_OUT_OF_SCOPE(KINAll0D_GetExitMassFlowRate, "open-reactor output", double*)
+CKMI_OUT_OF_SCOPE(KINPremix_SetParameter, "the premixed flame model", char*, double*)
+CKMI_OUT_OF_SCOPE(KINPremix_CalculateFlame, "the premixed flame model", int*, int*, double*, double*, double*,
+                  double*, double*)
+CKMI_OUT_OF_SCOPE(KINPremix_GetSolution, "the premixed flame model", int*, int*, double*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINPremix_GetSolutionGridPoints, "the premixed flame model", int*)
+CKMI_OUT_OF_SCOPE(KINPremix_GetFlameMassFlux, "the premixed flame model", double*)
+CKMI_OUT_OF_SCOPE(KINOppdif_SetInlet, "the opposed-flow flame model", char*, int*, double*, double*, double*, int*)
+CKMI_OUT_OF_SCOPE(KINOppdif_SetParameter, "the opposed-flow flame model", char*, double*)
+CKMI_OUT_OF_SCOPE(KINOppdif_CalculateFlame, "the opposed-flow flame model", int*, int*, double*, double*)
+CKMI_OUT_OF_SCOPE(KINOppdif_GetSolutionGridPoints, "the opposed-flow flame model", int*)
+CKMI_OUT_OF_SCOPE(KINOppdif_GetSolution, "the opposed-flow flame model", int*, int*, double*, double*, double**)
+CKMI_OUT_OF_SCOPE(KINOppdif_GetSolnSpeciesIntegratedROP, "the opposed-flow flame model", int*, int*, int*, int*,
+                  double**)
+#undef CKMI_OUT_OF_SCOPE
 
 }  // extern "C"

@@ -1,0 +1,848 @@
+// ckmi_parse.cpp -- native Chemkin-II gas-phase mechanism interpreter (host code).
+//
+// The parse half of KINPreProcess (chemkin_wrapper.py:303-316, called from chemistry.py:675-687):
+// chem.inp (ELEMENTS / SPECIES / optional THERMO / REACTIONS) + therm.dat (fixed-column NASA-7) ->
+// the flat tables of ckmi_mech_desc (include/ckmi.h) plus the symbols, atomic weights and element
+// counts the KIN getters return.  The grammar and every table entry follow pychemkin_amd/mechanism.py
+// (the package's Python interpreter, kept as the test-side reader): tests/test_parse_native.py
+// checks that the two produce bitwise-identical tables for every mechanism under data/.
+//
+// Supported: element /weight/, species lists, inline THERMO (overrides the thermo file),
+// REACTIONS unit keywords and per-reaction UNITS, '=', '<=>', '=>', +M, (+M) / (+species)
+// falloff, LOW, HIGH (chemically activated), TROE (3/4), SRI (3/5), REV, DUPLICATE, efficiencies,
+// FORD / RORD, non-integral coefficients, PLOG.  Anything else raises (an error code + message),
+// never a silent skip.
+#include <algorithm>
+#include <array>
+#include <cctype>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/ckmi.h"
+#include "../../include/ckmi_kin.h"
+
+namespace {
+
+constexpr double AVOGADRO = 6.02214179e23;            // reference constants.py:27
+constexpr double P_ATM = 1.01325e6;                   // reference constants.py:28
+constexpr double RU_ACT = 8.314510e7;                 // Chemkin's interpreter RU (mechanism.py RU_ACT)
+constexpr double RUC_ACT = RU_ACT / 4.184e7;          // cal/mol-K
+constexpr int S = CKMI_SLOTS;
+
+enum Kind { ELEMENTARY = 0, THIRDBODY = 1, FALLOFF = 2, CHEMACT = 3 };
+
+struct ParseError {
+  std::string msg;
+};
+[[noreturn]] void die(const std::string& m) { throw ParseError{m}; }
+
+std::string upper(std::string s) {
+  for (char& c : s) c = (char)std::toupper((unsigned char)c);
+  return s;
+}
+std::string trim(const std::string& s) {
+  size_t a = s.find_first_not_of(" \t\r\n"), b = s.find_last_not_of(" \t\r\n");
+  return a == std::string::npos ? std::string() : s.substr(a, b - a + 1);
+}
+std::string rstrip(const std::string& s) {
+  size_t b = s.find_last_not_of(" \t\r\n");
+  return b == std::string::npos ? std::string() : s.substr(0, b + 1);
+}
+std::vector<std::string> split_ws(const std::string& s) {
+  std::vector<std::string> out;
+  std::istringstream is(s);
+  std::string t;
+  while (is >> t) out.push_back(t);
+  return out;
+}
+std::string strip_comment(const std::string& l) {
+  size_t i = l.find('!');
+  return i == std::string::npos ? l : l.substr(0, i);
+}
+// Fortran-style real: D exponents allowed (mechanism.py _to_float)
+bool to_float(std::string s, double* out) {
+  for (char& c : s)
+    if (c == 'D' || c == 'd') c = 'E';
+  s = trim(s);
+  if (s.empty()) return false;
+  char* end = nullptr;
+  *out = std::strtod(s.c_str(), &end);
+  return end && *end == '\0';
+}
+double num(const std::string& s, const std::string& ctx) {
+  double v;
+  if (!to_float(s, &v)) die("bad number '" + s + "' in " + ctx);
+  return v;
+}
+bool is_number(const std::string& s) {
+  double v;
+  return to_float(s, &v);
+}
+
+const std::map<std::string, double>& atomic_weights() {  // Chemkin defaults (mechanism.py ATOMIC_WEIGHTS)
+  static const std::map<std::string, double> w = {
+      {"H", 1.00797},   {"HE", 4.0026},   {"LI", 6.939},    {"BE", 9.01220},  {"B", 10.811},    {"C", 12.01115},
+      {"N", 14.0067},   {"O", 15.9994},   {"F", 18.9984},   {"NE", 20.183},   {"NA", 22.9898},  {"MG", 24.312},
+      {"AL", 26.9815},  {"SI", 28.086},   {"P", 30.9738},   {"S", 32.064},    {"CL", 35.453},   {"AR", 39.948},
+      {"K", 39.102},    {"CA", 40.08},    {"SC", 44.956},   {"TI", 47.90},    {"V", 50.942},    {"CR", 51.996},
+      {"MN", 54.938},   {"FE", 55.847},   {"CO", 58.9332},  {"NI", 58.71},    {"CU", 63.54},    {"ZN", 65.37},
+      {"GA", 69.72},    {"GE", 72.59},    {"AS", 74.9216},  {"SE", 78.96},    {"BR", 79.9009},  {"KR", 83.80},
+      {"RB", 85.47},    {"SR", 87.62},    {"Y", 88.905},    {"ZR", 91.22},    {"NB", 92.906},   {"MO", 95.94},
+      {"TC", 99.0},     {"RU", 101.07},   {"RH", 102.905},  {"PD", 106.4},    {"AG", 107.87},   {"CD", 112.40},
+      {"IN", 114.82},   {"SN", 118.69},   {"SB", 121.75},   {"TE", 127.60},   {"I", 126.904},   {"XE", 131.30},
+      {"CS", 132.905},  {"BA", 137.34},   {"D", 2.01410},   {"E", 5.45e-4}};
+  return w;
+}
+
+// activation-energy unit -> factor to E/R [K]; A-factor units.  Full REACTIONS-line names and the
+// four-letter UNITS abbreviations (mechanism.py _unit_token).
+bool unit_token(const std::string& tok, std::string* e_units, std::string* a_units) {
+  const std::string t = upper(tok);
+  auto pre = [&](const char* p) { return t.rfind(p, 0) == 0; };
+  if (pre("MOLEC") || pre("MOLC")) *a_units = "MOLECULES";
+  else if (pre("MOLE")) *a_units = "MOLES";
+  else if (pre("KCAL")) *e_units = "KCAL/MOLE";
+  else if (pre("CAL")) *e_units = "CAL/MOLE";
+  else if (pre("KJOU")) *e_units = "KJOULES/MOLE";
+  else if (pre("JOUL")) *e_units = "JOULES/MOLE";
+  else if (pre("KELV")) *e_units = "KELVINS";
+  else if (pre("EVOL")) *e_units = "EVOLTS";
+  else return false;
+  return true;
+}
+double e_to_kelvin(const std::string& u) {
+  if (u == "CAL/MOLE") return 1.0 / RUC_ACT;
+  if (u == "KCAL/MOLE") return 1.0e3 / RUC_ACT;
+  if (u == "JOULES/MOLE") return 1.0 / (RU_ACT * 1.0e-7);
+  if (u == "KJOULES/MOLE") return 1.0e3 / (RU_ACT * 1.0e-7);
+  if (u == "KELVINS") return 1.0;
+  if (u == "EVOLTS") return 1.602176487e-12 / 1.3806504e-16;
+  die("unknown energy units " + u);
+}
+
+struct Thermo {
+  double tlow = 0, thigh = 0, tmid = 0;
+  double high[7] = {0}, low[7] = {0};
+  std::vector<std::pair<std::string, int>> comp;  // element, count (insertion order)
+};
+
+struct Reaction {
+  std::string equation;
+  std::vector<std::pair<int, double>> reac, prod;  // species index, coefficient
+  bool reversible = true;
+  double A = 0, b = 0, E = 0;
+  int kind = ELEMENTARY;
+  int third = -2;  // -2 none, -1 mixture M, >= 0 collider species
+  std::vector<std::pair<int, double>> eff;  // insertion order, later entries overwrite
+  bool has_low = false, has_high = false, has_rev = false, has_troe = false, has_sri = false;
+  double low[3] = {0}, high[3] = {0}, rev[3] = {0};
+  std::vector<double> troe, sri;
+  bool duplicate = false;
+  std::vector<std::pair<int, double>> ford, rord;
+  std::vector<std::array<double, 4>> plog;
+  std::string e_units = "CAL/MOLE", a_units = "MOLES";
+};
+
+void set_pair(std::vector<std::pair<int, double>>& v, int k, double x) {
+  for (auto& p : v)
+    if (p.first == k) {
+      p.second = x;
+      return;
+    }
+  v.push_back({k, x});
+}
+const double* find_pair(const std::vector<std::pair<int, double>>& v, int k) {
+  for (const auto& p : v)
+    if (p.first == k) return &p.second;
+  return nullptr;
+}
+
+// fixed-column NASA-7 records (mechanism.py parse_thermo_text); first definition wins
+void parse_thermo(const std::vector<std::string>& lines, const std::map<std::string, int>& wanted,
+                  std::map<std::string, Thermo>& out) {
+  size_t i = 0;
+  while (i < lines.size()) {
+    const std::string s = upper(trim(lines[i]));
+    if (s.rfind("THERMO", 0) == 0) {
+      ++i;
+      if (i < lines.size()) {  // the optional default-temperature line
+        const auto t = split_ws(strip_comment(lines[i]));
+        if (t.size() == 3 && is_number(t[0]) && is_number(t[1]) && is_number(t[2])) ++i;
+      }
+      break;
+    }
+    if (!s.empty() && s[0] != '!') break;
+    ++i;
+  }
+  for (; i < lines.size();) {
+    const std::string& raw = lines[i];
+    const std::string st = trim(raw);
+    if (st.empty() || st[0] == '!') {
+      ++i;
+      continue;
+    }
+    if (upper(st).rfind("END", 0) == 0) break;
+    if (i + 3 >= lines.size()) break;
+    std::string l1 = rstrip(raw);
+    l1.resize(std::max<size_t>(l1.size(), 80), ' ');
+    const auto nt = split_ws(l1.substr(0, 18));
+    const std::string name = nt.empty() ? "" : nt[0];
+    Thermo th;
+    auto add_el = [&](const std::string& el, int n) {
+      for (auto& p : th.comp)
+        if (p.first == el) {
+          p.second += n;
+          return;
+        }
+      th.comp.push_back({el, n});
+    };
+    for (int k = 0; k < 4; ++k) {
+      const std::string fld = l1.substr(24 + 5 * k, 5);
+      const std::string el = upper(trim(fld.substr(0, 2))), cnt = trim(fld.substr(2, 3));
+      if (!el.empty() && el != "0" && !cnt.empty()) {
+        double x;
+        const int n = to_float(cnt, &x) ? (int)x : 0;
+        if (n != 0) add_el(el, n);
+      }
+    }
+    {
+      const std::string fld = l1.substr(73, 5);
+      const std::string el = upper(trim(fld.substr(0, 2))), cnt = trim(fld.substr(2, 3));
+      double x;
+      if (!el.empty() && !cnt.empty() && to_float(cnt, &x) && (int)x) add_el(el, (int)x);
+    }
+    double v;
+    if (!to_float(l1.substr(45, 10), &th.tlow) || !to_float(l1.substr(55, 10), &th.thigh))
+      die("bad thermo header for '" + name + "': " + raw);
+    const std::string tm = trim(l1.substr(65, 8));
+    th.tmid = 1000.0;
+    if (!tm.empty() && !to_float(tm, &th.tmid)) die("bad thermo header for '" + name + "': " + raw);
+    double c[14];
+    int nc = 0;
+    for (int k = 1; k <= 3; ++k) {
+      std::string ln = rstrip(lines[i + k]);
+      ln.resize(std::max<size_t>(ln.size(), 80), ' ');
+      const int nf = k < 3 ? 5 : 4;
+      for (int m = 0; m < nf; ++m) {
+        const std::string f = trim(ln.substr(15 * m, 15));
+        c[nc++] = f.empty() ? 0.0 : (to_float(f, &v) ? v : (die("bad thermo coefficient for " + name), 0.0));
+      }
+    }
+    i += 4;
+    const std::string key = upper(name);
+    if (!wanted.count(key) || out.count(key)) continue;
+    std::copy(c, c + 7, th.high);
+    std::copy(c + 7, c + 14, th.low);
+    out[key] = th;
+  }
+}
+
+struct Mech {
+  std::vector<std::string> elements, species;
+  std::vector<double> awt;
+  std::map<std::string, int> sp_index;  // upper-case name -> index
+  std::vector<Reaction> rx;
+  std::vector<Thermo> thermo;
+  std::vector<int32_t> ncf;  // [MM][KK]
+  std::vector<double> wt;
+  std::vector<std::string> inline_thermo;
+
+  // flat tables (ckmi_mech_desc)
+  std::vector<double> t_thermo, rnu, pnu, ford, rord, arr, low, revp, fpar, eff_val, plog_par;
+  std::vector<int32_t> rtype, rev, nr, np, rsp, psp, has_rev, ftype, tbsp, eff_ptr, eff_sp, plog_ptr;
+
+  int species_of(const std::string& tok) const {
+    auto it = sp_index.find(upper(tok));
+    return it == sp_index.end() ? -1 : it->second;
+  }
+
+  // one side of an equation -> merged (species, coefficient), third body, falloff flag
+  void side(std::string s, const std::string& eq, std::vector<std::pair<int, double>>& terms, int* third,
+            bool* falloff) {
+    *third = -2;
+    *falloff = false;
+    size_t p = s.find("(+");
+    if (p != std::string::npos) {
+      size_t q = s.find(')', p);
+      if (q == std::string::npos) die("unclosed (+ in " + eq);
+      const std::string tb = trim(s.substr(p + 2, q - p - 2));
+      *falloff = true;
+      if (upper(tb) == "M") *third = -1;
+      else if ((*third = species_of(tb)) < 0) die("unknown falloff collider " + tb + " in " + eq);
+      s = s.substr(0, p) + s.substr(q + 1);
+    }
+    std::vector<std::pair<int, double>> raw;
+    size_t a = 0;
+    while (a <= s.size()) {
+      size_t b = s.find('+', a);
+      if (b == std::string::npos) b = s.size();
+      const std::string tok = trim(s.substr(a, b - a));
+      a = b + 1;
+      if (tok.empty()) continue;
+      if (upper(tok) == "M") {
+        if (*third != -2 && !*falloff) die("two third bodies in " + eq);
+        if (!*falloff) *third = -1;
+        continue;
+      }
+      int k = species_of(tok);
+      if (k >= 0) {
+        raw.push_back({k, 1.0});
+        continue;
+      }
+      // leading coefficient, mechanism.py's ^(\d+\.?\d*|\.\d+)(.+)$: the greedy number, then the rest
+      size_t j = 0;
+      while (j < tok.size() && std::isdigit((unsigned char)tok[j])) ++j;
+      const bool lead_digits = j > 0;
+      if (j < tok.size() && tok[j] == '.') {
+        ++j;
+        const size_t f = j;
+        while (j < tok.size() && std::isdigit((unsigned char)tok[j])) ++j;
+        if (!lead_digits && j == f) j = 0;  // "." alone is not a number
+      }
+      if (j == tok.size() && j > 0) --j;   // (.+) needs one character: the regex backtracks
+      if (j > 0 && !(j == 1 && tok[0] == '.')) {
+        if ((k = species_of(tok.substr(j))) >= 0) {
+          raw.push_back({k, std::strtod(tok.substr(0, j).c_str(), nullptr)});
+          continue;
+        }
+      }
+      die("unknown species '" + tok + "' in reaction " + eq);
+    }
+    for (const auto& t : raw) {
+      bool found = false;
+      for (auto& m : terms)
+        if (m.first == t.first) {
+          m.second += t.second;
+          found = true;
+        }
+      if (!found) terms.push_back({t.first, 0.0 + t.second});
+    }
+  }
+
+  Reaction* reaction_line(const std::string& s, Reaction* cur, const std::string& e_units,
+                          const std::string& a_units) {
+    const std::string up = upper(s);
+    bool aux = s.find('=') == std::string::npos;
+    if (!aux) {
+      const std::string w = split_ws(up)[0];
+      static const char* kws[] = {"LOW", "TROE", "SRI", "REV", "HIGH", "FORD", "RORD", "PLOG", "DUP", "DUPLICATE", "UNITS"};
+      for (const char* k : kws) {
+        const size_t n = std::strlen(k);
+        if (up.compare(up.find_first_not_of(" \t"), n, k) == 0) {
+          const size_t at = up.find_first_not_of(" \t") + n;
+          if (at >= up.size() || !(std::isalnum((unsigned char)up[at]) || up[at] == '_')) aux = true;
+        }
+      }
+      (void)w;
+    }
+    if (!aux) {
+      const auto toks = split_ws(s);
+      if (toks.size() < 4) die("reaction line needs equation + A b E: '" + s + "'");
+      Reaction r;
+      r.A = num(toks[toks.size() - 3], s);
+      r.b = num(toks[toks.size() - 2], s);
+      r.E = num(toks[toks.size() - 1], s);
+      std::string eq;
+      for (size_t i = 0; i + 3 < toks.size(); ++i) eq += toks[i];
+      r.equation = eq;
+      std::string lhs, rhs;
+      size_t p;
+      if ((p = eq.find("<=>")) != std::string::npos) {
+        lhs = eq.substr(0, p), rhs = eq.substr(p + 3), r.reversible = true;
+      } else if ((p = eq.find("=>")) != std::string::npos) {
+        lhs = eq.substr(0, p), rhs = eq.substr(p + 2), r.reversible = false;
+      } else if ((p = eq.find('=')) != std::string::npos) {
+        lhs = eq.substr(0, p), rhs = eq.substr(p + 1), r.reversible = true;
+      } else {
+        die("no '=' in " + eq);
+      }
+      if (rhs.find('=') != std::string::npos) die("more than one '=' in " + eq);
+      int rt, pt;
+      bool rf, pf;
+      side(lhs, eq, r.reac, &rt, &rf);
+      side(rhs, eq, r.prod, &pt, &pf);
+      if ((rt == -2) != (pt == -2) || rf != pf) die("unbalanced third body in " + eq);
+      if (rf) {
+        r.kind = FALLOFF;
+        r.third = rt;
+      } else if (rt != -2) {
+        r.kind = THIRDBODY;
+        r.third = -1;
+      }
+      r.e_units = e_units;
+      r.a_units = a_units;
+      rx.push_back(r);
+      return &rx.back();
+    }
+    if (!cur) die("auxiliary data before any reaction: '" + s + "'");
+    // keywords with /values/ and efficiency pairs (mechanism.py: ([A-Za-z0-9()\-,*#\[\]_]+)\s*(?:/([^/]*)/)?)
+    auto keych = [](char c) {
+      return std::isalnum((unsigned char)c) || std::strchr("()-,*#[]_", c) != nullptr;
+    };
+    size_t i = 0;
+    while (i < s.size()) {
+      if (!keych(s[i])) {
+        ++i;
+        continue;
+      }
+      size_t j = i;
+      while (j < s.size() && keych(s[j])) ++j;
+      const std::string key = s.substr(i, j - i);
+      std::string vals;
+      bool has_vals = false;
+      size_t q = j;
+      while (q < s.size() && (s[q] == ' ' || s[q] == '\t')) ++q;
+      if (q < s.size() && s[q] == '/') {
+        const size_t e = s.find('/', q + 1);
+        if (e != std::string::npos) {
+          vals = s.substr(q + 1, e - q - 1);
+          has_vals = true;
+          j = e + 1;
+        }
+      }
+      i = j;
+      const std::string k = upper(key);
+      const auto parts = split_ws(vals);
+      std::vector<double> nums;
+      if (has_vals && k != "FORD" && k != "RORD" && k != "UNITS")
+        for (const auto& v : parts) nums.push_back(num(v, s));
+      auto need = [&](size_t n) {
+        if (nums.size() < n) die(k + " needs " + std::to_string(n) + " values: '" + s + "'");
+      };
+      if (k == "DUP" || k == "DUPLICATE") {
+        cur->duplicate = true;
+      } else if (k == "LOW") {
+        need(3);
+        std::copy(nums.begin(), nums.begin() + 3, cur->low);
+        cur->has_low = true;
+        if (cur->kind != FALLOFF) die("LOW on a non-falloff reaction " + cur->equation);
+      } else if (k == "HIGH") {
+        need(3);
+        if ((cur->kind != FALLOFF && cur->kind != CHEMACT) || cur->third == -2)
+          die("HIGH on a reaction without (+M): " + cur->equation);
+        std::copy(nums.begin(), nums.begin() + 3, cur->high);
+        cur->has_high = true;
+        cur->kind = CHEMACT;
+      } else if (k == "TROE") {
+        cur->troe = nums;
+        cur->has_troe = true;
+      } else if (k == "SRI") {
+        cur->sri = nums;
+        cur->has_sri = true;
+      } else if (k == "REV") {
+        need(3);
+        std::copy(nums.begin(), nums.begin() + 3, cur->rev);
+        cur->has_rev = true;
+      } else if (k == "FORD" || k == "RORD") {
+        int sp;
+        double o;
+        if (parts.size() != 2 || (sp = species_of(parts[0])) < 0 || !to_float(parts[1], &o))
+          die(k + " needs /species order/: '" + s + "'");
+        set_pair(k == "FORD" ? cur->ford : cur->rord, sp, o);
+      } else if (k == "PLOG") {
+        need(4);
+        cur->plog.push_back({nums[0], nums[1], nums[2], nums[3]});
+      } else if (k == "UNITS") {
+        // per-reaction units: this reaction's A / E (and its LOW, HIGH, REV, PLOG) are in them
+        if (parts.empty()) die("UNITS needs /unit .../: '" + s + "'");
+        for (const auto& u : parts)
+          if (!unit_token(u, &cur->e_units, &cur->a_units)) die("unknown UNITS '" + u + "' for " + cur->equation);
+      } else {
+        const int sp = species_of(key);
+        if (sp < 0) die("unknown auxiliary keyword '" + key + "' for " + cur->equation);
+        if (cur->kind == ELEMENTARY) die("efficiency on a reaction without +M: " + cur->equation);
+        set_pair(cur->eff, sp, nums.empty() ? 1.0 : nums[0]);
+      }
+    }
+    return cur;
+  }
+
+  void parse_chem(const std::string& text) {
+    std::vector<std::string> raw;
+    {
+      std::istringstream is(text);
+      std::string l;
+      while (std::getline(is, l)) raw.push_back(l);
+    }
+    std::string section, e_units = "CAL/MOLE", a_units = "MOLES";
+    Reaction* cur = nullptr;
+    size_t cur_i = (size_t)-1;
+    for (size_t ln = 0; ln < raw.size(); ++ln) {
+      std::string s = trim(rstrip(strip_comment(raw[ln])));
+      if (s.empty()) {
+        if (section == "THERMO") inline_thermo.push_back(raw[ln]);
+        continue;
+      }
+      std::string up = upper(s);
+      const std::string head = split_ws(up)[0];
+      auto rest = [&]() {
+        const size_t p = s.find_first_of(" \t");
+        return p == std::string::npos ? std::string() : trim(s.substr(p));
+      };
+      if (section != "THERMO" && (head == "ELEMENTS" || head == "ELEM")) {
+        section = "ELEMENTS";
+        s = rest();
+        up = upper(s);
+        if (s.empty()) continue;
+      } else if (section != "THERMO" && (head == "SPECIES" || head == "SPEC")) {
+        section = "SPECIES";
+        s = rest();
+        up = upper(s);
+        if (s.empty()) continue;
+      } else if (section != "THERMO" && (head == "THERMO" || head == "THER")) {
+        section = "THERMO";
+        inline_thermo.push_back(raw[ln]);
+        continue;
+      } else if (section != "THERMO" && (head == "REACTIONS" || head == "REAC")) {
+        section = "REACTIONS";
+        const auto t = split_ws(up);
+        for (size_t j = 1; j < t.size(); ++j) (void)unit_token(t[j], &e_units, &a_units);  // others ignored
+        continue;
+      }
+      if (up == "END" || up.rfind("END ", 0) == 0) {
+        if (section == "THERMO") inline_thermo.push_back(raw[ln]);
+        section.clear();
+        cur = nullptr;
+        continue;
+      }
+      bool end_here = false;
+      if (section == "ELEMENTS" || section == "SPECIES") {
+        auto t = split_ws(s);
+        for (size_t j = 0; j < t.size(); ++j)
+          if (upper(t[j]) == "END") {
+            std::string kept;
+            for (size_t m = 0; m < j; ++m) kept += (m ? " " : "") + t[m];
+            s = kept;
+            end_here = true;
+            break;
+          }
+      }
+      if (section == "ELEMENTS") {
+        // symbols, each with an optional /weight/
+        size_t i = 0;
+        while (i < s.size()) {
+          if (!std::isalpha((unsigned char)s[i])) {
+            ++i;
+            continue;
+          }
+          size_t j = i;
+          while (j < s.size() && std::isalnum((unsigned char)s[j])) ++j;
+          const std::string el = upper(s.substr(i, j - i));
+          double w = 0.0;
+          bool has_w = false;
+          size_t q = j;
+          while (q < s.size() && (s[q] == ' ' || s[q] == '\t')) ++q;
+          if (q < s.size() && s[q] == '/') {
+            const size_t e = s.find('/', q + 1);
+            if (e != std::string::npos && to_float(s.substr(q + 1, e - q - 1), &w)) {
+              has_w = true;
+              j = e + 1;
+            }
+          }
+          i = j;
+          if (std::find(elements.begin(), elements.end(), el) != elements.end()) continue;
+          elements.push_back(el);
+          if (has_w) awt.push_back(w);
+          else if (atomic_weights().count(el)) awt.push_back(atomic_weights().at(el));
+          else die("unknown element " + el + " without atomic weight");
+        }
+      } else if (section == "SPECIES") {
+        for (const auto& t : split_ws(s))
+          if (!sp_index.count(upper(t))) {
+            sp_index[upper(t)] = (int)species.size();
+            species.push_back(t);
+          }
+      }
+      if (end_here) {
+        section.clear();
+        cur = nullptr;
+        continue;
+      } else if (section == "THERMO") {
+        inline_thermo.push_back(raw[ln]);
+      } else if (section == "REACTIONS") {
+        // rx may reallocate: keep the current reaction as an index
+        Reaction* c = cur_i == (size_t)-1 || !cur ? nullptr : &rx[cur_i];
+        Reaction* r = reaction_line(s, c, e_units, a_units);
+        cur = r;
+        cur_i = r ? (size_t)(r - rx.data()) : (size_t)-1;
+      }
+    }
+  }
+
+  double A_cgs(const Reaction& r, double A, const std::vector<std::pair<int, double>>& sd, int extra) const {
+    if (r.a_units != "MOLECULES") return A;
+    double order = 0.0;
+    for (const auto& t : sd) order += t.second;
+    order += extra;
+    return A * std::pow(AVOGADRO, order - 1.0);
+  }
+
+  void finish() {
+    const int KK = (int)species.size(), MM = (int)elements.size(), II = (int)rx.size();
+    ncf.assign((size_t)MM * KK, 0);
+    for (int k = 0; k < KK; ++k)
+      for (const auto& p : thermo[k].comp) {
+        auto it = std::find(elements.begin(), elements.end(), p.first);
+        if (it == elements.end()) die("species " + species[k] + " uses undeclared element " + p.first);
+        ncf[(size_t)(it - elements.begin()) * KK + k] = p.second;
+      }
+    wt.assign(KK, 0.0);
+    for (int k = 0; k < KK; ++k) {
+      double w = 0.0;
+      for (int m = 0; m < MM; ++m) w = (m == 0) ? awt[m] * ncf[(size_t)m * KK + k] : w + awt[m] * ncf[(size_t)m * KK + k];
+      wt[k] = w;
+    }
+    for (const Reaction& r : rx) {
+      for (const auto& f : r.ford)
+        if (!find_pair(r.reac, f.first)) die("FORD species " + species[f.first] + " is not a reactant of " + r.equation);
+      for (const auto& f : r.rord)
+        if (!find_pair(r.prod, f.first)) die("RORD species " + species[f.first] + " is not a product of " + r.equation);
+      if (!r.rord.empty() && !r.reversible) die("RORD on an irreversible reaction " + r.equation);
+      for (int m = 0; m < MM; ++m) {
+        double bal = 0.0;
+        for (const auto& t : r.prod) bal += t.second * ncf[(size_t)m * KK + t.first];
+        for (const auto& t : r.reac) bal -= t.second * ncf[(size_t)m * KK + t.first];
+        if (std::fabs(bal) > 1e-6) die("reaction " + r.equation + " is not element balanced");
+      }
+    }
+    // ---- flat tables (mechanism.py Mechanism.to_tables)
+    rtype.assign(II, 0), rev.assign(II, 0), nr.assign(II, 0), np.assign(II, 0);
+    rsp.assign((size_t)II * S, 0), psp.assign((size_t)II * S, 0);
+    rnu.assign((size_t)II * S, 0.0), pnu.assign((size_t)II * S, 0.0), ford.assign((size_t)II * S, 0.0),
+        rord.assign((size_t)II * S, 0.0);
+    arr.assign((size_t)II * 3, 0.0), low.assign((size_t)II * 3, 0.0), revp.assign((size_t)II * 3, 0.0);
+    has_rev.assign(II, 0), ftype.assign(II, 0), fpar.assign((size_t)II * 5, 0.0), tbsp.assign(II, -1);
+    eff_ptr.assign(1, 0), eff_sp.clear(), eff_val.clear(), plog_ptr.assign(II + 1, 0), plog_par.clear();
+    for (int i = 0; i < II; ++i) {
+      const Reaction& r = rx[i];
+      const double es = e_to_kelvin(r.e_units);
+      if (!r.plog.empty()) {
+        if (r.kind != ELEMENTARY || r.has_rev) die("PLOG on a third-body/falloff reaction or with REV (" + r.equation + ")");
+        auto pts = r.plog;
+        std::stable_sort(pts.begin(), pts.end(), [](const auto& a, const auto& b) { return a[0] < b[0]; });
+        for (size_t j = 0; j + 1 < pts.size(); ++j)
+          if (pts[j][0] == pts[j + 1][0]) die("PLOG pressures must be positive and distinct (" + r.equation + ")");
+        if (pts[0][0] <= 0.0) die("PLOG pressures must be positive and distinct (" + r.equation + ")");
+        for (const auto& e : pts) {
+          const double Ap = A_cgs(r, e[1], r.reac, 0);
+          plog_par.insert(plog_par.end(), {std::log(e[0] * P_ATM), std::log(Ap), e[2], e[3] * es});
+        }
+      }
+      if ((int)r.reac.size() > S || (int)r.prod.size() > S)
+        die("more than " + std::to_string(S) + " species on one side of " + r.equation);
+      rtype[i] = !r.plog.empty() ? CKMI_RXN_PLOG : (r.kind == CHEMACT ? CKMI_RXN_CHEMACT : r.kind);
+      plog_ptr[i + 1] = (int32_t)(plog_par.size() / 4);
+      rev[i] = r.reversible ? 1 : 0;
+      nr[i] = (int32_t)r.reac.size();
+      np[i] = (int32_t)r.prod.size();
+      for (size_t j = 0; j < r.reac.size(); ++j) {
+        rsp[(size_t)i * S + j] = r.reac[j].first;
+        rnu[(size_t)i * S + j] = r.reac[j].second;
+        const double* f = find_pair(r.ford, r.reac[j].first);
+        ford[(size_t)i * S + j] = f ? *f : r.reac[j].second;
+      }
+      for (size_t j = 0; j < r.prod.size(); ++j) {
+        psp[(size_t)i * S + j] = r.prod[j].first;
+        pnu[(size_t)i * S + j] = r.prod[j].second;
+        const double* f = find_pair(r.rord, r.prod[j].first);
+        rord[(size_t)i * S + j] = f ? *f : r.prod[j].second;
+      }
+      const int extra = r.kind == THIRDBODY ? 1 : 0;
+      const double A = A_cgs(r, r.A, r.reac, (r.kind == THIRDBODY || r.kind == CHEMACT) ? 1 : 0);
+      arr[(size_t)i * 3 + 0] = A > 0 ? std::log(A) : -1e300;
+      arr[(size_t)i * 3 + 1] = r.b;
+      arr[(size_t)i * 3 + 2] = r.E * es;
+      if (r.kind == FALLOFF || r.kind == CHEMACT) {
+        if (r.kind == FALLOFF && !r.has_low) die("falloff reaction without LOW: " + r.equation);
+        if (r.kind == CHEMACT && (!r.has_high || r.has_low))
+          die("chemically activated reaction needs HIGH and no LOW: " + r.equation);
+        const double* lim = r.kind == FALLOFF ? r.low : r.high;
+        const double A0 = A_cgs(r, lim[0], r.reac, r.kind == FALLOFF ? 1 : 0);
+        low[(size_t)i * 3 + 0] = std::log(A0);
+        low[(size_t)i * 3 + 1] = lim[1];
+        low[(size_t)i * 3 + 2] = lim[2] * es;
+        if (r.has_troe) {
+          if (r.troe.size() == 3) ftype[i] = CKMI_FALL_TROE3;
+          else if (r.troe.size() == 4) ftype[i] = CKMI_FALL_TROE4;
+          else die("TROE needs 3 or 4 parameters: " + r.equation);
+          std::copy(r.troe.begin(), r.troe.end(), fpar.begin() + (size_t)i * 5);
+        } else if (r.has_sri) {
+          ftype[i] = CKMI_FALL_SRI;
+          if (r.sri.size() != 3 && r.sri.size() != 5) die("SRI needs 3 or 5 parameters: " + r.equation);
+          std::vector<double> sri = r.sri;
+          if (sri.size() == 3) sri.insert(sri.end(), {1.0, 0.0});
+          for (size_t j = 0; j < 5 && j < sri.size(); ++j) fpar[(size_t)i * 5 + j] = sri[j];
+        } else {
+          ftype[i] = CKMI_FALL_LINDEMANN;
+        }
+        if (r.third >= 0) tbsp[i] = r.third;
+      }
+      if (r.has_rev) {
+        if (!r.reversible) die("REV on an irreversible reaction " + r.equation);
+        has_rev[i] = 1;
+        const double Ar = A_cgs(r, r.rev[0], r.prod, extra);
+        revp[(size_t)i * 3 + 0] = Ar > 0 ? std::log(Ar) : -1e300;
+        revp[(size_t)i * 3 + 1] = r.rev[1];
+        revp[(size_t)i * 3 + 2] = r.rev[2] * es;
+      }
+      if ((r.kind == THIRDBODY || r.kind == FALLOFF || r.kind == CHEMACT) && tbsp[i] < 0)
+        for (const auto& e : r.eff) {
+          eff_sp.push_back(e.first);
+          eff_val.push_back(e.second);
+        }
+      eff_ptr.push_back((int32_t)eff_sp.size());
+    }
+    if (plog_par.empty()) plog_par.assign(4, 0.0);
+    t_thermo.assign((size_t)KK * 17, 0.0);
+    for (int k = 0; k < KK; ++k) {
+      double* t = &t_thermo[(size_t)k * 17];
+      t[0] = thermo[k].tlow, t[1] = thermo[k].tmid, t[2] = thermo[k].thigh;
+      std::copy(thermo[k].low, thermo[k].low + 7, t + 3);
+      std::copy(thermo[k].high, thermo[k].high + 7, t + 10);
+    }
+  }
+
+  void load(const std::string& chem_text, const std::string& therm_text) {
+    parse_chem(chem_text);
+    std::map<std::string, Thermo> data;
+    std::map<std::string, int> wanted;
+    for (const auto& s : species) wanted[upper(s)] = 1;
+    auto lines_of = [](const std::string& t) {
+      std::vector<std::string> v;
+      std::istringstream is(t);
+      std::string l;
+      while (std::getline(is, l)) v.push_back(l);
+      return v;
+    };
+    if (!therm_text.empty()) parse_thermo(lines_of(therm_text), wanted, data);
+    if (!inline_thermo.empty()) {  // a THERMO block inside chem.inp overrides the thermo file
+      std::map<std::string, Thermo> in;
+      parse_thermo(inline_thermo, wanted, in);
+      for (auto& kv : in) data[kv.first] = kv.second;
+    }
+    std::string missing;
+    for (const auto& s : species)
+      if (!data.count(upper(s))) missing += (missing.empty() ? "" : ", ") + s;
+    if (!missing.empty()) die("no thermo data for species [" + missing + "]");
+    for (const auto& s : species) thermo.push_back(data[upper(s)]);
+    finish();
+  }
+};
+
+thread_local std::string g_perr;
+
+bool read_file(const char* path, std::string* out) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::ostringstream ss;
+  ss << f.rdbuf();
+  *out = ss.str();
+  return true;
+}
+
+}  // namespace
+
+struct ckmi_parsed {
+  Mech m;
+};
+
+extern "C" {
+
+const char* ckmi_parse_last_error(void) { return g_perr.c_str(); }
+
+int ckmi_parse_mechanism(const char* chem_text, const char* therm_text, ckmi_parsed** out) {
+  if (!chem_text || !out) {
+    g_perr = "null argument";
+    return CKMI_ERR_ARG;
+  }
+  auto* p = new ckmi_parsed();
+  try {
+    p->m.load(chem_text, therm_text ? therm_text : "");
+  } catch (const ParseError& e) {
+    g_perr = e.msg;
+    delete p;
+    return CKMI_ERR_ARG;
+  } catch (const std::exception& e) {
+    g_perr = std::string("mechanism parse failed: ") + e.what();
+    delete p;
+    return CKMI_ERR_ARG;
+  }
+  *out = p;
+  return CKMI_OK;
+}
+
+int ckmi_parse_files(const char* chemfile, const char* thermfile, ckmi_parsed** out) {
+  std::string chem, therm;
+  if (!chemfile || !read_file(chemfile, &chem)) {
+    g_perr = std::string("cannot read mechanism file ") + (chemfile ? chemfile : "(null)");
+    return CKMI_ERR_ARG;
+  }
+  if (thermfile && *thermfile && !read_file(thermfile, &therm)) {
+    g_perr = std::string("cannot read thermo file ") + thermfile;
+    return CKMI_ERR_ARG;
+  }
+  return ckmi_parse_mechanism(chem.c_str(), therm.c_str(), out);
+}
+
+void ckmi_parsed_free(ckmi_parsed* p) { delete p; }
+
+int ckmi_parsed_sizes(const ckmi_parsed* p, int32_t* MM, int32_t* KK, int32_t* II) {
+  if (!p) return CKMI_ERR_ARG;
+  if (MM) *MM = (int32_t)p->m.elements.size();
+  if (KK) *KK = (int32_t)p->m.species.size();
+  if (II) *II = (int32_t)p->m.rx.size();
+  return CKMI_OK;
+}
+
+int ckmi_parsed_desc(const ckmi_parsed* p, ckmi_mech_desc* d) {
+  if (!p || !d) return CKMI_ERR_ARG;
+  const Mech& m = p->m;
+  d->KK = (int32_t)m.species.size();
+  d->II = (int32_t)m.rx.size();
+  d->wt = m.wt.data(), d->thermo = m.t_thermo.data();
+  d->rtype = m.rtype.data(), d->rev = m.rev.data(), d->nr = m.nr.data(), d->np = m.np.data();
+  d->rsp = m.rsp.data(), d->psp = m.psp.data(), d->rnu = m.rnu.data(), d->pnu = m.pnu.data();
+  d->arr = m.arr.data(), d->low = m.low.data(), d->revp = m.revp.data(), d->has_rev = m.has_rev.data();
+  d->ftype = m.ftype.data(), d->fpar = m.fpar.data(), d->tbsp = m.tbsp.data();
+  d->eff_ptr = m.eff_ptr.data(), d->eff_sp = m.eff_sp.data(), d->eff_val = m.eff_val.data();
+  d->plog_ptr = m.plog_ptr.data(), d->plog_par = m.plog_par.data();
+  d->ford = m.ford.data(), d->rord = m.rord.data();
+  return CKMI_OK;
+}
+
+int ckmi_parsed_symbols(const ckmi_parsed* p, char* species, char* elements, double* awt, int32_t* ncf) {
+  if (!p) return CKMI_ERR_ARG;
+  const Mech& m = p->m;
+  for (size_t k = 0; species && k < m.species.size(); ++k) {
+    std::memset(species + 16 * k, 0, 16);
+    std::memcpy(species + 16 * k, m.species[k].c_str(), std::min<size_t>(16, m.species[k].size()));
+  }
+  for (size_t e = 0; elements && e < m.elements.size(); ++e) {
+    std::memset(elements + 16 * e, 0, 16);
+    std::memcpy(elements + 16 * e, m.elements[e].c_str(), std::min<size_t>(16, m.elements[e].size()));
+  }
+  if (awt) std::copy(m.awt.begin(), m.awt.end(), awt);
+  if (ncf) std::copy(m.ncf.begin(), m.ncf.end(), ncf);
+  return CKMI_OK;
+}
+
+int ckmi_parsed_equation(const ckmi_parsed* p, int32_t i, char* buf, int32_t cap, int32_t* len) {
+  if (!p || i < 0 || i >= (int32_t)p->m.rx.size()) return CKMI_ERR_ARG;
+  const std::string& e = p->m.rx[i].equation;
+  if (len) *len = (int32_t)e.size();
+  if (buf && cap > 0) {
+    const size_t n = std::min<size_t>(e.size(), (size_t)cap - 1);
+    std::memcpy(buf, e.data(), n);
+    buf[n] = '\0';
+  }
+  return CKMI_OK;
+}
+
+}  // extern "C"

@@ -26,38 +26,92 @@ _IF = np.ctypeslib.ndpointer(dtype=np.int32, flags="F_CONTIGUOUS")
 
 # name -> (restype, argtypes), as chemkin_wrapper.py declares them (line of each in ckmi_kin.h)
 KIN_PROTOTYPES = {
-    "KINSetUnitSystem": (ct.c_int, [_I]),
-    "KINInitialize": (ct.c_int, [_I, _I]),
-    "KINFinish": (None, []),
-    "KINUpdateChemistrySet": (ct.c_int, [_I]),
-    "KINSwitchChemistrySet": (ct.c_int, [_I]),
-    "KINGetChemistrySizes": (ct.c_int, [_I] * 9),
-    "KINGetGasSpeciesNames": (ct.c_int, [_I, ct.POINTER(_C)]),
-    "KINGetElementNames": (ct.c_int, [_I, ct.POINTER(_C)]),
-    "KINGetAtomicWeights": (ct.c_int, [_I, _DC]),
-    "KINGetGasMolecularWeights": (ct.c_int, [_I, _DC]),
-    "KINGetGasSpeciesComposition": (ct.c_int, [_I, _IF]),
-    "KINGetGasSpecificHeat": (ct.c_int, [_I, _D, _DC]),
-    "KINGetGasSpeciesEnthalpy": (ct.c_int, [_I, _D, _DC]),
-    "KINGetGasSpeciesInternalEnergy": (ct.c_int, [_I, _D, _DC]),
-    "KINGetMassDensity": (ct.c_int, [_I, _D, _D, _DC, _D]),
-    "KINGetGasMixtureSpecificHeat": (ct.c_int, [_I, _D, _DC, _D]),
-    "KINGetGasMixtureEnthalpy": (ct.c_int, [_I, _D, _DC, _D]),
-    "KINGetGasROP": (ct.c_int, [_I, _D, _D, _DC, _DC]),
-    "KINGetGasReactionRates": (ct.c_int, [_I, _D, _D, _DC, _DC, _DC]),
-    "KINGetReactionRateParameters": (ct.c_int, [_I, _DC, _DC, _DC]),
-    "KINSetAFactorForAReaction": (ct.c_int, [_I, _I, _D]),
-    "KINAll0D_Setup": (ct.c_int, [_I, _I, _I, _I, _I, _I, _IC, _I]),
-    "KINAll0D_SetupWorkArrays": (ct.c_int, [_I, _I]),
-    "KINAll0D_SetupBatchInputs": (ct.c_int, [_I, _D, _D, _D, _D, _D, _D, _DC, _DC, _DC]),
-    "KINAll0D_IntegrateHeatRelease": (ct.c_int, []),
-    "KINAll0D_SetProfilePoints": (ct.c_int, [_I]),
-    "KINAll0D_SetProfileParameter": (ct.c_int, [_C, _I, _DC, _DC]),
-    "KINAll0D_SetUserKeyword": (ct.c_int, [_C]),
-    "KINAll0D_Calculate": (ct.c_int, [_I]),
-    "KINAll0D_GetIgnitionDelay": (ct.c_int, [_D]),
-    "KINAll0D_GetSolnResponseSize": (ct.c_int, [_I, _I]),
-    "KINAll0D_GetGasSolnResponse": (ct.c_int, [_I, _I, _I, _DC, _DC, _DC, _DC, _DF]),
+    "KINSetUnitSystem": (ct.c_int, [_I]),                                                           # :301
+    "KINPreProcess": (ct.c_int, [_I, _I, _C, _C, _C, _C, _C, _C, _C, _C, _I]),                      # :304
+    "KINInitialize": (ct.c_int, [_I, _I]),                                                          # :318
+    "KINFinish": (None, []),                                                                        # :323
+    "KINUpdateChemistrySet": (ct.c_int, [_I]),                                                      # :325
+    "KINSwitchChemistrySet": (ct.c_int, [_I]),                                                      # :329
+    "KINGetChemistrySizes": (ct.c_int, [_I, _I, _I, _I, _I, _I, _I, _I, _I]),                       # :334
+    "KINGetGasSpeciesNames": (ct.c_int, [_I, ct.POINTER(_C)]),                                      # :346
+    "KINGetElementNames": (ct.c_int, [_I, ct.POINTER(_C)]),                                         # :351
+    "KINGetAtomicWeights": (ct.c_int, [_I, _DC]),                                                   # :356
+    "KINGetGasMolecularWeights": (ct.c_int, [_I, _DC]),                                             # :361
+    "KINGetGasReactionString": (ct.c_int, [_I, _I, _I, _C]),                                        # :366
+    "KINGetReactionStringLength": (ct.c_int, [_I]),                                                 # :373
+    "KINGetGasSpecificHeat": (ct.c_int, [_I, _D, _DC]),                                             # :376
+    "KINGetGasSpeciesEnthalpy": (ct.c_int, [_I, _D, _DC]),                                          # :382
+    "KINGetGasSpeciesInternalEnergy": (ct.c_int, [_I, _D, _DC]),                                    # :388
+    "KINGetGasSpeciesComposition": (ct.c_int, [_I, _IF]),                                           # :394
+    "KINGetMassDensity": (ct.c_int, [_I, _D, _D, _DC, _D]),                                         # :399
+    "KINGetViscosity": (ct.c_int, [_I, _D, _DC]),                                                   # :408
+    "KINGetConductivity": (ct.c_int, [_I, _D, _DC]),                                                # :414
+    "KINGetDiffusionCoeffs": (ct.c_int, [_I, _D, _D, _DF]),                                         # :420
+    "KINGetGasMixtureSpecificHeat": (ct.c_int, [_I, _D, _DC, _D]),                                  # :428
+    "KINGetGasMixtureEnthalpy": (ct.c_int, [_I, _D, _DC, _D]),                                      # :435
+    "KINGetMixtureViscosity": (ct.c_int, [_I, _D, _DC, _D]),                                        # :443
+    "KINGetMixtureConductivity": (ct.c_int, [_I, _D, _DC, _D]),                                     # :450
+    "KINGetMixtureDiffusionCoeffs": (ct.c_int, [_I, _D, _D, _DC, _DC]),                             # :457
+    "KINGetOrdinaryDiffusionCoeffs": (ct.c_int, [_I, _D, _D, _DC, _DF]),                            # :465
+    "KINGetThermalDiffusionCoeffs": (ct.c_int, [_I, _D, _D, _DC, _DC, _D]),                         # :473
+    "KINGetGasROP": (ct.c_int, [_I, _D, _D, _DC, _DC]),                                             # :483
+    "KINGetGasReactionRates": (ct.c_int, [_I, _D, _D, _DC, _DC, _DC]),                              # :491
+    "KINGetReactionRateParameters": (ct.c_int, [_I, _DC, _DC, _DC]),                                # :500
+    "KINSetAFactorForAReaction": (ct.c_int, [_I, _I, _D]),                                          # :507
+    "KINCalculateEquil": (ct.c_int, [_I, _D, _D, _DC, _DC]),                                        # :514
+    "KINCalculateEquilWithOption": (ct.c_int, [_I, _I, _D, _D, _DC, _DC]),                          # :522
+    "KINCalculateEqGasWithOption": (ct.c_int, [_I, _I, _I, _D, _D, _DC, _D, _D, _D, _D, _DC]),      # :531
+    "KINRealGas_SetParameter": (ct.c_int, [_C, _D]),                                                # :546
+    "KINRealGas_GetEOSMode": (ct.c_int, [_I, _I, _C]),                                              # :551
+    "KINRealGas_SetMixingRule": (ct.c_int, [_I, _I, _I]),                                           # :557
+    "KINRealGas_UseIdealGasLaw": (ct.c_int, [_I, _I]),                                              # :563
+    "KINRealGas_UseCubicEOS": (ct.c_int, [_I, _I]),                                                 # :568
+    "KINRealGas_SetCurrentPressure": (ct.c_int, [_I, _D]),                                          # :573
+    "KINRealGas_CheckRealGasStatus": (ct.c_int, [_I, _I]),                                          # :578
+    "KINGetGamma": (ct.c_int, [_I, _D, _DC, _D]),                                                   # :583
+    "KINAll0D_Setup": (ct.c_int, [_I, _I, _I, _I, _I, _I, _IC, _I]),                                # :591
+    "KINAll0D_SetupWorkArrays": (ct.c_int, [_I, _I]),                                               # :602
+    "KINAll0D_SetupBatchInputs": (ct.c_int, [_I, _D, _D, _D, _D, _D, _D, _DC, _DC, _DC]),           # :607
+    "KINAll0D_SetupPSRReactorInputs": (ct.c_int, [_I, _I, _D, _D, _D, _D, _D, _D, _D, _DC, _DC, _DC]),# :620
+    "KINAll0D_SetupPSRInletInputs": (ct.c_int, [_I, _I, _I, _D, _D, _DC]),                          # :635
+    "KINAll0D_SetupPFRInputs": (ct.c_int, [_I, _D, _D, _D, _D, _D, _D, _DC, _DC, _D, _DC]),         # :644
+    "KINAll0D_SetupHCCIInputs": (ct.c_int, [_I, _D, _D, _D, _D, _D, _D, _D, _D, _D, _D, _DC]),      # :658
+    "KINAll0D_SetupHCCIZoneInputs": (ct.c_int, [_I, _I, _D, _D]),                                   # :673
+    "KINAll0D_SetupSIInputs": (ct.c_int, [_I, _D, _D, _D, _D, _D]),                                 # :680
+    "KINAll0D_Calculate": (ct.c_int, [_I]),                                                         # :689
+    "KINAll0D_CalculateInput": (ct.c_int, [_I, _I, _C, _I, _IC]),                                   # :691
+    "KINAll0D_SetUserKeyword": (ct.c_int, [_C]),                                                    # :699
+    "KINAll0D_IntegrateHeatRelease": (ct.c_int, []),                                                # :701
+    "KINAll0D_SetHeatTransfer": (ct.c_int, [_D, _D]),                                               # :703
+    "KINAll0D_SetHeatTransferArea": (ct.c_int, [_D]),                                               # :708
+    "KINAll0D_SetProfilePoints": (ct.c_int, [_I]),                                                  # :711
+    "KINAll0D_SetProfileParameter": (ct.c_int, [_C, _I, _DC, _DC]),                                 # :713
+    "KINAll0D_SetProfileKeyword": (ct.c_int, [_I, _I, _C, _I, _DC, _DC]),                           # :720
+    "KINAll0D_SetSolverInitialStepTime": (ct.c_int, [_D]),                                          # :730
+    "KINAll0D_SetSolverMaximumStepTime": (ct.c_int, [_D]),                                          # :732
+    "KINAll0D_SetSolverMaximumIteration": (ct.c_int, [_I]),                                         # :734
+    "KINAll0D_SetRelaxIteration": (ct.c_int, []),                                                   # :736
+    "KINAll0D_SetMinimumSpeciesBound": (ct.c_int, [_D]),                                            # :738
+    "KINAll0D_GetSolution": (ct.c_int, [_D, _D, _DC]),                                              # :741
+    "KINAll0D_GetSolnResponseSize": (ct.c_int, [_I, _I]),                                           # :747
+    "KINAll0D_GetGasSolnResponse": (ct.c_int, [_I, _I, _I, _DC, _DC, _DC, _DC, _DF]),               # :752
+    "KINAll0D_GetIgnitionDelay": (ct.c_int, [_D]),                                                  # :763
+    "KINAll0D_GetHeatRelease": (ct.c_int, [_D, _D]),                                                # :765
+    "KINAll0D_GetEngineHeatRelease": (ct.c_int, [_DC, _D, _D, _D, _D, _D]),                         # :770
+    "KINAll0D_GetExitMassFlowRate": (ct.c_int, [_D]),                                               # :779
+    "KINPremix_SetParameter": (ct.c_int, [_C, _D]),                                                 # :782
+    "KINPremix_CalculateFlame": (ct.c_int, [_I, _I, _D, _D, _DC, _D, _D]),                          # :787
+    "KINPremix_GetSolution": (ct.c_int, [_I, _I, _DC, _DC, _DF]),                                   # :797
+    "KINPremix_GetSolutionGridPoints": (ct.c_int, [_I]),                                            # :805
+    "KINPremix_GetFlameMassFlux": (ct.c_int, [_D]),                                                 # :809
+    "KINOppdif_SetInlet": (ct.c_int, [_C, _I, _D, _DC, _D, _I]),                                    # :818
+    "KINOppdif_SetParameter": (ct.c_int, [_C, _D]),                                                 # :826
+    "KINOppdif_CalculateFlame": (ct.c_int, [_I, _I, _D, _D]),                                       # :831
+    "KINOppdif_GetSolutionGridPoints": (ct.c_int, [_I]),                                            # :837
+    "KINOppdif_GetSolution": (ct.c_int, [_I, _I, _D, _D, ct.POINTER(_D)]),                          # :838
+    "KINOppdif_GetSolnSpeciesIntegratedROP": (ct.c_int, [_I, _I, _I, _I, ct.POINTER(_D)]),          # :847
+    "KINGetMassFractionFromMoleFraction": (ct.c_int, [_I, _DC, _DC]),                               # :856
+    "KINGetMoleFractionFromMassFraction": (ct.c_int, [_I, _DC, _DC]),                               # :863
 }
 
 _REG = {

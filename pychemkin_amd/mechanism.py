@@ -260,10 +260,7 @@ class Mechanism:
             elif section != "THERMO" and head in ("REACTIONS", "REAC"):
                 section = "REACTIONS"
                 for tok in up.split()[1:]:
-                    if tok in ("CAL/MOLE", "KCAL/MOLE", "JOULES/MOLE", "KJOULES/MOLE", "KELVINS", "EVOLTS"):
-                        e_units = tok
-                    elif tok in ("MOLES", "MOLECULES"):
-                        a_units = tok
+                    e_units, a_units = _unit_token(tok, e_units, a_units)  # other options ignored
                 continue
             if up == "END" or up.startswith("END "):
                 if section == "THERMO":
@@ -391,7 +388,7 @@ class Mechanism:
             if not k:
                 continue
             # FORD / RORD carry "species order"; every other keyword numbers only
-            nums = [_to_float(v) for v in vals.split()] if vals and k not in ("FORD", "RORD") else []
+            nums = [_to_float(v) for v in vals.split()] if vals and k not in ("FORD", "RORD", "UNITS") else []
             if k in ("DUP", "DUPLICATE"):
                 current.duplicate = True
             elif k == "LOW":
@@ -407,6 +404,8 @@ class Mechanism:
             elif k == "TROE":
                 current.troe = tuple(nums)
             elif k == "SRI":
+                if len(nums) not in (3, 5):
+                    raise MechanismError(f"SRI needs 3 or 5 parameters: {current.equation}")
                 current.sri = tuple(nums)
             elif k == "REV":
                 current.rev = tuple(nums[:3])
@@ -419,7 +418,21 @@ class Mechanism:
             elif k == "PLOG":
                 current.plog.append(tuple(nums[:4]))
             elif k == "UNITS":
-                pass
+                # per-reaction units: this reaction's A and E (and its LOW / HIGH / REV / PLOG
+                # parameters) are in them (Chemkin's UNITS auxiliary keyword, e.g. UNITS /KCAL/)
+                toks = vals.split() if vals else []
+                if not toks:
+                    raise MechanismError(f"UNITS needs /unit .../: {s!r}")
+                e_u = a_u = None
+                for t in toks:
+                    e2, a2 = _unit_token(t.upper(), None, None)
+                    if e2 is None and a2 is None:
+                        raise MechanismError(f"unknown UNITS {t!r} for {current.equation}")
+                    e_u, a_u = e2 or e_u, a2 or a_u
+                if e_u is not None:
+                    current.E_scale = _e_to_kelvin(e_u)
+                if a_u is not None:
+                    current.A_scale_per_order = 1.0 / AVOGADRO if a_u == "MOLECULES" else 1.0
             else:
                 names = self._species_index_upper()
                 if k in names:
@@ -617,6 +630,21 @@ class Mechanism:
             plog_ptr=plog_ptr,
             plog_par=np.asarray(plog_par if plog_par else [(0.0, 0.0, 0.0, 0.0)], np.float64).reshape(-1, 4),
         )
+
+
+def _unit_token(tok: str, e_units, a_units):
+    """A REACTIONS-line unit keyword or a UNITS abbreviation (MOLE, MOLC, CAL, KCAL, JOUL, KJOU,
+    KELV, EVOL) -> updated (e_units, a_units); anything else leaves both unchanged."""
+    t = tok.upper()
+    if t.startswith(("MOLEC", "MOLC")):
+        return e_units, "MOLECULES"
+    if t.startswith("MOLE"):
+        return e_units, "MOLES"
+    for pre, name in (("KCAL", "KCAL/MOLE"), ("CAL", "CAL/MOLE"), ("KJOU", "KJOULES/MOLE"), ("JOUL", "JOULES/MOLE"),
+                      ("KELV", "KELVINS"), ("EVOL", "EVOLTS")):
+        if t.startswith(pre):
+            return name, a_units
+    return e_units, a_units
 
 
 def _e_to_kelvin(units: str) -> float:

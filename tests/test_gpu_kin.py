@@ -268,3 +268,99 @@ def test_qpro_with_aext_through_kin_calls(K, mech, oracle):
         assert (abs(tau.value / ref.tau - 1) < 1e-4) if ref.tau > 0 else tau.value == ref.tau, order
         t, T, P, V, Y = _solution(L, mech.KK)
         assert abs(T[-1] / ref.T - 1) < 1e-5, order
+
+
+def _preprocess(L, chem, therm, summary=""):
+    """chemistry.py:675-687: KINPreProcess with the reference's argument list (isurf, itran, 8 file
+    names, chemset)."""
+    cs = ct.c_int(0)
+    z = ct.c_int(0)
+    names = [chem, "", therm, "", "chem.asc", "surf.asc", "tran.asc", summary]
+    rc = L.KINPreProcess(ct.byref(z), ct.byref(z), *[ct.c_char_p(x.encode()) for x in names], ct.byref(cs))
+    return rc, cs
+
+
+def test_preprocess_then_h2_golden_through_kin_calls_only(mech, tmp_path):
+    """File paths -> KINPreProcess (native interpreter) -> KINGetChemistrySizes / names / weights
+    (chemistry.py:693-1064) -> the closed_homogeneous__transient golden on all five columns, through
+    KIN calls alone -- no Python parser, no ckmi_kin_register."""
+    from conftest import CHEM, THERM
+    from pychemkin_amd import kin
+
+    L = kin.bind()
+    summary = str(tmp_path / "Summary.out")
+    rc, cs = _preprocess(L, CHEM, THERM, summary)
+    assert rc == 0, kin.last_error()
+    s = [ct.c_int(-1) for _ in range(8)]
+    assert L.KINGetChemistrySizes(ct.byref(cs), *[ct.byref(x) for x in s]) == 0
+    assert [s[0].value, s[1].value, s[2].value] == [5, 53, 325]
+    buf = (ct.POINTER(ct.c_char) * 53)()
+    for i in range(53):
+        buf[i] = ct.create_string_buffer(17)
+    assert L.KINGetGasSpeciesNames(ct.byref(cs), ct.cast(buf, ct.POINTER(ct.POINTER(ct.c_char)))) == 0
+    names = [ct.cast(buf[i], ct.c_char_p).value.decode() for i in range(53)]
+    assert names == mech.species
+    wt = np.zeros(53)
+    assert L.KINGetGasMolecularWeights(ct.byref(cs), wt) == 0 and np.array_equal(wt, mech.wt)
+    mode, eos = ct.c_int(-1), ct.create_string_buffer(17)
+    assert L.KINRealGas_GetEOSMode(ct.byref(cs), ct.byref(mode), eos) == 0 and mode.value == 0
+    assert L.KINRealGas_CheckRealGasStatus(ct.byref(cs), ct.byref(mode)) == 0 and mode.value == 0
+    n = ct.c_int(0)
+    rs = ct.create_string_buffer(b" " * 1024)
+    assert L.KINGetGasReactionString(ct.byref(cs), ct.byref(ct.c_int(38)), ct.byref(n), rs) == 0
+    assert rs.raw[:n.value].decode() == "H+O2<=>O+OH"
+    assert "H+O2<=>O+OH" in open(summary).read()
+    g = golden("closed_homogeneous__transient")
+    _setup(L, cs, 1, 1, 5e-4, 1000.0, P_ATM, 1.0, h2_air_Y(mech))
+    for line in ("ATOL    1e-20", "RTOL    1e-08", "NNEG", "DTSV    5e-06", "DTIGN    400", "NADAP"):
+        assert L.KINAll0D_SetUserKeyword(line.encode()) == 0, line
+    assert L.KINAll0D_Calculate(ct.byref(cs)) == 0, kin.last_error()
+    t, T, P, V, Y = _solution(L, mech.KK)
+    k = mech.species.index("H2O")
+    wdot = np.zeros(mech.KK)
+    rop = np.zeros(len(t))
+    for i in range(len(t)):
+        assert L.KINGetGasROP(ct.byref(cs), ct.byref(ct.c_double(T[i])), ct.byref(ct.c_double(P[i])),
+                              np.ascontiguousarray(Y[:, i]), wdot) == 0
+        rop[i] = wdot[k]
+    check_h2_golden(g, mech, t, T, Y.T, rop, min_ok=99)
+    kin.release(cs.value)
+
+
+def test_full_keyword_mode_calculate_input(K, mech):
+    """KINAll0D_CalculateInput (chemkin_wrapper.py:690-697): the keyword block the reference builds
+    in full-keyword mode (batchreactor.py:822-978: TRAN, CONP, ENRG, PRES [atm], TEMP, TIME, REAC
+    lines, solver keywords, QRGEQ, END) gives the same run as API mode -- the H2 golden case."""
+    L, cs = K
+    g = golden("closed_homogeneous__transient")
+    Y0 = h2_air_Y(mech)
+    _setup(L, cs, 1, 1, 5e-4, 1000.0, P_ATM, 1.0, Y0)
+    X0 = (Y0 / mech.wt) / np.sum(Y0 / mech.wt)
+    lines = ["TRAN", "CONP", "ENRG", "PRES    1.0", "TEMP    1000.0", "TIME    0.0005"]
+    lines += [f"REAC    {mech.species[k]}    {X0[k]!r}" for k in range(mech.KK) if X0[k] > 1e-12]
+    lines += ["ATOL    1e-20", "RTOL    1e-08", "NNEG", "DTSV    5e-06", "DTIGN    400", "NADAP", "QRGEQ", "END"]
+    blob = "".join(lines).encode()
+    lens = np.array([len(x) for x in lines], np.int32)
+    assert L.KINAll0D_CalculateInput(ct.byref(ct.c_int(154)), ct.byref(cs), blob, ct.byref(ct.c_int(len(lines))),
+                                     lens) == 0, L.ckmi_kin_last_error()
+    t, T, P, V, Y = _solution(L, mech.KK)
+    tau_full = ct.c_double(0.0)
+    assert L.KINAll0D_GetIgnitionDelay(ct.byref(tau_full)) == 0
+    Tg = np.asarray(g["state-temperature"])
+    assert t.tolist() == g["state-time"]
+    assert within(T, Tg, *g["tolerance-var"]).sum() >= 99
+    # API mode on the same inputs: the same numbers
+    _setup(L, cs, 1, 1, 5e-4, 1000.0, P_ATM, 1.0, Y0)
+    for line in ("ATOL    1e-20", "RTOL    1e-08", "NNEG", "DTSV    5e-06", "DTIGN    400", "NADAP"):
+        assert L.KINAll0D_SetUserKeyword(line.encode()) == 0
+    assert L.KINAll0D_Calculate(ct.byref(cs)) == 0
+    t2, T2, P2, V2, Y2 = _solution(L, mech.KK)
+    assert np.allclose(T2, T, rtol=1e-9, atol=0)  # REAC mole fractions -> Y: last-bit differences only
+    tau = ct.c_double(0.0)
+    assert L.KINAll0D_GetIgnitionDelay(ct.byref(tau)) == 0 and abs(tau.value / tau_full.value - 1) < 1e-9
+    # an unknown keyword in the block is rejected with a message
+    _setup(L, cs, 1, 1, 5e-4, 1000.0, P_ATM, 1.0, Y0)
+    bad = ["TRAN", "CONP", "ENRG", "FROB    3", "END"]
+    assert L.KINAll0D_CalculateInput(ct.byref(ct.c_int(154)), ct.byref(cs), "".join(bad).encode(),
+                                     ct.byref(ct.c_int(len(bad))), np.array([len(x) for x in bad], np.int32)) != 0
+    assert b"FROB" in L.ckmi_kin_last_error()

@@ -125,3 +125,26 @@ def test_jit_unavailable_for_plog_mechanism(jit_path):
     _native.set_rop_path(0)
     w = dm.rop_thermo(T, P, Y)[0].cpu().numpy()
     assert np.all(np.isfinite(w))
+
+
+@pytest.mark.skipif(not (__import__("torch").cuda.is_available() and __import__("torch").cuda.device_count() >= 2),
+                    reason="needs two GPUs")
+def test_jit_module_loads_on_the_mechanism_device(tables, oracle, mech):
+    """A mechanism on GPU 1 driven while GPU 0 is current, with a batch large enough for the
+    specialised kernel: jit_ready loads the hipRTC module on the mechanism's device (ckmi.hip
+    DeviceScope) and the launch runs there, and the caller's current device is left as it was."""
+    import torch
+
+    from pychemkin_amd import _native
+
+    torch.cuda.set_device(0)
+    dm = _native.DeviceMechanism(tables, device=1)
+    n = 20000
+    T, P, Y = _states(mech.KK, n, seed=5)
+    w = dm.rop_thermo(T, P, Y)[0]
+    assert w.device.index == 1 and torch.cuda.current_device() == 0
+    assert _jit_state(dm) == 1
+    wo = oracle.rop_batch(T[:64], P[:64], Y[:, :64].copy())[0]
+    err = np.max(np.abs(w.cpu().numpy()[:, :64] - wo) / np.max(np.abs(wo), axis=0, keepdims=True))
+    assert err < 1e-11
+    dm.close()

@@ -20,38 +20,92 @@ IC = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
 IF = np.ctypeslib.ndpointer(dtype=np.int32, flags="F_CONTIGUOUS")
 
 REFERENCE_ARGTYPES = {
-    "KINSetUnitSystem": [I],                                    # chemkin_wrapper.py:300-301
-    "KINInitialize": [I, I],                                    # :317-321
-    "KINFinish": [],                                            # :322-323
-    "KINUpdateChemistrySet": [I],                               # :324-327
-    "KINSwitchChemistrySet": [I],                               # :328-331
-    "KINGetChemistrySizes": [I] * 9,                            # :333-344
-    "KINGetGasSpeciesNames": [I, ct.POINTER(C)],                # :345-349
-    "KINGetElementNames": [I, ct.POINTER(C)],                   # :350-354
-    "KINGetAtomicWeights": [I, DC],                             # :355-359
-    "KINGetGasMolecularWeights": [I, DC],                       # :360-364
-    "KINGetGasSpecificHeat": [I, D, DC],                        # :375-380
-    "KINGetGasSpeciesEnthalpy": [I, D, DC],                     # :381-386
-    "KINGetGasSpeciesInternalEnergy": [I, D, DC],               # :387-392
-    "KINGetGasSpeciesComposition": [I, IF],                     # :393-397
-    "KINGetMassDensity": [I, D, D, DC, D],                      # :398-405
-    "KINGetGasMixtureSpecificHeat": [I, D, DC, D],              # :427-433
-    "KINGetGasMixtureEnthalpy": [I, D, DC, D],                  # :434-440
-    "KINGetGasROP": [I, D, D, DC, DC],                          # :482-489
-    "KINGetGasReactionRates": [I, D, D, DC, DC, DC],            # :490-498
-    "KINGetReactionRateParameters": [I, DC, DC, DC],            # :499-505
-    "KINSetAFactorForAReaction": [I, I, D],                     # :506-511
-    "KINAll0D_Setup": [I, I, I, I, I, I, IC, I],                # :590-600
-    "KINAll0D_SetupWorkArrays": [I, I],                         # :601-605
-    "KINAll0D_SetupBatchInputs": [I, D, D, D, D, D, D, DC, DC, DC],  # :606-618
-    "KINAll0D_Calculate": [I],                                  # :688-689
-    "KINAll0D_SetUserKeyword": [C],                             # :698-699
-    "KINAll0D_IntegrateHeatRelease": [],                        # :700-701
-    "KINAll0D_SetProfilePoints": [I],                           # :710-711
-    "KINAll0D_SetProfileParameter": [C, I, DC, DC],             # :712-718
-    "KINAll0D_GetSolnResponseSize": [I, I],                     # :746-750
-    "KINAll0D_GetGasSolnResponse": [I, I, I, DC, DC, DC, DC, DF],  # :751-761
-    "KINAll0D_GetIgnitionDelay": [D],                           # :762-763
+    "KINSetUnitSystem": [I],                                                  # chemkin_wrapper.py:301
+    "KINPreProcess": [I, I, C, C, C, C, C, C, C, C, I],                       # chemkin_wrapper.py:304
+    "KINInitialize": [I, I],                                                  # chemkin_wrapper.py:318
+    "KINFinish": [],                                                          # chemkin_wrapper.py:323
+    "KINUpdateChemistrySet": [I],                                             # chemkin_wrapper.py:325
+    "KINSwitchChemistrySet": [I],                                             # chemkin_wrapper.py:329
+    "KINGetChemistrySizes": [I, I, I, I, I, I, I, I, I],                      # chemkin_wrapper.py:334
+    "KINGetGasSpeciesNames": [I, ct.POINTER(C)],                              # chemkin_wrapper.py:346
+    "KINGetElementNames": [I, ct.POINTER(C)],                                 # chemkin_wrapper.py:351
+    "KINGetAtomicWeights": [I, DC],                                           # chemkin_wrapper.py:356
+    "KINGetGasMolecularWeights": [I, DC],                                     # chemkin_wrapper.py:361
+    "KINGetGasReactionString": [I, I, I, C],                                  # chemkin_wrapper.py:366
+    "KINGetReactionStringLength": [I],                                        # chemkin_wrapper.py:373
+    "KINGetGasSpecificHeat": [I, D, DC],                                      # chemkin_wrapper.py:376
+    "KINGetGasSpeciesEnthalpy": [I, D, DC],                                   # chemkin_wrapper.py:382
+    "KINGetGasSpeciesInternalEnergy": [I, D, DC],                             # chemkin_wrapper.py:388
+    "KINGetGasSpeciesComposition": [I, IF],                                   # chemkin_wrapper.py:394
+    "KINGetMassDensity": [I, D, D, DC, D],                                    # chemkin_wrapper.py:399
+    "KINGetViscosity": [I, D, DC],                                            # chemkin_wrapper.py:408
+    "KINGetConductivity": [I, D, DC],                                         # chemkin_wrapper.py:414
+    "KINGetDiffusionCoeffs": [I, D, D, DF],                                   # chemkin_wrapper.py:420
+    "KINGetGasMixtureSpecificHeat": [I, D, DC, D],                            # chemkin_wrapper.py:428
+    "KINGetGasMixtureEnthalpy": [I, D, DC, D],                                # chemkin_wrapper.py:435
+    "KINGetMixtureViscosity": [I, D, DC, D],                                  # chemkin_wrapper.py:443
+    "KINGetMixtureConductivity": [I, D, DC, D],                               # chemkin_wrapper.py:450
+    "KINGetMixtureDiffusionCoeffs": [I, D, D, DC, DC],                        # chemkin_wrapper.py:457
+    "KINGetOrdinaryDiffusionCoeffs": [I, D, D, DC, DF],                       # chemkin_wrapper.py:465
+    "KINGetThermalDiffusionCoeffs": [I, D, D, DC, DC, D],                     # chemkin_wrapper.py:473
+    "KINGetGasROP": [I, D, D, DC, DC],                                        # chemkin_wrapper.py:483
+    "KINGetGasReactionRates": [I, D, D, DC, DC, DC],                          # chemkin_wrapper.py:491
+    "KINGetReactionRateParameters": [I, DC, DC, DC],                          # chemkin_wrapper.py:500
+    "KINSetAFactorForAReaction": [I, I, D],                                   # chemkin_wrapper.py:507
+    "KINCalculateEquil": [I, D, D, DC, DC],                                   # chemkin_wrapper.py:514
+    "KINCalculateEquilWithOption": [I, I, D, D, DC, DC],                      # chemkin_wrapper.py:522
+    "KINCalculateEqGasWithOption": [I, I, I, D, D, DC, D, D, D, D, DC],       # chemkin_wrapper.py:531
+    "KINRealGas_SetParameter": [C, D],                                        # chemkin_wrapper.py:546
+    "KINRealGas_GetEOSMode": [I, I, C],                                       # chemkin_wrapper.py:551
+    "KINRealGas_SetMixingRule": [I, I, I],                                    # chemkin_wrapper.py:557
+    "KINRealGas_UseIdealGasLaw": [I, I],                                      # chemkin_wrapper.py:563
+    "KINRealGas_UseCubicEOS": [I, I],                                         # chemkin_wrapper.py:568
+    "KINRealGas_SetCurrentPressure": [I, D],                                  # chemkin_wrapper.py:573
+    "KINRealGas_CheckRealGasStatus": [I, I],                                  # chemkin_wrapper.py:578
+    "KINGetGamma": [I, D, DC, D],                                             # chemkin_wrapper.py:583
+    "KINAll0D_Setup": [I, I, I, I, I, I, IC, I],                              # chemkin_wrapper.py:591
+    "KINAll0D_SetupWorkArrays": [I, I],                                       # chemkin_wrapper.py:602
+    "KINAll0D_SetupBatchInputs": [I, D, D, D, D, D, D, DC, DC, DC],           # chemkin_wrapper.py:607
+    "KINAll0D_SetupPSRReactorInputs": [I, I, D, D, D, D, D, D, D, DC, DC, DC],# chemkin_wrapper.py:620
+    "KINAll0D_SetupPSRInletInputs": [I, I, I, D, D, DC],                      # chemkin_wrapper.py:635
+    "KINAll0D_SetupPFRInputs": [I, D, D, D, D, D, D, DC, DC, D, DC],          # chemkin_wrapper.py:644
+    "KINAll0D_SetupHCCIInputs": [I, D, D, D, D, D, D, D, D, D, D, DC],        # chemkin_wrapper.py:658
+    "KINAll0D_SetupHCCIZoneInputs": [I, I, D, D],                             # chemkin_wrapper.py:673
+    "KINAll0D_SetupSIInputs": [I, D, D, D, D, D],                             # chemkin_wrapper.py:680
+    "KINAll0D_Calculate": [I],                                                # chemkin_wrapper.py:689
+    "KINAll0D_CalculateInput": [I, I, C, I, IC],                              # chemkin_wrapper.py:691
+    "KINAll0D_SetUserKeyword": [C],                                           # chemkin_wrapper.py:699
+    "KINAll0D_IntegrateHeatRelease": [],                                      # chemkin_wrapper.py:701
+    "KINAll0D_SetHeatTransfer": [D, D],                                       # chemkin_wrapper.py:703
+    "KINAll0D_SetHeatTransferArea": [D],                                      # chemkin_wrapper.py:708
+    "KINAll0D_SetProfilePoints": [I],                                         # chemkin_wrapper.py:711
+    "KINAll0D_SetProfileParameter": [C, I, DC, DC],                           # chemkin_wrapper.py:713
+    "KINAll0D_SetProfileKeyword": [I, I, C, I, DC, DC],                       # chemkin_wrapper.py:720
+    "KINAll0D_SetSolverInitialStepTime": [D],                                 # chemkin_wrapper.py:730
+    "KINAll0D_SetSolverMaximumStepTime": [D],                                 # chemkin_wrapper.py:732
+    "KINAll0D_SetSolverMaximumIteration": [I],                                # chemkin_wrapper.py:734
+    "KINAll0D_SetRelaxIteration": [],                                         # chemkin_wrapper.py:736
+    "KINAll0D_SetMinimumSpeciesBound": [D],                                   # chemkin_wrapper.py:738
+    "KINAll0D_GetSolution": [D, D, DC],                                       # chemkin_wrapper.py:741
+    "KINAll0D_GetSolnResponseSize": [I, I],                                   # chemkin_wrapper.py:747
+    "KINAll0D_GetGasSolnResponse": [I, I, I, DC, DC, DC, DC, DF],             # chemkin_wrapper.py:752
+    "KINAll0D_GetIgnitionDelay": [D],                                         # chemkin_wrapper.py:763
+    "KINAll0D_GetHeatRelease": [D, D],                                        # chemkin_wrapper.py:765
+    "KINAll0D_GetEngineHeatRelease": [DC, D, D, D, D, D],                     # chemkin_wrapper.py:770
+    "KINAll0D_GetExitMassFlowRate": [D],                                      # chemkin_wrapper.py:779
+    "KINPremix_SetParameter": [C, D],                                         # chemkin_wrapper.py:782
+    "KINPremix_CalculateFlame": [I, I, D, D, DC, D, D],                       # chemkin_wrapper.py:787
+    "KINPremix_GetSolution": [I, I, DC, DC, DF],                              # chemkin_wrapper.py:797
+    "KINPremix_GetSolutionGridPoints": [I],                                   # chemkin_wrapper.py:805
+    "KINPremix_GetFlameMassFlux": [D],                                        # chemkin_wrapper.py:809
+    "KINOppdif_SetInlet": [C, I, D, DC, D, I],                                # chemkin_wrapper.py:818
+    "KINOppdif_SetParameter": [C, D],                                         # chemkin_wrapper.py:826
+    "KINOppdif_CalculateFlame": [I, I, D, D],                                 # chemkin_wrapper.py:831
+    "KINOppdif_GetSolutionGridPoints": [I],                                   # chemkin_wrapper.py:837
+    "KINOppdif_GetSolution": [I, I, D, D, ct.POINTER(D)],                     # chemkin_wrapper.py:838
+    "KINOppdif_GetSolnSpeciesIntegratedROP": [I, I, I, I, ct.POINTER(D)],     # chemkin_wrapper.py:847
+    "KINGetMassFractionFromMoleFraction": [I, DC, DC],                        # chemkin_wrapper.py:856
+    "KINGetMoleFractionFromMassFraction": [I, DC, DC],                        # chemkin_wrapper.py:863
 }
 
 

@@ -1,0 +1,164 @@
+"""The native Chemkin interpreter in libckmi.so (ckmi_parse.cpp, the parse half of KINPreProcess,
+chemkin_wrapper.py:303-316) against the package's Python interpreter (pychemkin_amd/mechanism.py).
+
+Host-only calls, no GPU: every table of every mechanism under data/ must come out bitwise equal, the
+symbols / weights / element counts and reaction strings identical, and both must reject the same
+malformed inputs."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+DATA = os.path.join(ROOT, "data")
+MECHS = [("grimech30_chem.inp", "grimech30_thermo.dat"), ("gri30_ford_chem.inp", "grimech30_thermo.dat"),
+         ("gri30_plog_chem.inp", "grimech30_thermo.dat"), ("gri30_tracer161_chem.inp", "gri30_tracer161_thermo.dat")]
+
+
+def _read(name):
+    with open(os.path.join(DATA, name)) as f:
+        return f.read()
+
+
+def _both(chem, therm):
+    from pychemkin_amd import _native
+    from pychemkin_amd.mechanism import Mechanism
+
+    m = Mechanism(chem, therm)
+    return m, _native.parse_mechanism(chem, therm)
+
+
+def _assert_same(m, native):
+    t_py = m.to_tables()
+    t, species, elements, awt, ncf, eqs = native
+    assert species == m.species and elements == m.elements
+    assert np.array_equal(awt, np.asarray(m.awt)) and np.array_equal(ncf, m.ncf)
+    assert eqs == [rx.equation for rx in m.reactions]
+    assert set(t) == set(t_py)
+    for k, v in t_py.items():
+        a = np.asarray(t[k])
+        assert a.dtype == np.asarray(v).dtype, k
+        assert np.array_equal(a, np.asarray(v)), k  # bitwise: same parse, same arithmetic
+
+
+@pytest.mark.parametrize("chem,therm", MECHS)
+def test_native_parser_matches_python_tables(chem, therm):
+    m, native = _both(_read(chem), _read(therm))
+    _assert_same(m, native)
+
+
+MINI = """ELEMENTS H O N AR END
+SPECIES H2 H O O2 OH H2O HO2 N2 AR END
+REACTIONS
+H+O2<=>O+OH                              2.650E+16    -.6707  17041.00
+O+H2<=>H+OH                              3.870E+04    2.700    6260.00
+H+O2(+M)<=>HO2(+M)                       4.650E+12    0.440       0.0
+     LOW  /  1.737E+19   -1.230   0.0/
+     TROE/   0.67  1.0E-30  1.0E+30  1.0E+30 /
+H2/1.3/ H2O/10.0/ AR/0.67/
+2OH<=>O+H2O                              3.570E+04    2.400   -2110.00
+H+OH+M<=>H2O+M                           2.200E+22   -2.000        .00
+H2/ .73/ H2O/3.65/ AR/ .38/
+END
+"""
+
+
+def _thermo_text():
+    return _read("grimech30_thermo.dat")
+
+
+def test_per_reaction_units_are_honoured():
+    """Chemkin's UNITS auxiliary keyword: this reaction's A and E (and its LOW) in the given units.
+    Round 2 parsed UNITS and dropped it (A and E silently wrong)."""
+    from pychemkin_amd.mechanism import AVOGADRO, Mechanism
+
+    base = MINI
+    alt = MINI.replace("O+H2<=>H+OH                              3.870E+04    2.700    6260.00",
+                       "O+H2<=>H+OH                              3.870E+04    2.700    6.26\n UNITS /KCAL/")
+    alt = alt.replace("2OH<=>O+H2O                              3.570E+04    2.400   -2110.00",
+                      "2OH<=>O+H2O                              %.17g    2.400   -2110.00\n UNITS /MOLC/"
+                      % (3.57e4 / AVOGADRO))
+    th = _thermo_text()
+    m0, m1 = Mechanism(base, th), Mechanism(alt, th)
+    for m in (m0, m1):  # both parsers, both files
+        from pychemkin_amd import _native
+        _assert_same(m, _native.parse_mechanism(base if m is m0 else alt, th))
+    a0, a1 = m0.to_tables()["arr"], m1.to_tables()["arr"]
+    assert np.allclose(a1, a0, rtol=1e-14, atol=0)
+    assert not np.array_equal(m1.reactions[1].E_scale, m0.reactions[1].E_scale)
+
+
+def test_reactions_line_units_and_abbreviations():
+    from pychemkin_amd.mechanism import Mechanism
+
+    th = _thermo_text()
+    k = Mechanism(MINI.replace("REACTIONS", "REACTIONS KELVINS"), th)
+    c = Mechanism(MINI, th)
+    assert abs(k.to_tables()["arr"][0, 2] - 17041.0) == 0.0
+    assert abs(c.to_tables()["arr"][0, 2] / (17041.0 / (8.314510e7 / 4.184e7)) - 1) < 1e-15
+    j = Mechanism(MINI.replace("REACTIONS", "REACTIONS KJOULES/MOLE"), th)
+    assert abs(j.to_tables()["arr"][0, 2] / (17041.0e3 / 8.314510) - 1) < 1e-15
+    from pychemkin_amd import _native
+
+    for text in (MINI.replace("REACTIONS", "REACTIONS KELVINS"), MINI.replace("REACTIONS", "REACTIONS KJOU MOLC")):
+        _assert_same(Mechanism(text, th), _native.parse_mechanism(text, th))
+
+
+BAD = {
+    "unknown species": MINI.replace("O+H2<=>H+OH", "O+H3<=>H+OH"),
+    "not element balanced": MINI.replace("O+H2<=>H+OH", "O+H2<=>H+H2O"),
+    "unknown auxiliary keyword": MINI.replace("H2/ .73/", "CHEB/ 7 3 /\nH2/ .73/"),
+    "UNITS": MINI.replace("H2/ .73/", "UNITS /FURLONGS/\nH2/ .73/"),
+    "efficiency on a reaction without": MINI.replace("O+H2<=>H+OH                              3.870E+04    2.700    6260.00",
+                                                     "O+H2<=>H+OH                              3.870E+04    2.700    6260.00\nH2O/2.0/"),
+    "LOW on a non-falloff": MINI.replace("H2/ .73/", "LOW / 1 0 0 /\nH2/ .73/"),
+    "no thermo data": MINI.replace("AR END", "AR XYZ END"),
+}
+
+
+@pytest.mark.parametrize("what", list(BAD))
+def test_both_parsers_reject_malformed_input(what):
+    from pychemkin_amd import _native
+    from pychemkin_amd.mechanism import Mechanism, MechanismError
+
+    text = BAD[what]
+    with pytest.raises(MechanismError):
+        Mechanism(text, _thermo_text())
+    with pytest.raises(_native.NativeError):
+        _native.parse_mechanism(text, _thermo_text())
+
+
+def test_more_than_four_species_per_side_is_rejected_loudly():
+    from pychemkin_amd import _native
+    from pychemkin_amd.mechanism import Mechanism, MechanismError
+
+    text = MINI.replace("END\nREACTIONS", "END\nREACTIONS\nH2+O2+OH+H+O<=>2H2O+O2          1.0E+10 0.0 0.0", 1)
+    with pytest.raises(MechanismError, match="more than 4"):
+        Mechanism(text, _thermo_text()).to_tables()
+    with pytest.raises(_native.NativeError, match="more than 4"):
+        _native.parse_mechanism(text, _thermo_text())
+
+
+def test_kin_preprocess_reports_parse_errors_without_a_gpu(tmp_path):
+    """KINPreProcess with the reference's argument list: a malformed file fails in the host parser
+    with a non-zero code and the interpreter's message (no device call is reached)."""
+    import ctypes as ct
+
+    from pychemkin_amd import kin
+
+    L = kin.bind()
+    chem = tmp_path / "bad.inp"
+    chem.write_text(BAD["unknown species"])
+    therm = os.path.join(DATA, "grimech30_thermo.dat")
+    cs = ct.c_int(0)
+    z = ct.c_int(0)
+    args = [ct.c_char_p(x.encode()) for x in (str(chem), "", therm, "", "chem.asc", "surf.asc", "tran.asc",
+                                                 str(tmp_path / "Summary.out"))]
+    rc = L.KINPreProcess(ct.byref(z), ct.byref(z), args[0], args[1], args[2], args[3], args[4], args[5], args[6],
+                         args[7], ct.byref(cs))
+    assert rc != 0
+    assert "unknown species" in kin.last_error()
+    one = ct.c_int(1)
+    rc = L.KINPreProcess(ct.byref(one), ct.byref(z), *args, ct.byref(cs))
+    assert rc != 0 and "surface" in kin.last_error()
