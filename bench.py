@@ -22,12 +22,20 @@ CPU baseline: the oracle C restatement (OpenMP) timed on a bounded sample of the
 this host.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu]
+
+Launch: under torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one
+rank.  Run directly with --gpus N > 1, bench.py is its own launcher: it starts N child processes
+(one GPU each, same arguments, MASTER_ADDR 127.0.0.1) before anything touches a GPU, forwards
+rank 0's JSON line and exits with the worst child status; N above the visible devices is an error.
+--plan prints the shard layout and the max-over-ranks timing path without a GPU (gloo).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -103,6 +111,14 @@ def ch4_air_Y(mech, phi, tracer=0.0):
     X /= X.sum(axis=1, keepdims=True)
     Y = X * mech.wt
     return Y / Y.sum(axis=1, keepdims=True)
+
+
+def sweep_index(world, rank, nT=64, nphi=32, nP=32):
+    """Global reactor indices (iT, iphi, iP flattened over the 64*world x 32 x 32 sweep) of rank's
+    shard, in the order sweep() lays them out."""
+    iT = np.arange(nT * world)[rank::world]
+    I, F, Q = np.meshgrid(iT, np.arange(nphi), np.arange(nP), indexing="ij")
+    return (I.ravel() * nphi + F.ravel()) * nP + Q.ravel()
 
 
 def sweep(mech, world, rank, nT=64, nphi=32, nP=32):
@@ -362,9 +378,72 @@ def secondary_sweep(name, dm, dev, mech, ops, sweep_fn, world, rank, args, kerne
     return line
 
 
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, visible=None):
+    """bench.py --gpus N run directly: start N rank processes (children, never exec) on one node and
+    return (worst exit status, rank 0's stdout).  Called before anything initialises a GPU
+    (torch.cuda.device_count() does not); N must not exceed the visible devices."""
+    if visible is not None and n > visible:
+        raise SystemExit(f"bench.py: --gpus {n} but only {visible} GPU(s) are visible")
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = procs[0].communicate()[0].decode()
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    return max(rcs, key=abs), out0
+
+
+def plan(world, rank):
+    """--plan: the sharding and the timing protocol of a run without a GPU (gloo): every rank builds
+    its shard of the headline sweep, 'runs' for a rank-dependent time between the same barriers, and
+    rank 0 reports the shard sizes, whether the shards are disjoint and complete, and the
+    max-over-ranks time that value would be computed from."""
+    if world > 1:
+        dist.init_process_group(backend="gloo", init_method="env://")
+    idx = torch.as_tensor(sweep_index(world, rank))
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.05 * (rank + 1))
+    if world > 1:
+        dist.barrier()
+    elapsed = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    mine = elapsed.clone()
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        sizes = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([idx.numel()]))
+        allidx = [torch.zeros(int(k.item()), dtype=idx.dtype) for k in sizes]
+        dist.all_gather(allidx, idx)
+        times = [torch.zeros(1, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(times, mine)
+    else:
+        allidx, times = [idx], [mine]
+    if rank == 0:
+        cat = torch.cat(allidx)
+        total = 65536 * world
+        print(json.dumps({"plan": True, "n_ranks": world, "shard_sizes": [int(a.numel()) for a in allidx],
+                          "disjoint": int(torch.unique(cat).numel()) == int(cat.numel()),
+                          "complete": int(torch.unique(cat).numel()) == total and int(cat.min()) == 0
+                          and int(cat.max()) == total - 1,
+                          "rank_seconds": [float(t.item()) for t in times], "max_seconds": float(elapsed.item())}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs of this node (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reactors", type=int, default=0, help="override the headline reactors per GPU (0 = full 65,536)")
@@ -377,12 +456,24 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=16384, help="max reactors in a CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget of the headline")
     ap.add_argument("--cpu-seconds-secondary", type=float, default=6.0, help="CPU-baseline budget of c4 / c5")
+    ap.add_argument("--plan", action="store_true", help="print the shard layout / timing protocol (no GPU)")
     args = ap.parse_args()
     lines = set(args.lines.split(","))
 
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:  # be the launcher (no GPU touched yet)
+        visible = None if args.plan else torch.cuda.device_count()
+        rc, out0 = launch_ranks(args.gpus, sys.argv[1:], visible)
+        sys.stdout.write(out0)
+        sys.stdout.flush()
+        raise SystemExit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE is {world}")
+    if args.plan:
+        plan(world, rank)
+        return
     if world > 1:
         dist.init_process_group(backend="nccl", init_method="env://")
     torch.cuda.set_device(local)

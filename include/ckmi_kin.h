@@ -37,6 +37,9 @@ int ckmi_kin_register(const ckmi_mech_desc* desc, int32_t MM, const char* names,
                       const double* awt, const int32_t* ncf, int32_t* chemset);
 int ckmi_kin_release(int32_t chemset);
 const char* ckmi_kin_last_error(void);
+/* The reactor keyword policy shared by KINAll0D_Calculate and the Python drop-in: 1 = sets a
+ * ckmi_reactor_cfg field, 2 = accepted without effect on the device path, 0 = rejected. */
+int ckmi_kin_keyword_class(const char* key);
 
 /* ---- session and preprocessing (chemkin_wrapper.py:300-331) */
 /* :303-316.  Parses chem (+ therm; an inline THERMO block overrides it) with the native interpreter

@@ -15,7 +15,8 @@ profiles are mass fractions, reactormodel.py:784).  For many reactors at once us
 
 Keywords on the device path: TIME, ATOL/RTOL, HO, STPT, NNEG, TIFP/DTIGN/TLIM/KLIM, IGN_STOP,
 VPRO/PPRO/TPRO, QLOS/HTC/AREAQ/TAMB with QPRO/AEXT, GFAC, ADAP with ASTEPS or AVAR/AVALUE
-(adaptive points are merged with the DTSV grid).  Not yet: HTCPRO, QPRO together with AEXT.
+(adaptive points are merged with the DTSV grid), MAXIT/NSTP; QPRO together with AEXT.  Any other
+keyword or profile is rejected at run(): the same policy as the KIN ABI (ckmi_kin_keyword_class).
 """
 from __future__ import annotations
 
@@ -275,6 +276,16 @@ class BatchReactors(ReactorModel):
         """Translate the keyword list into the typed ckmi configuration."""
         if self._endtime <= 0.0:
             raise ReactorError("required input TIME (reactor.time) is not set")
+        # one keyword policy with the KIN ABI's KINAll0D_Calculate (ckmi_kin_keyword_class): a
+        # keyword the device path does not know is an error, not a silent default
+        from . import kin
+
+        for kw in self._keyword_list:
+            if kin.keyword_class(kw.keyphrase) == 0:
+                raise ReactorError(f"keyword {kw.keyphrase} is not supported on the device path")
+        for key in self._profiles_index:
+            if key not in ("VPRO", "PPRO", "TPRO", "QPRO", "AEXT"):
+                raise ReactorError(f"{key} profiles are not supported on the device path")
         for key in ("HTCPRO",):
             if self.getprofile(key) is not None:
                 raise ReactorError(f"{key} profiles are not supported on the device path yet")
@@ -319,7 +330,8 @@ class BatchReactors(ReactorModel):
             h0=float(self.getkeyword("HO", 0.0)), hmax=float(self.getkeyword("STPT", 0.0)),
             nneg=bool(self.getkeyword("NNEG", False)), ign_mode=ign_mode, ign_val=ign_val, ign_species=ign_sp,
             ign_stop=bool(self.getkeyword("IGN_STOP", False)), profile=prof, prof_kind=prof_kind,
-            gfac=self._gasratemultiplier, **heat, **adap)
+            gfac=self._gasratemultiplier, max_steps=int(self.getkeyword("MAXIT", self.getkeyword("NSTP", 0)) or 0),
+            **heat, **adap)
 
     # ------------------------------------------------------------------ run
     def run(self) -> int:

@@ -166,10 +166,28 @@ int species_index(const ChemSet* s, const std::string& name) {
   return -1;
 }
 
+// The one keyword policy of both front-ends (this KIN ABI and the Python drop-in's reactor_cfg,
+// which asks ckmi_kin_keyword_class): keywords that set a ckmi_reactor_cfg field, keywords accepted
+// without effect on the device path (print interval, volume / area given elsewhere, output files),
+// and everything else rejected with a message.
+const char* const KW_DEVICE[] = {"ATOL", "RTOL", "HO", "STPT", "NNEG", "TIFP", "DTIGN", "TLIM", "KLIM", "IGN_STOP",
+                                 "DTSV", "ADAP", "ASTEPS", "AVAR", "AVALUE", "GFAC", "QLOS", "HTC", "TAMB", "AREAQ",
+                                 "MAXIT", "NSTP"};
+const char* const KW_NOEFFECT[] = {"DELT", "VOL", "AREA", "NADAP", "NO_SDOUTPUT_WRITE", "NO_XMLOUTPUT_WRITE"};
+int keyword_class(const std::string& k) {
+  for (const char* x : KW_DEVICE)
+    if (k == x) return 1;
+  for (const char* x : KW_NOEFFECT)
+    if (k == x) return 2;
+  return 0;
+}
+
 // Keyword text (reactormodel.py:349-372: "KEY    value", or "KEY" for booleans) -> ckmi_reactor_cfg.
 // Unknown keywords are errors (the reference's library rejects what it does not know).
 int apply_keywords(const ChemSet* s, ckmi_reactor_cfg& c, double& dtsv, bool& adap) {
   for (const auto& kv : g_r.kw) {
+    if (!keyword_class(kv.first))
+      return fail(CKMI_ERR_UNSUPPORTED, "keyword " + kv.first + " is not supported on the device path");
     const std::string& k = kv.first;
     const std::string& v = kv.second;
     bool ok = true;
@@ -428,6 +446,8 @@ int register_set(const ckmi_mech_desc* desc, int32_t MM, const char* names, cons
 extern "C" {
 
 const char* ckmi_kin_last_error(void) { return g_err.c_str(); }
+
+int ckmi_kin_keyword_class(const char* key) { return key ? keyword_class(upper(trim(key))) : 0; }
 
 int ckmi_kin_register(const ckmi_mech_desc* desc, int32_t MM, const char* names, const char* elements,
                       const double* awt, const int32_t* ncf, int32_t* chemset) {

@@ -119,6 +119,7 @@ _REG = {
                                      ct.c_void_p, ct.POINTER(ct.c_int32)]),
     "ckmi_kin_release": (ct.c_int, [ct.c_int32]),
     "ckmi_kin_last_error": (ct.c_char_p, []),
+    "ckmi_kin_keyword_class": (ct.c_int, [ct.c_char_p]),
 }
 
 NAME_LEN = 16
@@ -132,6 +133,12 @@ def bind(L: ct.CDLL = None) -> ct.CDLL:
         fn.restype = res
         fn.argtypes = args
     return L
+
+
+def keyword_class(key: str) -> int:
+    """The device path's keyword policy (ckmi_kin_keyword_class; host only): 1 sets a reactor
+    configuration field, 2 accepted without effect, 0 rejected."""
+    return int(bind().ckmi_kin_keyword_class(key.encode()))
 
 
 def last_error() -> str:

@@ -97,3 +97,39 @@ def test_secondary_sweeps_partition_over_ranks(world):
     assert sum(p[0].size for p in parts) == T5.size
     for r, p in enumerate(parts):
         assert np.array_equal(p[1], P5[r::world])
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_bench_launcher_shards_and_max_time(n):
+    """bench.py --gpus N run directly is its own launcher (no external torchrun): it starts N rank
+    processes, the headline shards are disjoint and together complete (64 N x 32 x 32 reactors, the
+    strided T0 split), and the reported time is the max over ranks.  --plan runs the same launcher
+    and timing protocol on CPU (gloo)."""
+    import json
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--plan"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    rep = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rep["n_ranks"] == n and rep["shard_sizes"] == [65536] * n
+    assert rep["disjoint"] and rep["complete"]
+    assert rep["max_seconds"] >= max(rep["rank_seconds"]) - 1e-9
+    assert rep["max_seconds"] >= 0.05 * n
+
+
+def test_bench_launcher_refuses_more_gpus_than_visible():
+    import subprocess
+    import sys
+
+    import torch
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = torch.cuda.device_count() + 1
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(max(n, 2)), "--steps", "1"],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0 and "visible" in (out.stderr + out.stdout)

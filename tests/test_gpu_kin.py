@@ -337,7 +337,7 @@ def test_full_keyword_mode_calculate_input(K, mech):
     _setup(L, cs, 1, 1, 5e-4, 1000.0, P_ATM, 1.0, Y0)
     X0 = (Y0 / mech.wt) / np.sum(Y0 / mech.wt)
     lines = ["TRAN", "CONP", "ENRG", "PRES    1.0", "TEMP    1000.0", "TIME    0.0005"]
-    lines += [f"REAC    {mech.species[k]}    {X0[k]!r}" for k in range(mech.KK) if X0[k] > 1e-12]
+    lines += [f"REAC    {mech.species[k]}    {float(X0[k])!r}" for k in range(mech.KK) if X0[k] > 1e-12]
     lines += ["ATOL    1e-20", "RTOL    1e-08", "NNEG", "DTSV    5e-06", "DTIGN    400", "NADAP", "QRGEQ", "END"]
     blob = "".join(lines).encode()
     lens = np.array([len(x) for x in lines], np.int32)
