@@ -45,6 +45,14 @@ extern "C" {
 #define CKMI_RXN_FALLOFF 2
 #define CKMI_RXN_PLOG 3 /* elementary with a PLOG table: ln k linear in ln P, clamped outside */
 #define CKMI_RXN_CHEMACT 4 /* chemically activated: arr = k0, low = HIGH (k_inf); k = k0 F / (1 + Pr) */
+/* Chebyshev (TCHEB / PCHEB / CHEB on a (+M) reaction): log10 k = sum_t sum_p a[t][p] T_t(Tr) T_p(Pr),
+ * Tr = (2/T - 1/Tmin - 1/Tmax) / (1/Tmax - 1/Tmin), Pr = (2 log P - log Pmin - log Pmax) /
+ * (log Pmax - log Pmin), no [M] factor, not clamped outside the range.  Its plog_par rows:
+ * (NT, NP, 0, 0), (Tmin [K], Tmax [K], Pmin [atm], Pmax [atm]), then a[t][p] t-major, 4 per row. */
+#define CKMI_RXN_CHEB 5
+/* Landau-Teller elementary reaction: k = A T^b exp(-E/RT + B T^(-1/3) + C T^(-2/3)), low = (B, C, 0);
+ * with REV, fpar[0..1] = the RLT (B, C) of the reverse rate */
+#define CKMI_RXN_LT 6
 /* falloff forms */
 #define CKMI_FALL_NONE 0
 #define CKMI_FALL_LINDEMANN 1

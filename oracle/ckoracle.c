@@ -44,7 +44,9 @@ void cko_thermo(const cko_mech* m, double T, double* cp_R, double* h_RT, double*
  *     then settles into a period-2 cycle at C ~ 0 with the step size locked, and at some tolerances
  *     the integration hits max steps (case 1 of tests/test_ford.py at rtol 0.97e-8).
  *     The chord changes the rate only below 1e-14 mol/cm3 (this implementation's choice: the
- *     reference holds no FORD golden, parity unpinned);
+ *     reference holds no FORD golden, parity unpinned).  A Jacobian-only fix does not do it: with
+ *     the rate left flat for C <= 0, a floored or chord-slope derivative still stalls (measured);
+ *     with the Lipschitz rate, the plain derivative of it is robust;
  *   any other o: pow(C, o) for C > 0 and 0 for C <= 0. */
 #define CFLOOR 1e-14
 static double conc_pow(double c, double o) {
@@ -55,16 +57,14 @@ static double conc_pow(double c, double o) {
   if (o < 1.0 && c < CFLOOR) return pow(CFLOOR, o - 1.0) * c;
   return c > 0.0 ? pow(c, o) : 0.0;
 }
-/* the Jacobian's d C^o / dC under the same rule.  For 0 < o < 1 it is the chord slope
- * max(C, CFLOOR)^(o-1) (exact below CFLOOR, >= the tangent o C^(o-1) above it): C^o is concave, so
- * the tangent lets the modified Newton iteration overshoot past C = 0 and cycle; the chord damps it
- * (only the Newton matrix changes, not the rates). */
+/* d C^o / dC of that rule (the Jacobian): the tangent o C^(o-1) above CFLOOR, the chord's slope
+ * CFLOOR^(o-1) below it -- the exact derivative of the Lipschitz rate */
 static double dconc_pow(double c, double o) {
   if (o == 0.0) return 0.0;
   if (o == 1.0) return 1.0;
   if (o == 2.0) return 2.0 * c;
   if (o == 3.0) return 3.0 * c * c;
-  if (o < 1.0) return pow(fmax(c, CFLOOR), o - 1.0);
+  if (o < 1.0) return c < CFLOOR ? pow(CFLOOR, o - 1.0) : o * pow(c, o - 1.0);
   return c > 0.0 ? o * pow(c, o - 1.0) : 0.0;
 }
 /* order of reactant slot s / product slot s of reaction i */
@@ -104,6 +104,36 @@ static void plog_rate(const cko_mech* m, int i, double lnP, double lnT, double i
   *dlk = dk0 + w * (dk1 - dk0);
 }
 
+/* Chebyshev rate (CKMI_RXN_CHEB, include/ckmi.h): log10 k = sum_t sum_p a[t][p] T_t(Tr) T_p(Pr) with
+ * the reduced inverse temperature and log pressure; d ln k / dT through dTr/dT.  Rows of plog_par:
+ * (NT, NP), (Tmin, Tmax, Pmin, Pmax [atm]), then a[t][p] t-major.  No clamping outside the range. */
+static void cheb_rate(const cko_mech* m, int i, double P, double invT, double* lnk, double* dlk) {
+  const double* r = m->plog_par + 4 * m->plog_ptr[i];
+  const int nt = (int)r[0], np = (int)r[1];
+  const double iTmin = 1.0 / r[4], iTmax = 1.0 / r[5];
+  const double lPmin = log10(r[6] * PATM), lPmax = log10(r[7] * PATM);
+  const double Tr = (2.0 * invT - iTmin - iTmax) / (iTmax - iTmin);
+  const double Pr = (2.0 * log10(P) - lPmin - lPmax) / (lPmax - lPmin);
+  const double* a = r + 8;
+  double tp[16], tt[16], dt[16], lk = 0.0, dl = 0.0;
+  tp[0] = 1.0, tt[0] = 1.0, dt[0] = 0.0;
+  tp[1] = Pr, tt[1] = Tr, dt[1] = 1.0;
+  for (int p = 2; p < np; ++p) tp[p] = 2.0 * Pr * tp[p - 1] - tp[p - 2];
+  for (int t = 2; t < nt; ++t) {
+    tt[t] = 2.0 * Tr * tt[t - 1] - tt[t - 2];
+    dt[t] = 2.0 * tt[t - 1] + 2.0 * Tr * dt[t - 1] - dt[t - 2];
+  }
+  for (int t = 0; t < nt; ++t) {
+    double row = 0.0;
+    for (int p = 0; p < np; ++p) row += a[t * np + p] * tp[p];
+    lk += tt[t] * row;
+    dl += dt[t] * row;
+  }
+  const double LN10 = 2.302585092994046;
+  *lnk = lk * LN10;
+  *dlk = dl * LN10 * (-2.0 * invT * invT / (iTmax - iTmin));
+}
+
 static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double invT, double lnPRT, double P,
                           const double* C, double Ctot, const double* g_RT, const double* h_RT, double dlnA,
                           double gfac, rxn_eval* e) {
@@ -111,10 +141,18 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
   double kf, dlkf;
   double mfac = 1.0;
   const int type = m->rtype[i];
-  if (type == 3) {
+  double t13 = 0.0, t23 = 0.0; /* Landau-Teller T^(-1/3), T^(-2/3) */
+  if (type == 3 || type == 5) {
     double lnk;
-    plog_rate(m, i, log(P), lnT, invT, &lnk, &dlkf);
+    if (type == 3) plog_rate(m, i, log(P), lnT, invT, &lnk, &dlkf);
+    else cheb_rate(m, i, P, invT, &lnk, &dlkf);
     kf = exp(lnk + dlnA);
+  } else if (type == 6) {
+    const double* lt = m->low + 3 * i;
+    t13 = exp(-lnT / 3.0);
+    t23 = t13 * t13;
+    kf = exp(a[0] + dlnA + a[1] * lnT - a[2] * invT + lt[0] * t13 + lt[1] * t23);
+    dlkf = (a[1] + a[2] * invT - (lt[0] * t13 + 2.0 * lt[1] * t23) / 3.0) * invT;
   } else {
     kf = exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
     dlkf = (a[1] + a[2] * invT) * invT;
@@ -157,9 +195,15 @@ static void eval_reaction(const cko_mech* m, int i, double T, double lnT, double
   if (m->rev[i]) {
     if (m->has_rev[i]) {
       const double* r = m->revp + 3 * i;
-      kr = exp(r[0] + r[1] * lnT - r[2] * invT);
-      if (type == 2 || type == 4) kr *= kf / exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
-      dlkr = (r[1] + r[2] * invT) * invT;
+      if (type == 6) { /* RLT terms of the explicit reverse rate */
+        const double* rl = m->fpar + 5 * i;
+        kr = exp(r[0] + r[1] * lnT - r[2] * invT + rl[0] * t13 + rl[1] * t23);
+        dlkr = (r[1] + r[2] * invT - (rl[0] * t13 + 2.0 * rl[1] * t23) / 3.0) * invT;
+      } else {
+        kr = exp(r[0] + r[1] * lnT - r[2] * invT);
+        if (type == 2 || type == 4) kr *= kf / exp(a[0] + dlnA + a[1] * lnT - a[2] * invT);
+        dlkr = (r[1] + r[2] * invT) * invT;
+      }
     } else {
       double dG = 0.0, dH = 0.0, dnu = 0.0;
       for (int s = 0; s < m->nr[i]; ++s) {

@@ -85,6 +85,19 @@ class NumpyKinetics:
         lnk = tab[:, 1] + tab[:, 2] * np.log(T) - tab[:, 3] / T
         return float(np.exp(np.interp(np.log(P), tab[:, 0], lnk)))
 
+    def _cheb_k(self, i, P, T):
+        # Chebyshev: log10 k = sum_t sum_p a[t][p] T_t(Tr) T_p(Pr) (numpy.polynomial.chebyshev)
+        from numpy.polynomial import chebyshev as ch
+
+        r = self.plog_par[self.plog_ptr[i]:self.plog_ptr[i + 1]].ravel()
+        nt, npr = int(r[0]), int(r[1])
+        tmin, tmax, pmin, pmax = r[4:8]
+        a = r[8:8 + nt * npr].reshape(nt, npr)
+        Tr = (2.0 / T - 1.0 / tmin - 1.0 / tmax) / (1.0 / tmax - 1.0 / tmin)
+        lp = np.log10([pmin * PATM, pmax * PATM])
+        Pr = (2.0 * np.log10(P) - lp[0] - lp[1]) / (lp[1] - lp[0])
+        return float(10.0 ** ch.chebval2d(Tr, Pr, a))
+
     def rates(self, T, P, Y):
         Y = np.asarray(Y, dtype=np.float64)
         rho = P / (RU * T) / np.sum(Y / self.wt)
@@ -94,6 +107,11 @@ class NumpyKinetics:
         kf = np.exp(self.arr[:, 0] + self.arr[:, 1] * np.log(T) - self.arr[:, 2] / T)
         for i in np.nonzero(self.rtype == 3)[0]:
             kf[i] = self._plog_k(i, P, T)
+        for i in np.nonzero(self.rtype == 5)[0]:
+            kf[i] = self._cheb_k(i, P, T)
+        lt = self.rtype == 6  # Landau-Teller: + B T^-1/3 + C T^-2/3 (low[:, :2]; RLT in fpar[:, :2])
+        t13 = T ** (-1.0 / 3.0)
+        kf = np.where(lt, kf * np.exp(self.low[:, 0] * t13 + self.low[:, 1] * t13 * t13), kf)
         M = self.eff @ C
         tbc = self.tbsp >= 0
         M = np.where(tbc, C[np.maximum(self.tbsp, 0)], M)
@@ -122,6 +140,7 @@ class NumpyKinetics:
         Kc = np.exp(-dG) * (PATM / (RU * T)) ** dn
         kr_rev = np.exp(self.revp[:, 0] + self.revp[:, 1] * np.log(T) - self.revp[:, 2] / T)
         kr_rev = np.where(fo, kr_rev * kf / kinf, kr_rev)
+        kr_rev = np.where(lt, kr_rev * np.exp(self.fpar[:, 0] * t13 + self.fpar[:, 1] * t13 * t13), kr_rev)
         kr = np.where(self.rev, np.where(self.has_rev, kr_rev, kf / Kc), 0.0)
         pf = np.prod(_cpow(C[None, :], self.ordf), axis=1)
         pr = np.prod(_cpow(C[None, :], self.ordr), axis=1)

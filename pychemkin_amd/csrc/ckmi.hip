@@ -1085,8 +1085,20 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     const int fl = flags[s];
     const int type = fl & 3;
     uint32_t inf = (uint32_t)(fl & 0x7f) | ((uint32_t)ns_r << 7) | ((uint32_t)ns_p << 10) | (uint32_t)(fl & 0x2000) |
-                   (uint32_t)(fl & RX_GEN);
-    if (slots[s] >= 0 && type == CKMI_RXN_PLOG) {
+                   (uint32_t)(fl & RX_GEN) | (uint32_t)(fl & RX_ALT);
+    if (slots[s] >= 0 && type == CKMI_RXN_PLOG && (fl & RX_ALT)) {
+      // Chebyshev stream: NT, NP, 1/Tmin, 1/Tmax, log10 Pmin, log10 Pmax [dyn/cm2], then a[t][p]
+      const int i = slots[s];
+      const double* r = d->plog_par + 4 * d->plog_ptr[i];
+      const int nt = (int)r[0], npr = (int)r[1];
+      std::vector<double> rec{(double)nt, (double)npr, 1.0 / r[4], 1.0 / r[5], std::log10(r[6] * 1.01325e6),
+                              std::log10(r[7] * 1.01325e6)};
+      rec.insert(rec.end(), r + 8, r + 8 + nt * npr);
+      rec.resize((rec.size() + AUXW - 1) / AUXW * AUXW, 0.0);
+      aux.insert(aux.end(), rec.begin(), rec.end());
+      inf |= (uint32_t)naux << 16;
+      naux += (int)rec.size() / AUXW;
+    } else if (slots[s] >= 0 && type == CKMI_RXN_PLOG) {
       // PLOG stream: npts, then (ln P, ln A, b, E/R) per point, over ceil((1 + 4 npts) / AUXW) records
       const int i = slots[s], p0 = d->plog_ptr[i], n = d->plog_ptr[i + 1] - p0;
       std::vector<double> rec{(double)n};
@@ -1095,7 +1107,8 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
       aux.insert(aux.end(), rec.begin(), rec.end());
       inf |= (uint32_t)naux << 16;
       naux += (int)rec.size() / AUXW;
-    } else if (slots[s] >= 0 && (type == 2 || (fl & 8) || gen)) {
+    } else if (slots[s] >= 0 && (type == 2 || (fl & 8) || gen || (fl & RX_ALT))) {
+      // (a Landau-Teller reaction's record: low = B, C of LT; fp[0], fp[1] = B, C of RLT)
       double rec[AUXW] = {lnA0[s], beta0[s], Ea0[s], fp[0 * IIp + s], fp[1 * IIp + s], fp[2 * IIp + s],
                           fp[3 * IIp + s], fp[4 * IIp + s], rlnA[s], rbeta[s], rEa[s], 0.0};
       const int ft = (fl >> 4) & 7;
@@ -1381,14 +1394,27 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     for (int u = 0; u < d->np[i]; ++u) up += d->pnu[4 * i + u];
     return (ur > 2.0 || up > 2.0) ? 1 : 0;
   };
-  for (int t : {CKMI_RXN_ELEMENTARY, CKMI_RXN_THIRDBODY, CKMI_RXN_FALLOFF, CKMI_RXN_CHEMACT, CKMI_RXN_PLOG})
+  for (int t : {CKMI_RXN_ELEMENTARY, CKMI_RXN_LT, CKMI_RXN_THIRDBODY, CKMI_RXN_FALLOFF, CKMI_RXN_CHEMACT, CKMI_RXN_PLOG,
+                CKMI_RXN_CHEB})
     for (int cls = 0; cls < 3; ++cls)
       for (int i = 0; i < II; ++i)
         if (d->rtype[i] == t && slot_class(i) == cls) ordr.push_back(i);
   for (int i = 0; i < II; ++i) {
-    if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_CHEMACT) {
+    if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_LT) {
       delete m;
       return fail(CKMI_ERR_UNSUPPORTED, "unsupported reaction type");
+    }
+    if (d->rtype[i] == CKMI_RXN_CHEB) {
+      const int p0 = d->plog_ptr ? d->plog_ptr[i] : 0, nrow = d->plog_ptr ? d->plog_ptr[i + 1] - p0 : 0;
+      const double* r = d->plog_par ? d->plog_par + 4 * p0 : nullptr;
+      const int nt = r && nrow >= 2 ? (int)r[0] : 0, npr = r && nrow >= 2 ? (int)r[1] : 0;
+      const bool ok = r && nt >= 1 && nt <= 12 && npr >= 1 && npr <= 12 && nrow == 2 + (nt * npr + 3) / 4 &&
+                      r[4] > 0.0 && r[5] > r[4] && r[6] > 0.0 && r[7] > r[6] && !d->has_rev[i];
+      if (!ok) {
+        delete m;
+        return fail(CKMI_ERR_UNSUPPORTED, "Chebyshev record must hold 1..12 x 1..12 coefficients, increasing "
+                                          "positive ranges and no REV");
+      }
     }
     if (d->rtype[i] == CKMI_RXN_PLOG) {
       const int p0 = d->plog_ptr ? d->plog_ptr[i] : 0, n = d->plog_ptr ? d->plog_ptr[i + 1] - p0 : 0;
@@ -1451,13 +1477,17 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     if (i < 0) continue;
     m->slot_of[i] = s;
     const bool chemact = d->rtype[i] == CKMI_RXN_CHEMACT;  // device type 2 + info bit 13
-    const int type = chemact ? CKMI_RXN_FALLOFF : d->rtype[i];
-    flags[s] = type | (d->rev[i] ? 4 : 0) | (d->has_rev[i] ? 8 : 0) | ((d->ftype[i] & 7) << 4) | (chemact ? 0x2000 : 0);
+    const bool cheb = d->rtype[i] == CKMI_RXN_CHEB;        // device type 3 (rate from the aux stream) + bit 15
+    const bool lt = d->rtype[i] == CKMI_RXN_LT;            // device type 0 + bit 15 (B, C in the aux record)
+    const int type = chemact ? CKMI_RXN_FALLOFF : (cheb ? CKMI_RXN_PLOG : (lt ? CKMI_RXN_ELEMENTARY : d->rtype[i]));
+    flags[s] = type | (d->rev[i] ? 4 : 0) | (d->has_rev[i] ? 8 : 0) | ((d->ftype[i] & 7) << 4) | (chemact ? 0x2000 : 0) |
+               ((cheb || lt) ? (int)RX_ALT : 0);
     const int nr = d->nr[i], np = d->np[i];
     if (rxn_general(d, i)) {  // FORD / RORD / non-integral: real coefficients, extended variants
-      if (type == CKMI_RXN_PLOG) {
+      if (type == CKMI_RXN_PLOG || lt) {
         delete m;
-        return fail(CKMI_ERR_UNSUPPORTED, "FORD / RORD or non-integral coefficients on a PLOG reaction");
+        return fail(CKMI_ERR_UNSUPPORTED,
+                    "FORD / RORD or non-integral coefficients on a PLOG, Chebyshev or Landau-Teller reaction");
       }
       for (int u = 0; u < nr; ++u)
         if (!(d->rnu[i * SLOTS + u] > 0.0) || (d->ford && d->ford[i * SLOTS + u] < 0.0)) {
@@ -1493,7 +1523,7 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     dnu[s] = sr - sf;
     ordf[s] = sf;
     ordrr[s] = sr;
-    const bool plog = type == CKMI_RXN_PLOG;  // rate from the aux stream; the slot holds ln 1, 0, 0
+    const bool plog = type == CKMI_RXN_PLOG;  // PLOG / CHEB: rate from the aux stream; the slot holds ln 1, 0, 0
     lnA[s] = plog ? 0.0 : d->arr[3 * i];
     beta[s] = plog ? 0.0 : d->arr[3 * i + 1];
     Ea[s] = plog ? 0.0 : d->arr[3 * i + 2];
@@ -1510,7 +1540,9 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   m->rtype_orig.assign(d->rtype, d->rtype + II);
   // PLOG and chemically activated reactions are evaluated by the extended kernel variant
   m->has_plog = std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_PLOG) > 0 ||
-                std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_CHEMACT) > 0;
+                std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_CHEMACT) > 0 ||
+                std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_CHEB) > 0 ||
+                std::count(d->rtype, d->rtype + II, (int32_t)CKMI_RXN_LT) > 0;
   for (int i = 0; i < II; ++i) m->has_general = m->has_general || rxn_general(d, i);
   m->has_plog = m->has_plog || m->has_general;
   m->lnA_orig.resize(II);
@@ -1624,8 +1656,8 @@ int ckmi_get_arrhenius(const ckmi_mech* m, double* A, double* b, double* E) {
 
 int ckmi_set_afactor(ckmi_mech* m, int32_t irxn, double A) {
   if (!m || irxn < 0 || irxn >= m->II || !(A > 0.0)) return fail(CKMI_ERR_ARG, "bad reaction index or A");
-  if (m->rtype_orig[irxn] == CKMI_RXN_PLOG)
-    return fail(CKMI_ERR_UNSUPPORTED, "A-factor of a PLOG reaction (its rates come from the PLOG table)");
+  if (m->rtype_orig[irxn] == CKMI_RXN_PLOG || m->rtype_orig[irxn] == CKMI_RXN_CHEB)
+    return fail(CKMI_ERR_UNSUPPORTED, "A-factor of a PLOG / Chebyshev reaction (its rate comes from its table)");
   const double lnA = std::log(A);
   m->lnA_orig[irxn] = lnA;
   const int s = m->slot_of[irxn];

@@ -721,6 +721,76 @@ template <int NB>
 using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB>, BigMatrix<NB>>;
 #endif
 
+// ------------------------------------------------------------------ general reactions
+// FORD / RORD orders and non-integral coefficients (mechanisms flagged has_general, PL = true):
+// the reaction keeps no unit slots, its species, coefficients and orders are in the aux stream
+// (eval_gen_img).  RHS: q scattered with the real coefficients into this wave's wdot copy; with
+// the Jacobian, dwdot/dT through the orders and dq/dC of each slot (the chord rule of dconc_pow)
+// into the reaction's 8 Dg slots (reactant slots 0..3, product slots 4..7), as oracle reactor_rhs.
+__device__ __noinline__ void gen_rhs_big(const MechView& V, const RunCtx& R, int i, uint32_t inf, double T,
+                                         double lnT, double invT, double lnPRT, double P, const double* C,
+                                         const double* gRT, const double* hRT, const double* Mg, double* wdw,
+                                         double* dwdw, int conp, bool with_j, double* __restrict__ Dg, int IIp) {
+  const double* g;
+  const Rxn e = eval_gen_img(V, i, inf, T, lnT, invT, lnPRT, P, C, gRT, hRT, Mg, with_j, R.pslot, R.plnf, R.gfac, g);
+  const double* e2t = V.e2t();
+  const int nr = (int)g[0], np = (int)g[1];
+  const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
+  for (int u = 0; u < nr; ++u) atomicAdd(&wdw[(int)g[2 + 3 * u]], -g[3 + 3 * u] * q);
+  for (int u = 0; u < np; ++u) atomicAdd(&wdw[(int)g[14 + 3 * u]], g[15 + 3 * u] * q);
+  if (!with_j) return;
+  double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
+  if (conp) {
+    double of = 0.0, orr = 0.0;
+    for (int u = 0; u < nr; ++u) of += g[4 + 3 * u];
+    for (int u = 0; u < np; ++u) orr += g[16 + 3 * u];
+    dqdT -= e.mfac * (of * e.kf * e.pf - orr * e.kr * e.pr) * invT;
+    if (rx_type(inf) == 1) dqdT -= q * invT;
+  }
+  for (int u = 0; u < nr; ++u) atomicAdd(&dwdw[(int)g[2 + 3 * u]], -g[3 + 3 * u] * dqdT);
+  for (int u = 0; u < np; ++u) atomicAdd(&dwdw[(int)g[14 + 3 * u]], g[15 + 3 * u] * dqdT);
+  for (int side = 0; side < 2; ++side) {
+    const int ns = side == 0 ? nr : np;
+    const double* sl = g + (side == 0 ? 2 : 14);
+    const double kk = side == 0 ? e.mfac * e.kf : -e.mfac * e.kr;
+    for (int s = 0; s < 4; ++s) {
+      double d = 0.0;
+      if (s < ns && kk != 0.0) {
+        d = dconc_pow(C[(int)sl[3 * s]], sl[3 * s + 2], e2t);
+        for (int u = 0; u < ns; ++u)
+          if (u != s) d *= conc_pow(C[(int)sl[3 * u]], sl[3 * u + 2], e2t);
+        d *= kk;
+      }
+      Dg[(4 * side + s) * IIp + i] = d;
+    }
+  }
+}
+// Jacobian columns lo..hi-1 of a general reaction from its Dg slots: column 1 + j of slot species
+// j gets -nu_r dq W_k / W_j on reactant rows k and +nu_p dq W_k / W_j on product rows
+__device__ __noinline__ void gen_jac_cols_big(const MechView& V, int i, uint32_t inf, const double* __restrict__ Dg,
+                                              int IIp, double* jb, int c0, int lo, int hi, int LDJ) {
+  const double* g = V.aux() + AUXW * (rx_aux(inf) + 1);
+  const int nr = (int)g[0], np = (int)g[1];
+  for (int sl = 0; sl < 8; ++sl) {
+    const bool prod = sl >= 4;
+    const int u0 = sl & 3;
+    if (u0 >= (prod ? np : nr)) continue;
+    const int j = (int)g[(prod ? 14 : 2) + 3 * u0];
+    const int col = 1 + j;
+    if (col < lo || col >= hi) continue;
+    const double dqw = Dg[sl * IIp + i] * V.rwt()[j];
+    double* jc = jb + (col - c0) * LDJ + 1;
+    for (int u = 0; u < nr; ++u) {
+      const int k = (int)g[2 + 3 * u];
+      atomicAdd(&jc[k], -g[3 + 3 * u] * dqw * V.wt()[k]);
+    }
+    for (int u = 0; u < np; ++u) {
+      const int k = (int)g[14 + 3 * u];
+      atomicAdd(&jc[k], g[15 + 3 * u] * dqw * V.wt()[k]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ right-hand side
 // f(t, y) for this thread's component (thread 0 = T) and, if with_j, the Jacobian into the
 // workgroup's HBM slot Jg (FP32, column-major, leading dimension NT).  Same formulation as
@@ -786,6 +856,12 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
     const int i = base + lane;
     const uint32_t inf = V.info()[i];
     const int nr = rx_nr(inf), np = rx_np(inf);
+    if constexpr (PL) {
+      if (inf & RX_GEN) {  // FORD / RORD / non-integral coefficients: real nu and orders
+        gen_rhs_big(V, R, i, inf, T, lnT, invT, lnPRT, P, C, gRT, hRT, Mg, wdw, dwdw, conp, with_j, Dg, IIp);
+        continue;
+      }
+    }
     if (nr + np == 0) continue;
     const uint32_t rs = V.rsp()[i], ps = V.psp()[i];
     const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, 0u, T, lnT, invT, lnPRT, P, C, gRT, hRT, Mg, with_j, R.pslot,
@@ -883,6 +959,12 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
       const int i = base + lane;
       const uint32_t inf = V.info()[i];
       const int nr = rx_nr(inf), np = rx_np(inf);
+      if constexpr (PL) {
+        if (inf & RX_GEN) {  // the general reaction's slots and real coefficients (aux stream)
+          gen_jac_cols_big(V, i, inf, Dg, IIp, jb, c0, lo, hi, LDJ);
+          continue;
+        }
+      }
       if (nr + np == 0) continue;
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i];
 #pragma unroll 1
@@ -1731,10 +1813,13 @@ int launch_big_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const React
   if (nvar > BIG_NMAX)
     return set_error(CKMI_ERR_UNSUPPORTED, "batch reactors with more than " + std::to_string(BIG_NMAX - 1) +
                                                " species are not supported (the ROP/thermo kernels are)");
-  if (m->has_plog)
-    return set_error(CKMI_ERR_UNSUPPORTED,
-                     "PLOG / chemically activated / FORD-RORD-fractional-order reactions in batch reactors with "
-                     "more than 63 species");
+  if (m->has_plog) {
+    // PLOG, chemically activated and general (FORD / RORD / fractional) reactions: the extended
+    // variant, compiled for three matrix sizes (a mechanism runs in the smallest that holds it)
+    if (nvar <= 128) return launch_big_nc<8, true>(m, n, dc, io, stream);
+    if (nvar <= 176) return launch_big_nc<11, true>(m, n, dc, io, stream);
+    return launch_big_nc<12, true>(m, n, dc, io, stream);
+  }
   switch ((nvar + 15) / 16) {  // NB: register blocks per dimension (NC = 16 NB >= n)
     case 1:
     case 2:

@@ -121,6 +121,11 @@ __device__ __forceinline__ int sp_of(uint32_t packed, int u) { return (packed >>
 __device__ __forceinline__ int nur_of(uint32_t nu, int u) { return (nu >> (4 * u)) & 0xf; }
 __device__ __forceinline__ int nup_of(uint32_t nu, int u) { return (nu >> (16 + 4 * u)) & 0xf; }
 
+// Info bit 15: on a type-3 slot a Chebyshev rate (aux stream NT, NP, 1/Tmin, 1/Tmax, log10 Pmin,
+// log10 Pmax, a[t][p]) instead of a PLOG table; on a type-0 slot Landau-Teller terms (aux record:
+// B, C at [0], [1]; the RLT B, C of an explicit reverse rate at [3], [4]).  Extended variants only.
+constexpr uint32_t RX_ALT = 0x8000u;
+
 // C^nu for a small non-negative integer nu, branch-free for nu <= 3
 __device__ __forceinline__ double powi(double c, int nu) {
   double r = nu >= 1 ? c : 1.0;
@@ -194,8 +199,47 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
   const double lnA = V.lnA()[i] + (i == pslot ? plnf : 0.0), b = V.beta()[i], Ea = V.Ea()[i];
   double lnkinf = lnA + b * lnT - Ea * invT;
   double dlkf = (b + Ea * invT) * invT;
+  double t13 = 0.0, t23 = 0.0;  // Landau-Teller T^(-1/3), T^(-2/3)
   if constexpr (PLOG) {
-    if (type == 3) {
+    if (type == 3 && (inf & RX_ALT)) {
+      // Chebyshev (lnA, b, Ea of the slot are 0): log10 k = sum_t sum_p a[t][p] T_t(Tr) T_p(Pr),
+      // Tr, Pr the reduced 1/T and log10 P; same arithmetic as oracle/ckoracle.c cheb_rate()
+      const double* pt = V.aux() + AUXW * rx_aux(inf);
+      const int nt = (int)pt[0], npr = (int)pt[1];
+      const double Tr = (2.0 * invT - pt[2] - pt[3]) / (pt[3] - pt[2]);
+      const double Pr = (2.0 * log10(P) - pt[4] - pt[5]) / (pt[5] - pt[4]);
+      const double* a = pt + 6;
+      double lk = 0.0, dl = 0.0;
+      double tm2 = 1.0, tm1 = Tr, dm2 = 0.0, dm1 = 1.0;  // T_{t-2}, T_{t-1} and derivatives
+      for (int t = 0; t < nt; ++t) {
+        double tt, dt;
+        if (t == 0) { tt = 1.0; dt = 0.0; }
+        else if (t == 1) { tt = Tr; dt = 1.0; }
+        else {
+          tt = 2.0 * Tr * tm1 - tm2;
+          dt = 2.0 * tm1 + 2.0 * Tr * dm1 - dm2;
+          tm2 = tm1, tm1 = tt, dm2 = dm1, dm1 = dt;
+        }
+        double row = 0.0, p0 = 1.0, p1 = Pr;
+        for (int p = 0; p < npr; ++p) {
+          const double tp = p == 0 ? 1.0 : (p == 1 ? Pr : 2.0 * Pr * p1 - p0);
+          if (p >= 2) p0 = p1, p1 = tp;
+          row += a[t * npr + p] * tp;
+        }
+        lk += tt * row;
+        dl += dt * row;
+      }
+      constexpr double LN10 = 2.302585092994046;
+      lnkinf += lk * LN10;
+      dlkf = dl * LN10 * (-2.0 * invT * invT / (pt[3] - pt[2]));
+    } else if (type == 0 && (inf & RX_ALT)) {
+      // Landau-Teller: + B T^(-1/3) + C T^(-2/3) (aux record [0], [1])
+      const double* lt = V.aux() + AUXW * rx_aux(inf);
+      t13 = fexp(lnT * (-1.0 / 3.0), V.e2t());
+      t23 = t13 * t13;
+      lnkinf += lt[0] * t13 + lt[1] * t23;
+      dlkf -= (lt[0] * t13 + 2.0 * lt[1] * t23) * (1.0 / 3.0) * invT;
+    } else if (type == 3) {
       // PLOG (lnA, b, Ea of the slot are 0): ln k linear in ln P between the bracketing table
       // pressures, clamped outside; aux stream = npts, then (ln P, ln A, b, E/R) per point.
       // Same arithmetic as oracle/ckoracle.c plog_rate().
@@ -266,9 +310,10 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
   const bool s23 = __ballot(rx_nr(inf) > 2 || rx_np(inf) > 2) != 0;
   if (rx_rev(inf)) {
     if (rx_hasrev(inf)) {
-      kr = fexp(ax[8] + ax[9] * lnT - ax[10] * invT, e2t);
+      const bool rlt = PLOG && type == 0 && (inf & RX_ALT);  // RLT terms of the explicit reverse rate
+      kr = fexp(ax[8] + ax[9] * lnT - ax[10] * invT + (rlt ? ax[3] * t13 + ax[4] * t23 : 0.0), e2t);
       if (type == 2) kr *= kf / kf_inf;
-      dlkr = (ax[9] + ax[10] * invT) * invT;
+      dlkr = (ax[9] + ax[10] * invT) * invT - (rlt ? (ax[3] * t13 + 2.0 * ax[4] * t23) * (1.0 / 3.0) * invT : 0.0);
     } else {
       // unit-coefficient slots: sum_products g - sum_reactants g, dnu = np - nr
       double gp = gRT[p0] + gRT[p1], gr = gRT[r0] + gRT[r1];
@@ -322,14 +367,14 @@ __device__ __forceinline__ double conc_pow(double c, double o, const double* e2t
   if (o < 1.0 && c < CONC_FLOOR) return fexp((o - 1.0) * LN_CONC_FLOOR, e2t) * c;
   return c > 0.0 ? fexp(o * log(c), e2t) : 0.0;
 }
-// The Jacobian's d C^o / dC (oracle dconc_pow): the chord slope max(C, CONC_FLOOR)^(o-1) for
-// 0 < o < 1 (damps the modified Newton iteration where C^o is concave), the tangent otherwise
+// The Jacobian's d C^o / dC (oracle dconc_pow): the exact derivative of that rule -- the tangent
+// o C^(o-1) above CONC_FLOOR, the chord's slope CONC_FLOOR^(o-1) below it
 __device__ __forceinline__ double dconc_pow(double c, double o, const double* e2t) {
   if (o == 1.0) return 1.0;
   if (o == 2.0) return 2.0 * c;
   if (o == 0.0) return 0.0;
   if (o == 3.0) return 3.0 * c * c;
-  if (o < 1.0) return fexp((o - 1.0) * (c > CONC_FLOOR ? log(c) : LN_CONC_FLOOR), e2t);
+  if (o < 1.0) return c < CONC_FLOOR ? fexp((o - 1.0) * LN_CONC_FLOOR, e2t) : o * fexp((o - 1.0) * log(c), e2t);
   return c > 0.0 ? o * fexp((o - 1.0) * log(c), e2t) : 0.0;
 }
 

@@ -119,8 +119,9 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
   if (const char* w = std::getenv("CKMI_JIT_WAVES")) wpe = std::max(1, std::atoi(w));
 
   for (int i = 0; i < II; ++i) {
-    if (d->rtype[i] == CKMI_RXN_PLOG || d->rtype[i] == CKMI_RXN_CHEMACT) {
-      why = "PLOG / chemically activated reactions";
+    if (d->rtype[i] == CKMI_RXN_PLOG || d->rtype[i] == CKMI_RXN_CHEMACT || d->rtype[i] == CKMI_RXN_CHEB ||
+        d->rtype[i] == CKMI_RXN_LT) {
+      why = "PLOG / chemically activated / Chebyshev / Landau-Teller reactions";
       return false;
     }
     if (rxn_general(d, i)) {

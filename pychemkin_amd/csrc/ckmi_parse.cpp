@@ -147,8 +147,12 @@ struct Reaction {
   bool duplicate = false;
   std::vector<std::pair<int, double>> ford, rord;
   std::vector<std::array<double, 4>> plog;
+  std::vector<double> cheb;  // CHEB values: NT, NP, then NT x NP coefficients
+  bool has_tcheb = false, has_pcheb = false, has_lt = false, has_rlt = false;
+  double tcheb[2] = {300.0, 2500.0}, pcheb[2] = {0.001, 100.0}, lt[2] = {0, 0}, rlt[2] = {0, 0};
   std::string e_units = "CAL/MOLE", a_units = "MOLES";
 };
+constexpr int CHEB_MAX = 12;  // Chebyshev orders per dimension (mechanism.py CHEB_MAX)
 
 void set_pair(std::vector<std::pair<int, double>>& v, int k, double x) {
   for (auto& p : v)
@@ -332,7 +336,8 @@ struct Mech {
     bool aux = s.find('=') == std::string::npos;
     if (!aux) {
       const std::string w = split_ws(up)[0];
-      static const char* kws[] = {"LOW", "TROE", "SRI", "REV", "HIGH", "FORD", "RORD", "PLOG", "DUP", "DUPLICATE", "UNITS"};
+      static const char* kws[] = {"LOW",  "TROE",  "SRI",   "REV",   "HIGH", "FORD", "RORD", "PLOG",
+                                  "DUP",  "DUPLICATE", "UNITS", "CHEB", "TCHEB", "PCHEB", "LT", "RLT"};
       for (const char* k : kws) {
         const size_t n = std::strlen(k);
         if (up.compare(up.find_first_not_of(" \t"), n, k) == 0) {
@@ -449,6 +454,18 @@ struct Mech {
       } else if (k == "PLOG") {
         need(4);
         cur->plog.push_back({nums[0], nums[1], nums[2], nums[3]});
+      } else if (k == "CHEB") {
+        cur->cheb.insert(cur->cheb.end(), nums.begin(), nums.end());
+      } else if (k == "TCHEB" || k == "PCHEB") {
+        if (nums.size() != 2) die(k + " needs /min max/: '" + s + "'");
+        double* dst = k == "TCHEB" ? cur->tcheb : cur->pcheb;
+        dst[0] = nums[0], dst[1] = nums[1];
+        (k == "TCHEB" ? cur->has_tcheb : cur->has_pcheb) = true;
+      } else if (k == "LT" || k == "RLT") {
+        if (nums.size() != 2) die(k + " needs /B C/: '" + s + "'");
+        double* dst = k == "LT" ? cur->lt : cur->rlt;
+        dst[0] = nums[0], dst[1] = nums[1];
+        (k == "LT" ? cur->has_lt : cur->has_rlt) = true;
       } else if (k == "UNITS") {
         // per-reaction units: this reaction's A / E (and its LOW, HIGH, REV, PLOG) are in them
         if (parts.empty()) die("UNITS needs /unit .../: '" + s + "'");
@@ -584,6 +601,29 @@ struct Mech {
     return A * std::pow(AVOGADRO, order - 1.0);
   }
 
+  // plog_par rows of a Chebyshev reaction (mechanism.py Mechanism._cheb_rows)
+  void cheb_rows(const Reaction& r) {
+    if (r.kind != FALLOFF || r.third != -1) die("CHEB needs a (+M) reaction (" + r.equation + ")");
+    if (r.has_low || r.has_high || r.has_troe || r.has_sri || !r.plog.empty() || r.has_rev)
+      die("CHEB with LOW / HIGH / TROE / SRI / PLOG / REV (" + r.equation + ")");
+    if (r.cheb.size() < 2) die("CHEB needs /NT NP/ then the coefficients (" + r.equation + ")");
+    const int nt = (int)r.cheb[0], npr = (int)r.cheb[1];
+    std::vector<double> coef(r.cheb.begin() + 2, r.cheb.end());
+    if (nt != r.cheb[0] || npr != r.cheb[1] || nt < 1 || nt > CHEB_MAX || npr < 1 || npr > CHEB_MAX ||
+        (int)coef.size() != nt * npr)
+      die("CHEB needs NT x NP coefficients with 1 <= NT, NP <= " + std::to_string(CHEB_MAX) + " (" + r.equation + ")");
+    if (!(0.0 < r.tcheb[0] && r.tcheb[0] < r.tcheb[1] && 0.0 < r.pcheb[0] && r.pcheb[0] < r.pcheb[1]))
+      die("TCHEB / PCHEB ranges must be positive and increasing (" + r.equation + ")");
+    if (r.a_units == "MOLECULES") {
+      double order = 0.0;
+      for (const auto& t : r.reac) order += t.second;
+      coef[0] += (order - 1.0) * std::log10(AVOGADRO);
+    }
+    while (coef.size() % 4) coef.push_back(0.0);
+    plog_par.insert(plog_par.end(), {(double)nt, (double)npr, 0.0, 0.0, r.tcheb[0], r.tcheb[1], r.pcheb[0], r.pcheb[1]});
+    plog_par.insert(plog_par.end(), coef.begin(), coef.end());
+  }
+
   void finish() {
     const int KK = (int)species.size(), MM = (int)elements.size(), II = (int)rx.size();
     ncf.assign((size_t)MM * KK, 0);
@@ -623,6 +663,13 @@ struct Mech {
     for (int i = 0; i < II; ++i) {
       const Reaction& r = rx[i];
       const double es = e_to_kelvin(r.e_units);
+      const bool cheb = !r.cheb.empty(), ltr = r.has_lt || r.has_rlt;
+      if (cheb) cheb_rows(r);
+      if (ltr) {
+        if (r.kind != ELEMENTARY || !r.plog.empty() || cheb)
+          die("LT / RLT on a pressure-dependent or third-body reaction (" + r.equation + ")");
+        if (r.has_rlt && !r.has_rev) die("RLT without REV (" + r.equation + ")");
+      }
       if (!r.plog.empty()) {
         if (r.kind != ELEMENTARY || r.has_rev) die("PLOG on a third-body/falloff reaction or with REV (" + r.equation + ")");
         auto pts = r.plog;
@@ -637,7 +684,9 @@ struct Mech {
       }
       if ((int)r.reac.size() > S || (int)r.prod.size() > S)
         die("more than " + std::to_string(S) + " species on one side of " + r.equation);
-      rtype[i] = !r.plog.empty() ? CKMI_RXN_PLOG : (r.kind == CHEMACT ? CKMI_RXN_CHEMACT : r.kind);
+      rtype[i] = cheb ? CKMI_RXN_CHEB
+                      : ltr ? CKMI_RXN_LT
+                            : !r.plog.empty() ? CKMI_RXN_PLOG : (r.kind == CHEMACT ? CKMI_RXN_CHEMACT : r.kind);
       plog_ptr[i + 1] = (int32_t)(plog_par.size() / 4);
       rev[i] = r.reversible ? 1 : 0;
       nr[i] = (int32_t)r.reac.size();
@@ -659,6 +708,16 @@ struct Mech {
       arr[(size_t)i * 3 + 0] = A > 0 ? std::log(A) : -1e300;
       arr[(size_t)i * 3 + 1] = r.b;
       arr[(size_t)i * 3 + 2] = r.E * es;
+      if (cheb) {  // the rate is the series alone: no [M], no falloff, no efficiencies
+        eff_ptr.push_back((int32_t)eff_sp.size());
+        continue;
+      }
+      if (ltr) {
+        low[(size_t)i * 3 + 0] = r.has_lt ? r.lt[0] : 0.0;
+        low[(size_t)i * 3 + 1] = r.has_lt ? r.lt[1] : 0.0;
+        fpar[(size_t)i * 5 + 0] = r.has_rlt ? r.rlt[0] : 0.0;
+        fpar[(size_t)i * 5 + 1] = r.has_rlt ? r.rlt[1] : 0.0;
+      }
       if (r.kind == FALLOFF || r.kind == CHEMACT) {
         if (r.kind == FALLOFF && !r.has_low) die("falloff reaction without LOW: " + r.equation);
         if (r.kind == CHEMACT && (!r.has_high || r.has_low))

@@ -12,7 +12,9 @@ Supported syntax (Chemkin-II gas phase): ELEMENTS (with optional /weight/), SPEC
 optional THERMO block, REACTIONS with unit keywords, ``=``/``<=>``/``=>``, ``+M``,
 ``(+M)``/``(+species)`` falloff, LOW, TROE (3 or 4 parameters), SRI (3 or 5), REV,
 DUPLICATE, third-body efficiencies, FORD/RORD and non-integral stoichiometric coefficients,
-PLOG (elementary reactions; ln k interpolated in ln P, clamped outside the table).
+PLOG (elementary reactions; ln k interpolated in ln P, clamped outside the table), Chebyshev
+(TCHEB / PCHEB / CHEB on a (+M) reaction; log10 k a double Chebyshev series in the reduced 1/T and
+log P, not clamped outside the fit's range), Landau-Teller (LT, with RLT on REV), per-reaction UNITS.
 """
 from __future__ import annotations
 
@@ -46,6 +48,9 @@ RXN_FALLOFF = 2
 RXN_CHEMACT = 3  # chemically activated (HIGH/): main line = k0, HIGH = k_inf
 TAB_PLOG = 3     # rtype of a PLOG reaction in to_tables() (CKMI_RXN_PLOG in include/ckmi.h)
 TAB_CHEMACT = 4  # rtype of a chemically activated reaction (CKMI_RXN_CHEMACT)
+TAB_CHEB = 5     # rtype of a Chebyshev (T, P) reaction (CKMI_RXN_CHEB)
+TAB_LT = 6       # rtype of a Landau-Teller elementary reaction (CKMI_RXN_LT)
+CHEB_MAX = 12    # Chebyshev orders per dimension the kernels accept
 
 FALL_NONE = 0
 FALL_LINDEMANN = 1
@@ -91,6 +96,11 @@ class Reaction:
     ford: Dict[str, float] = field(default_factory=dict)
     rord: Dict[str, float] = field(default_factory=dict)
     plog: List[Tuple[float, float, float, float]] = field(default_factory=list)
+    cheb: List[float] = field(default_factory=list)  # CHEB values: NT, NP, then NT x NP coefficients
+    tcheb: Optional[Tuple[float, float]] = None      # TCHEB Tmin, Tmax [K] (Chemkin default 300, 2500)
+    pcheb: Optional[Tuple[float, float]] = None      # PCHEB Pmin, Pmax [atm] (default 0.001, 100)
+    lt: Optional[Tuple[float, float]] = None         # LT B, C: k = A T^b exp(-E/RT + B T^-1/3 + C T^-2/3)
+    rlt: Optional[Tuple[float, float]] = None        # RLT B, C of the explicit reverse rate
     E_scale: float = 1.0  # multiply E by this to get E/R [K]
     A_scale_per_order: float = 1.0  # molecules->moles conversion factor base
 
@@ -345,7 +355,8 @@ class Mechanism:
 
     def _reaction_line(self, s: str, current: Optional[Reaction], e_units: str, a_units: str) -> Optional[Reaction]:
         up = s.upper()
-        is_aux = "=" not in s or re.match(r"^\s*(LOW|TROE|SRI|REV|HIGH|FORD|RORD|PLOG|DUP|DUPLICATE|UNITS)\b", up)
+        is_aux = "=" not in s or re.match(
+            r"^\s*(LOW|TROE|SRI|REV|HIGH|FORD|RORD|PLOG|DUP|DUPLICATE|UNITS|CHEB|TCHEB|PCHEB|LT|RLT)\b", up)
         if not is_aux:
             toks = s.split()
             if len(toks) < 4:
@@ -417,6 +428,22 @@ class Mechanism:
                 (current.ford if k == "FORD" else current.rord)[names[parts[0].upper()]] = _to_float(parts[1])
             elif k == "PLOG":
                 current.plog.append(tuple(nums[:4]))
+            elif k == "CHEB":
+                current.cheb.extend(nums)
+            elif k in ("TCHEB", "PCHEB"):
+                if len(nums) != 2:
+                    raise MechanismError(f"{k} needs /min max/: {s!r}")
+                if k == "TCHEB":
+                    current.tcheb = (nums[0], nums[1])
+                else:
+                    current.pcheb = (nums[0], nums[1])
+            elif k in ("LT", "RLT"):
+                if len(nums) != 2:
+                    raise MechanismError(f"{k} needs /B C/: {s!r}")
+                if k == "LT":
+                    current.lt = (nums[0], nums[1])
+                else:
+                    current.rlt = (nums[0], nums[1])
             elif k == "UNITS":
                 # per-reaction units: this reaction's A and E (and its LOW / HIGH / REV / PLOG
                 # parameters) are in them (Chemkin's UNITS auxiliary keyword, e.g. UNITS /KCAL/)
@@ -505,6 +532,33 @@ class Mechanism:
         E = np.array([rx.E * rx.E_scale for rx in self.reactions])
         return A, b, E
 
+    def _cheb_rows(self, rx: Reaction):
+        """plog_par rows of a Chebyshev reaction: (NT, NP, 0, 0), (Tmin, Tmax, Pmin, Pmax) [K, atm],
+        then the NT x NP coefficients of log10 k (temperature-major, 4 per row, zero padded), k in
+        cgs mole units (a MOLECULES-unit reaction shifts a_00 by (order - 1) log10 N_A)."""
+        if rx.kind not in (RXN_FALLOFF,) or rx.third_body != "M":
+            raise MechanismError(f"CHEB needs a (+M) reaction ({rx.equation})")
+        if rx.low is not None or rx.high is not None or rx.troe is not None or rx.sri is not None or rx.plog or \
+                rx.rev is not None:
+            raise MechanismError(f"CHEB with LOW / HIGH / TROE / SRI / PLOG / REV ({rx.equation})")
+        if len(rx.cheb) < 2:
+            raise MechanismError(f"CHEB needs /NT NP/ then the coefficients ({rx.equation})")
+        nt, npr = int(rx.cheb[0]), int(rx.cheb[1])
+        coef = list(rx.cheb[2:])
+        if nt != rx.cheb[0] or npr != rx.cheb[1] or not (1 <= nt <= CHEB_MAX and 1 <= npr <= CHEB_MAX) or \
+                len(coef) != nt * npr:
+            raise MechanismError(f"CHEB needs NT x NP coefficients with 1 <= NT, NP <= {CHEB_MAX} ({rx.equation})")
+        tmin, tmax = rx.tcheb if rx.tcheb is not None else (300.0, 2500.0)
+        pmin, pmax = rx.pcheb if rx.pcheb is not None else (0.001, 100.0)
+        if not (0.0 < tmin < tmax and 0.0 < pmin < pmax):
+            raise MechanismError(f"TCHEB / PCHEB ranges must be positive and increasing ({rx.equation})")
+        if rx.A_scale_per_order != 1.0:
+            coef[0] += (self._order(rx.reactants, 0) - 1.0) * math.log10(AVOGADRO)
+        coef += [0.0] * (-len(coef) % 4)
+        rows = [(float(nt), float(npr), 0.0, 0.0), (tmin, tmax, pmin, pmax)]
+        rows += [tuple(coef[j:j + 4]) for j in range(0, len(coef), 4)]
+        return rows
+
     @staticmethod
     def _order(terms, third_extra: int) -> float:
         return sum(nu for _, nu in terms) + third_extra
@@ -544,9 +598,16 @@ class Mechanism:
         eff_ptr = [0]
         eff_sp: List[int] = []
         eff_val: List[float] = []
-        plog_ptr = np.zeros(II + 1, np.int32)     # CSR into plog_par (rtype TAB_PLOG)
+        plog_ptr = np.zeros(II + 1, np.int32)     # CSR into plog_par (rtype TAB_PLOG; TAB_CHEB rows, _cheb_rows)
         plog_par: List[Tuple[float, float, float, float]] = []  # ln P [dyn/cm2], ln A [cgs], b, E/R
         for i, rx in enumerate(self.reactions):
+            if rx.cheb:
+                plog_par.extend(self._cheb_rows(rx))
+            if rx.lt is not None or rx.rlt is not None:
+                if rx.kind != RXN_ELEMENTARY or rx.plog or rx.cheb:
+                    raise MechanismError(f"LT / RLT on a pressure-dependent or third-body reaction ({rx.equation})")
+                if rx.rlt is not None and rx.rev is None:
+                    raise MechanismError(f"RLT without REV ({rx.equation})")
             if rx.plog:
                 if rx.kind != RXN_ELEMENTARY or rx.rev is not None:
                     raise MechanismError(f"PLOG on a third-body/falloff reaction or with REV ({rx.equation})")
@@ -558,7 +619,12 @@ class Mechanism:
                     plog_par.append((math.log(p_atm * P_ATM), math.log(Ap), b, e * rx.E_scale))
             if len(rx.reactants) > S or len(rx.products) > S:
                 raise MechanismError(f"more than {S} species on one side of {rx.equation}")
-            rtype[i] = TAB_PLOG if rx.plog else (TAB_CHEMACT if rx.kind == RXN_CHEMACT else rx.kind)
+            if rx.cheb:
+                rtype[i] = TAB_CHEB
+            elif rx.lt is not None or rx.rlt is not None:
+                rtype[i] = TAB_LT
+            else:
+                rtype[i] = TAB_PLOG if rx.plog else (TAB_CHEMACT if rx.kind == RXN_CHEMACT else rx.kind)
             plog_ptr[i + 1] = len(plog_par)
             rev[i] = 1 if rx.reversible else 0
             nr[i] = len(rx.reactants)
@@ -574,6 +640,12 @@ class Mechanism:
             extra = 1 if rx.kind == RXN_THIRDBODY else 0
             A = self.A_cgs(i)
             arr[i] = (math.log(A) if A > 0 else -1e300, rx.b, rx.E * rx.E_scale)
+            if rx.cheb:  # the rate is the series alone: no [M], no falloff, no efficiencies
+                eff_ptr.append(len(eff_sp))
+                continue
+            if rx.lt is not None or rx.rlt is not None:
+                low[i, :2] = rx.lt if rx.lt is not None else (0.0, 0.0)
+                fpar[i, :2] = rx.rlt if rx.rlt is not None else (0.0, 0.0)
             if rx.kind in (RXN_FALLOFF, RXN_CHEMACT):
                 if rx.kind == RXN_FALLOFF and rx.low is None:
                     raise MechanismError(f"falloff reaction without LOW: {rx.equation}")

@@ -136,8 +136,7 @@ def test_ford_oracle_jacobian_matches_finite_differences(eq):
     kernels use the same terms) against central differences of the RHS, one reaction at a time (the
     GRI-3.0 species with only that reaction of gri30_ford, none of them third-body), on a CONV state:
     there C_k = rho Y_k / W_k at fixed rho, so the approximate Chemkin Jacobian is exact in the species
-    rows.  For an order o < 1 the Jacobian carries the chord slope C^(o-1) instead of the tangent
-    o C^(o-1) (oracle/ckoracle.c dconc_pow): that column is the finite difference divided by o."""
+    rows (the states here are far above the 1e-14 mol/cm3 chord floor, so the tangent applies)."""
     from oracle.oracle import Oracle
 
     import re
@@ -169,8 +168,6 @@ def test_ford_oracle_jacobian_matches_finite_differences(eq):
         yp[col] += h
         ym[col] -= h
         fd = (orc.rhs_jac(yp, **kw)[0] - orc.rhs_jac(ym, **kw)[0]) / (2 * h)
-        if order < 1.0:
-            fd /= order
         sc = np.max(np.abs(fd[1:]))
         assert sc > 0
         assert np.max(np.abs(J[1:, col] - fd[1:])) < 1e-5 * sc, sp
@@ -205,13 +202,13 @@ def test_fractional_order_rule_near_zero(fmech, forc):
 def test_ford_reactor_robust_to_tolerance_perturbation(fmech, forc):
     """Round 2's stall: under rounding-level changes the integrator locked its step at a species
     running out with an order < 1 (period-2 corrector cycle at C ~ 0) and hit max steps (5 of 35 runs
-    here).  With the chord rule every case at every tolerance finishes in a few thousand steps."""
+    here).  With the Lipschitz chord rule every case at every tolerance finishes in under 2,000 steps."""
     cases = [(1200, 1, 1.0, 1), (1400, 10, 1.0, 2), (1100, 0.5, 0.7, 1), (1600, 50, 1.5, 1), (1300, 30, 0.5, 2)]
     for rt in (1e-8, 1.01e-8, 0.99e-8, 1.03e-8, 0.97e-8, 1e-7, 1e-9):
         for T0, p, phi, prob in cases:
             r, _ = forc.reactor(float(T0), p * P_ATM, 1.0, ch4_air_Y(fmech, phi)[0], problem=prob, energy=1,
                                 t_end=1.0, atol=1e-10, rtol=rt, ign_mode="TIFP")
-            assert r.status == 0 and r.nst < 4000 and r.ncf < 10, (T0, p, phi, prob, rt, r.nst, r.ncf)
+            assert r.status == 0 and r.nst < 2500 and r.ncf < 10, (T0, p, phi, prob, rt, r.nst, r.ncf)
 
 
 def test_ford_changes_ignition(fmech, forc, oracle, mech):

@@ -1,0 +1,92 @@
+"""Every reaction form the small-mechanism kernels support, in batch reactors with more than 63
+species (the workgroup-per-reactor kernel's extended variant, ckmi_big.hip big_reactor_kernel<NB,
+true>): PLOG, chemically activated (HIGH/), FORD / RORD orders and non-integral coefficients.
+
+Round 2 rejected all of these above 63 species.  Mechanism: data/gri30_tracer161_ext_chem.inp
+(data/make_big_ext_mechanism.py: the 161-species stand-in with the PLOG / HIGH / FORD
+transformations of the GRI-3.0 stand-ins plus tracer-side PLOG, FORD, HIGH and fractional
+reactions whose species indices exceed 63).  Parity with Chemkin is unpinned (no golden uses these
+forms at this size); the checker is the oracle's BDF on the same inputs, at the north_star bar
+held to 1e-4 (tau, final T, major species)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import P_ATM, ROOT
+
+pytestmark = pytest.mark.gpu
+
+CHEM = os.path.join(ROOT, "data", "gri30_tracer161_ext_chem.inp")
+THERM = os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat")
+MAJOR = ("CH4", "O2", "N2", "H2O", "CO2", "CO", "H2", "AX1")
+
+
+@pytest.fixture(scope="module")
+def ext():
+    from oracle.oracle import Oracle
+    from pychemkin_amd import _native
+    from pychemkin_amd.mechanism import Mechanism
+
+    m = Mechanism.from_files(CHEM, THERM)
+    return m, Oracle(m), _native.DeviceMechanism(m.to_tables())
+
+
+def _Y(mech, phi, frac=0.2):
+    X = np.zeros((len(phi), mech.KK))
+    X[:, mech.species.index("CH4")] = phi
+    X[:, mech.species.index("O2")] = 2.0
+    X[:, mech.species.index("N2")] = 7.52 * (1.0 - frac)
+    # the tracer charge spread over the species the extended reactions touch
+    for sp, w in (("AX1", 0.5), ("AX20", 0.1), ("AX40", 0.1), ("AX90", 0.1), ("AX91", 0.1), ("AX100", 0.05),
+                  ("AX101", 0.05)):
+        X[:, mech.species.index(sp)] = 7.52 * frac * w
+    Y = X * mech.wt
+    return Y / Y.sum(axis=1, keepdims=True)
+
+
+def test_extended_big_mechanism_tables(ext):
+    mech, _, _ = ext
+    t = mech.to_tables()
+    assert mech.KK == 161 and (t["rtype"] == 3).sum() == 8 and (t["rtype"] == 4).sum() == 4
+    assert np.any(t["ford"] != t["rnu"])
+
+
+@pytest.mark.parametrize("problem", [1, 2])
+def test_extended_big_reactors_match_oracle(ext, problem):
+    from pychemkin_amd import _native
+
+    mech, orc, dm = ext
+    rng = np.random.default_rng(5 + problem)
+    n = 8
+    T0 = rng.uniform(1250.0, 1650.0, n)
+    P0 = P_ATM * rng.uniform(0.5, 60.0, n)  # PLOG tables span 0.01-100 atm
+    phi = rng.uniform(0.5, 1.5, n)
+    Y0 = _Y(mech, phi)
+    prob = np.full(n, problem, np.int32)
+    run = dict(energy=1, t_end=0.02, atol=1e-10, rtol=1e-8, ign_mode="TIFP")
+    res = {k: v.cpu().numpy() for k, v in dm.reactor_run(_native.make_cfg(**run), prob, T0, P0, np.ones(n),
+                                                          Y0).items() if not k.startswith("_")}
+    for i in range(n):
+        r, Ye = orc.reactor(T0[i], P0[i], 1.0, Y0[i], problem=problem, **run)
+        assert r.status == 0 and res["stats"][i, 6] == 0, (i, res["stats"][i].tolist())
+        assert r.tau > 0 and abs(res["tau"][i] / r.tau - 1) < 1e-4, (i, res["tau"][i], r.tau)
+        assert abs(res["T"][i] / r.T - 1) < 1e-4
+        for sp in MAJOR + ("AX21", "AX41", "AX92", "AX102"):
+            k = mech.species.index(sp)
+            assert abs(res["Y"][i, k] - Ye[k]) <= 1e-4 * max(abs(Ye[k]), 1e-3), (i, sp)
+        assert abs(res["Y"][i].sum() - 1.0) < 1e-8
+
+
+def test_extended_big_rop_matches_oracle(ext):
+    """ROP of the extended mechanism (the generic kernel's extended variant) against the oracle."""
+    mech, orc, dm = ext
+    rng = np.random.default_rng(3)
+    n = 64
+    T = rng.uniform(600.0, 2600.0, n)
+    P = P_ATM * 10.0 ** rng.uniform(-1.5, 2.0, n)
+    Y = rng.dirichlet(np.ones(mech.KK), n).T.copy()
+    w = dm.rop_thermo(T, P, Y)[0].cpu().numpy()
+    wo = orc.rop_batch(T, P, Y)[0]
+    err = np.max(np.abs(w - wo) / np.max(np.abs(wo), axis=0, keepdims=True))
+    assert err < 1e-11

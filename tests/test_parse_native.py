@@ -13,7 +13,8 @@ from conftest import ROOT
 
 DATA = os.path.join(ROOT, "data")
 MECHS = [("grimech30_chem.inp", "grimech30_thermo.dat"), ("gri30_ford_chem.inp", "grimech30_thermo.dat"),
-         ("gri30_plog_chem.inp", "grimech30_thermo.dat"), ("gri30_tracer161_chem.inp", "gri30_tracer161_thermo.dat")]
+         ("gri30_plog_chem.inp", "grimech30_thermo.dat"), ("gri30_tracer161_chem.inp", "gri30_tracer161_thermo.dat"),
+         ("gri30_cheb_chem.inp", "grimech30_thermo.dat"), ("gri30_tracer161_ext_chem.inp", "gri30_tracer161_thermo.dat")]
 
 
 def _read(name):
@@ -108,7 +109,7 @@ def test_reactions_line_units_and_abbreviations():
 BAD = {
     "unknown species": MINI.replace("O+H2<=>H+OH", "O+H3<=>H+OH"),
     "not element balanced": MINI.replace("O+H2<=>H+OH", "O+H2<=>H+H2O"),
-    "unknown auxiliary keyword": MINI.replace("H2/ .73/", "CHEB/ 7 3 /\nH2/ .73/"),
+    "unknown auxiliary keyword": MINI.replace("H2/ .73/", "EXCI/ 7 3 /\nH2/ .73/"),
     "UNITS": MINI.replace("H2/ .73/", "UNITS /FURLONGS/\nH2/ .73/"),
     "efficiency on a reaction without": MINI.replace("O+H2<=>H+OH                              3.870E+04    2.700    6260.00",
                                                      "O+H2<=>H+OH                              3.870E+04    2.700    6260.00\nH2O/2.0/"),
