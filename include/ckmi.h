@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define CKMI_SLOTS 4 /* distinct species per reaction side in the flat tables */
+#define CKMI_SLOTS 8 /* distinct species per reaction side in the flat tables ([II][CKMI_SLOTS] arrays) */
 
 /* reaction types */
 #define CKMI_RXN_ELEMENTARY 0
@@ -76,10 +76,10 @@ typedef struct {
   const int32_t* rev;     /* [II] 1 reversible */
   const int32_t* nr;      /* [II] reactant slots used */
   const int32_t* np;      /* [II] product slots used */
-  const int32_t* rsp;     /* [II][4] reactant species */
-  const int32_t* psp;     /* [II][4] product species */
-  const double* rnu;      /* [II][4] reactant stoichiometric coefficients */
-  const double* pnu;      /* [II][4] product stoichiometric coefficients */
+  const int32_t* rsp;     /* [II][CKMI_SLOTS] reactant species */
+  const int32_t* psp;     /* [II][CKMI_SLOTS] product species */
+  const double* rnu;      /* [II][CKMI_SLOTS] reactant stoichiometric coefficients */
+  const double* pnu;      /* [II][CKMI_SLOTS] product stoichiometric coefficients */
   const double* arr;      /* [II][3] ln A (cgs), b, E/R (K) */
   const double* low;      /* [II][3] falloff low-pressure limit */
   const double* revp;     /* [II][3] explicit reverse parameters (REV) */
@@ -92,8 +92,8 @@ typedef struct {
   const double* eff_val;  /* third-body efficiencies (absolute) */
   const int32_t* plog_ptr; /* [II+1] CSR into plog_par for CKMI_RXN_PLOG reactions (may be NULL if none) */
   const double* plog_par;  /* [npl][4] ln P (dyn/cm2), ln A (cgs), b, E/R (K); ascending, distinct P */
-  const double* ford;      /* [II][4] forward order of each reactant slot (FORD; = rnu without it), or NULL */
-  const double* rord;      /* [II][4] reverse order of each product slot (RORD; = pnu without it), or NULL */
+  const double* ford;      /* [II][CKMI_SLOTS] forward order of each reactant slot (FORD; = rnu without it), or NULL */
+  const double* rord;      /* [II][CKMI_SLOTS] reverse order of each product slot (RORD; = pnu without it), or NULL */
 } ckmi_mech_desc;
 
 typedef struct ckmi_mech ckmi_mech; /* opaque: tables resident in HBM of one device */

@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define CKO_SLOTS 4
+#define CKO_SLOTS 8 /* = CKMI_SLOTS: distinct species per reaction side */
 
 typedef struct {
   int KK, II;

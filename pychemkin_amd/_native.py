@@ -120,19 +120,21 @@ def _check(rc: int, what: str) -> None:
         raise NativeError(f"{what} failed (code {rc}): {msg}")
 
 
+SLOTS = 8  # CKMI_SLOTS (include/ckmi.h): distinct species per reaction side of the flat tables
+
 # ckmi_mech_desc fields -> (dtype, shape given KK, II, npl)
 _DESC_LAYOUT = {
     "wt": (np.float64, lambda K, I, n: (K,)), "thermo": (np.float64, lambda K, I, n: (K, 17)),
     "rtype": (np.int32, lambda K, I, n: (I,)), "rev": (np.int32, lambda K, I, n: (I,)),
     "nr": (np.int32, lambda K, I, n: (I,)), "np": (np.int32, lambda K, I, n: (I,)),
-    "rsp": (np.int32, lambda K, I, n: (I, 4)), "psp": (np.int32, lambda K, I, n: (I, 4)),
-    "rnu": (np.float64, lambda K, I, n: (I, 4)), "pnu": (np.float64, lambda K, I, n: (I, 4)),
+    "rsp": (np.int32, lambda K, I, n: (I, SLOTS)), "psp": (np.int32, lambda K, I, n: (I, SLOTS)),
+    "rnu": (np.float64, lambda K, I, n: (I, SLOTS)), "pnu": (np.float64, lambda K, I, n: (I, SLOTS)),
     "arr": (np.float64, lambda K, I, n: (I, 3)), "low": (np.float64, lambda K, I, n: (I, 3)),
     "revp": (np.float64, lambda K, I, n: (I, 3)), "has_rev": (np.int32, lambda K, I, n: (I,)),
     "ftype": (np.int32, lambda K, I, n: (I,)), "fpar": (np.float64, lambda K, I, n: (I, 5)),
     "tbsp": (np.int32, lambda K, I, n: (I,)), "eff_ptr": (np.int32, lambda K, I, n: (I + 1,)),
     "plog_ptr": (np.int32, lambda K, I, n: (I + 1,)),
-    "ford": (np.float64, lambda K, I, n: (I, 4)), "rord": (np.float64, lambda K, I, n: (I, 4)),
+    "ford": (np.float64, lambda K, I, n: (I, SLOTS)), "rord": (np.float64, lambda K, I, n: (I, SLOTS)),
 }
 
 

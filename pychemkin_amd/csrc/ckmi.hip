@@ -954,7 +954,7 @@ __global__ __launch_bounds__(rop_waves(NCH)* WAVE) void rop_kernel(MechImage img
             } else {
               const double q = qf - qr;
               for (int u = 0; u < (int)g[0]; ++u) atomicAdd(&wdot[(int)g[2 + 3 * u]], -g[3 + 3 * u] * q);
-              for (int u = 0; u < (int)g[1]; ++u) atomicAdd(&wdot[(int)g[14 + 3 * u]], g[15 + 3 * u] * q);
+              for (int u = 0; u < (int)g[1]; ++u) atomicAdd(&wdot[(int)g[GEN_P + 3 * u]], g[GEN_P + 1 + 3 * u] * q);
             }
             continue;
           }
@@ -1125,14 +1125,14 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
         const int i = slots[s];
         double grec[GEN_RECORDS * AUXW] = {(double)nr, (double)np};
         for (int u = 0; u < nr; ++u) {
-          grec[2 + 3 * u] = d->rsp[4 * i + u];
-          grec[3 + 3 * u] = d->rnu[4 * i + u];
-          grec[4 + 3 * u] = d->ford ? d->ford[4 * i + u] : d->rnu[4 * i + u];
+          grec[2 + 3 * u] = d->rsp[CKMI_SLOTS * i + u];
+          grec[3 + 3 * u] = d->rnu[CKMI_SLOTS * i + u];
+          grec[4 + 3 * u] = d->ford ? d->ford[CKMI_SLOTS * i + u] : d->rnu[CKMI_SLOTS * i + u];
         }
         for (int u = 0; u < np; ++u) {
-          grec[14 + 3 * u] = d->psp[4 * i + u];
-          grec[15 + 3 * u] = d->pnu[4 * i + u];
-          grec[16 + 3 * u] = d->rord ? d->rord[4 * i + u] : d->pnu[4 * i + u];
+          grec[GEN_P + 3 * u] = d->psp[CKMI_SLOTS * i + u];
+          grec[GEN_P + 1 + 3 * u] = d->pnu[CKMI_SLOTS * i + u];
+          grec[GEN_P + 2 + 3 * u] = d->rord ? d->rord[CKMI_SLOTS * i + u] : d->pnu[CKMI_SLOTS * i + u];
         }
         aux.insert(aux.end(), grec, grec + GEN_RECORDS * AUXW);
         naux += GEN_RECORDS;
@@ -1390,8 +1390,8 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   auto slot_class = [&](int i) -> int {
     if (rxn_general(d, i)) return 2;
     double ur = 0.0, up = 0.0;
-    for (int u = 0; u < d->nr[i]; ++u) ur += d->rnu[4 * i + u];
-    for (int u = 0; u < d->np[i]; ++u) up += d->pnu[4 * i + u];
+    for (int u = 0; u < d->nr[i]; ++u) ur += d->rnu[CKMI_SLOTS * i + u];
+    for (int u = 0; u < d->np[i]; ++u) up += d->pnu[CKMI_SLOTS * i + u];
     return (ur > 2.0 || up > 2.0) ? 1 : 0;
   };
   for (int t : {CKMI_RXN_ELEMENTARY, CKMI_RXN_LT, CKMI_RXN_THIRDBODY, CKMI_RXN_FALLOFF, CKMI_RXN_CHEMACT, CKMI_RXN_PLOG,
@@ -1490,33 +1490,38 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
                     "FORD / RORD or non-integral coefficients on a PLOG, Chebyshev or Landau-Teller reaction");
       }
       for (int u = 0; u < nr; ++u)
-        if (!(d->rnu[i * SLOTS + u] > 0.0) || (d->ford && d->ford[i * SLOTS + u] < 0.0)) {
+        if (!(d->rnu[i * CKMI_SLOTS + u] > 0.0) || (d->ford && d->ford[i * CKMI_SLOTS + u] < 0.0)) {
           delete m;
           return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficients must be > 0 and orders >= 0");
         }
       for (int u = 0; u < np; ++u)
-        if (!(d->pnu[i * SLOTS + u] > 0.0) || (d->rord && d->rord[i * SLOTS + u] < 0.0)) {
+        if (!(d->pnu[i * CKMI_SLOTS + u] > 0.0) || (d->rord && d->rord[i * CKMI_SLOTS + u] < 0.0)) {
           delete m;
           return fail(CKMI_ERR_UNSUPPORTED, "stoichiometric coefficients must be > 0 and orders >= 0");
         }
       flags[s] |= RX_GEN;
     }
-    if (nr > SLOTS || np > SLOTS) {
+    if (nr > GEN_SLOTS || np > GEN_SLOTS || ((nr > SLOTS || np > SLOTS) && !(flags[s] & RX_GEN))) {
       delete m;
-      return fail(CKMI_ERR_UNSUPPORTED, "more than 4 species on a reaction side");
+      return fail(CKMI_ERR_UNSUPPORTED, "more than 8 species on a reaction side");
     }
     nrp[s] = nr | (np << 8);
     int rr[4] = {0, 0, 0, 0}, pp[4] = {0, 0, 0, 0};
     double sf = 0.0, sr = 0.0;
+    // per-slot device arrays hold the first SLOTS species (a general reaction reads its aux stream)
     for (int u = 0; u < nr; ++u) {
-      rr[u] = d->rsp[i * SLOTS + u];
-      rnu[u * IIpad + s] = d->rnu[i * SLOTS + u];
-      sf += d->rnu[i * SLOTS + u];
+      if (u < SLOTS) {
+        rr[u] = d->rsp[i * CKMI_SLOTS + u];
+        rnu[u * IIpad + s] = d->rnu[i * CKMI_SLOTS + u];
+      }
+      sf += d->rnu[i * CKMI_SLOTS + u];
     }
     for (int u = 0; u < np; ++u) {
-      pp[u] = d->psp[i * SLOTS + u];
-      pnu[u * IIpad + s] = d->pnu[i * SLOTS + u];
-      sr += d->pnu[i * SLOTS + u];
+      if (u < SLOTS) {
+        pp[u] = d->psp[i * CKMI_SLOTS + u];
+        pnu[u * IIpad + s] = d->pnu[i * CKMI_SLOTS + u];
+      }
+      sr += d->pnu[i * CKMI_SLOTS + u];
     }
     rsp[s] = make_int4(rr[0], rr[1], rr[2], rr[3]);
     psp[s] = make_int4(pp[0], pp[1], pp[2], pp[3]);

@@ -47,7 +47,7 @@ constexpr int BW = 4;           // waves per workgroup
 constexpr int NT = BW * WAVE;   // threads: state component / matrix row per thread
 constexpr int BIG_NMAX = 192;   // n = KK + 1 <= 192
 constexpr int RED_SET = 16;     // doubles per reduction set (two sets alternate)
-constexpr int NDQ = 8;          // dq/dC slots per reaction: 4 reactant + 4 product
+constexpr int NDQ = 16;         // dq/dC slots per reaction: unit reactions 4 + 4, general ones GEN_SLOTS + GEN_SLOTS
 
 // Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py --big): per-reactor shader
 // cycles per phase into a debug buffer [n][8]: rhs, rhs+J, build, factor, solve, total, -, -.
@@ -726,7 +726,7 @@ using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB>, BigMatrix<NB>>;
 // the reaction keeps no unit slots, its species, coefficients and orders are in the aux stream
 // (eval_gen_img).  RHS: q scattered with the real coefficients into this wave's wdot copy; with
 // the Jacobian, dwdot/dT through the orders and dq/dC of each slot (the chord rule of dconc_pow)
-// into the reaction's 8 Dg slots (reactant slots 0..3, product slots 4..7), as oracle reactor_rhs.
+// into the reaction's Dg slots (reactants 0..GEN_SLOTS-1, products GEN_SLOTS..), as oracle reactor_rhs.
 __device__ __noinline__ void gen_rhs_big(const MechView& V, const RunCtx& R, int i, uint32_t inf, double T,
                                          double lnT, double invT, double lnPRT, double P, const double* C,
                                          const double* gRT, const double* hRT, const double* Mg, double* wdw,
@@ -737,23 +737,23 @@ __device__ __noinline__ void gen_rhs_big(const MechView& V, const RunCtx& R, int
   const int nr = (int)g[0], np = (int)g[1];
   const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
   for (int u = 0; u < nr; ++u) atomicAdd(&wdw[(int)g[2 + 3 * u]], -g[3 + 3 * u] * q);
-  for (int u = 0; u < np; ++u) atomicAdd(&wdw[(int)g[14 + 3 * u]], g[15 + 3 * u] * q);
+  for (int u = 0; u < np; ++u) atomicAdd(&wdw[(int)g[GEN_P + 3 * u]], g[GEN_P + 1 + 3 * u] * q);
   if (!with_j) return;
   double dqdT = e.mfac * (e.kf * e.dlkf * e.pf - e.kr * e.dlkr * e.pr);
   if (conp) {
     double of = 0.0, orr = 0.0;
     for (int u = 0; u < nr; ++u) of += g[4 + 3 * u];
-    for (int u = 0; u < np; ++u) orr += g[16 + 3 * u];
+    for (int u = 0; u < np; ++u) orr += g[GEN_P + 2 + 3 * u];
     dqdT -= e.mfac * (of * e.kf * e.pf - orr * e.kr * e.pr) * invT;
     if (rx_type(inf) == 1) dqdT -= q * invT;
   }
   for (int u = 0; u < nr; ++u) atomicAdd(&dwdw[(int)g[2 + 3 * u]], -g[3 + 3 * u] * dqdT);
-  for (int u = 0; u < np; ++u) atomicAdd(&dwdw[(int)g[14 + 3 * u]], g[15 + 3 * u] * dqdT);
+  for (int u = 0; u < np; ++u) atomicAdd(&dwdw[(int)g[GEN_P + 3 * u]], g[GEN_P + 1 + 3 * u] * dqdT);
   for (int side = 0; side < 2; ++side) {
     const int ns = side == 0 ? nr : np;
-    const double* sl = g + (side == 0 ? 2 : 14);
+    const double* sl = g + (side == 0 ? 2 : GEN_P);
     const double kk = side == 0 ? e.mfac * e.kf : -e.mfac * e.kr;
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < GEN_SLOTS; ++s) {
       double d = 0.0;
       if (s < ns && kk != 0.0) {
         d = dconc_pow(C[(int)sl[3 * s]], sl[3 * s + 2], e2t);
@@ -761,7 +761,7 @@ __device__ __noinline__ void gen_rhs_big(const MechView& V, const RunCtx& R, int
           if (u != s) d *= conc_pow(C[(int)sl[3 * u]], sl[3 * u + 2], e2t);
         d *= kk;
       }
-      Dg[(4 * side + s) * IIp + i] = d;
+      Dg[(GEN_SLOTS * side + s) * IIp + i] = d;
     }
   }
 }
@@ -771,11 +771,11 @@ __device__ __noinline__ void gen_jac_cols_big(const MechView& V, int i, uint32_t
                                               int IIp, double* jb, int c0, int lo, int hi, int LDJ) {
   const double* g = V.aux() + AUXW * (rx_aux(inf) + 1);
   const int nr = (int)g[0], np = (int)g[1];
-  for (int sl = 0; sl < 8; ++sl) {
-    const bool prod = sl >= 4;
-    const int u0 = sl & 3;
+  for (int sl = 0; sl < 2 * GEN_SLOTS; ++sl) {
+    const bool prod = sl >= GEN_SLOTS;
+    const int u0 = sl % GEN_SLOTS;
     if (u0 >= (prod ? np : nr)) continue;
-    const int j = (int)g[(prod ? 14 : 2) + 3 * u0];
+    const int j = (int)g[(prod ? GEN_P : 2) + 3 * u0];
     const int col = 1 + j;
     if (col < lo || col >= hi) continue;
     const double dqw = Dg[sl * IIp + i] * V.rwt()[j];
@@ -785,8 +785,8 @@ __device__ __noinline__ void gen_jac_cols_big(const MechView& V, int i, uint32_t
       atomicAdd(&jc[k], -g[3 + 3 * u] * dqw * V.wt()[k]);
     }
     for (int u = 0; u < np; ++u) {
-      const int k = (int)g[14 + 3 * u];
-      atomicAdd(&jc[k], g[15 + 3 * u] * dqw * V.wt()[k]);
+      const int k = (int)g[GEN_P + 3 * u];
+      atomicAdd(&jc[k], g[GEN_P + 1 + 3 * u] * dqw * V.wt()[k]);
     }
   }
 }

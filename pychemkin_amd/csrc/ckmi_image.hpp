@@ -350,9 +350,11 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
 // FORD / RORD orders or non-integral stoichiometric coefficients (extended kernel variants only).
 // Such a reaction keeps empty unit slots (nr = np = 0, so the unit-slot code skips it), carries
 // info bit 14 and an aux stream after its own record (record rx_aux + 1 on):
-//   nr, np, then (species, nu, order) for 4 reactant slots and for 4 product slots.
+//   nr, np, then (species, nu, order) for GEN_SLOTS reactant slots and GEN_SLOTS product slots.
 constexpr uint32_t RX_GEN = 0x4000u;
-constexpr int GEN_RECORDS = 3;  // 2 + 24 doubles
+constexpr int GEN_SLOTS = 8;                                  // species per side of a general reaction
+constexpr int GEN_P = 2 + 3 * GEN_SLOTS;                        // first product slot of the aux stream
+constexpr int GEN_RECORDS = (2 + 6 * GEN_SLOTS + 11) / 12;      // 2 + 48 doubles in AUXW records
 
 // C^o for a reaction order o, the rule of oracle/ckoracle.c conc_pow: exact products for
 // o = 0..3; for 0 < o < 1 C^o above CONC_FLOOR and the chord CONC_FLOOR^(o-1) C below it (negative
@@ -396,7 +398,7 @@ __device__ __forceinline__ Rxn eval_gen_img(const MechView& V, int i, uint32_t i
   const int nr = (int)g[0], np = (int)g[1];
   double pf = 1.0, pr = 1.0, dG = 0.0, dH = 0.0, dnu = 0.0;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
+  for (int u = 0; u < GEN_SLOTS; ++u) {
     if (u < nr) {
       const int k = (int)g[2 + 3 * u];
       const double nu = g[3 + 3 * u];
@@ -406,9 +408,9 @@ __device__ __forceinline__ Rxn eval_gen_img(const MechView& V, int i, uint32_t i
       dnu -= nu;
     }
     if (u < np) {
-      const int k = (int)g[14 + 3 * u];
-      const double nu = g[15 + 3 * u];
-      pr *= conc_pow(C[k], g[16 + 3 * u], e2t);
+      const int k = (int)g[GEN_P + 3 * u];
+      const double nu = g[GEN_P + 1 + 3 * u];
+      pr *= conc_pow(C[k], g[GEN_P + 2 + 3 * u], e2t);
       dG += nu * gRT[k];
       if (need_h) dH += nu * hRT[k];
       dnu += nu;

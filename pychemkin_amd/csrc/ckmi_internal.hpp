@@ -43,18 +43,18 @@ inline const char* check_slots(const ckmi_mech_desc* d) {
 inline bool rxn_general(const ckmi_mech_desc* d, int i) {
   int mr = 0, mp = 0;
   for (int u = 0; u < d->nr[i]; ++u) {
-    const double nu = d->rnu[4 * i + u];
+    const double nu = d->rnu[CKMI_SLOTS * i + u];
     if (nu != (double)(int)nu || nu < 1.0) return true;
-    if (d->ford && d->ford[4 * i + u] != nu) return true;
+    if (d->ford && d->ford[CKMI_SLOTS * i + u] != nu) return true;
     mr += (int)nu;
   }
   for (int u = 0; u < d->np[i]; ++u) {
-    const double nu = d->pnu[4 * i + u];
+    const double nu = d->pnu[CKMI_SLOTS * i + u];
     if (nu != (double)(int)nu || nu < 1.0) return true;
-    if (d->rord && d->rord[4 * i + u] != nu) return true;
+    if (d->rord && d->rord[CKMI_SLOTS * i + u] != nu) return true;
     mp += (int)nu;
   }
-  return mr > 4 || mp > 4;
+  return mr > 4 || mp > 4 || d->nr[i] > 4 || d->np[i] > 4;
 }
 bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<double>& prm, std::vector<int>& lnA_off,
                       std::string& why);

@@ -149,9 +149,9 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
   std::vector<std::vector<int>> rs(II), ps(II), used(II);
   for (int i = 0; i < II; ++i) {
     for (int u = 0; u < d->nr[i]; ++u)
-      for (int c = 0; c < (int)std::lround(d->rnu[4 * i + u]); ++c) rs[i].push_back(d->rsp[4 * i + u]);
+      for (int c = 0; c < (int)std::lround(d->rnu[CKMI_SLOTS * i + u]); ++c) rs[i].push_back(d->rsp[CKMI_SLOTS * i + u]);
     for (int u = 0; u < d->np[i]; ++u)
-      for (int c = 0; c < (int)std::lround(d->pnu[4 * i + u]); ++c) ps[i].push_back(d->psp[4 * i + u]);
+      for (int c = 0; c < (int)std::lround(d->pnu[CKMI_SLOTS * i + u]); ++c) ps[i].push_back(d->psp[CKMI_SLOTS * i + u]);
     std::vector<int> u = rs[i];
     u.insert(u.end(), ps[i].begin(), ps[i].end());
     if (d->rtype[i] == CKMI_RXN_FALLOFF && d->tbsp[i] >= 0) u.push_back(d->tbsp[i]);

@@ -132,15 +132,15 @@ __device__ __noinline__ void gen_jac_terms(const MechView& V, const RunCtx& R, i
   if (conp) {
     double of = 0.0, orr = 0.0;
     for (int u = 0; u < nr; ++u) of += g[4 + 3 * u];
-    for (int u = 0; u < np; ++u) orr += g[16 + 3 * u];
+    for (int u = 0; u < np; ++u) orr += g[GEN_P + 2 + 3 * u];
     dqdT -= e.mfac * (of * e.kf * e.pf - orr * e.kr * e.pr) * invT;
     if (rx_type(inf) == 1) dqdT -= q * invT;
   }
   for (int u = 0; u < nr; ++u) atomicAdd(&L.dwdT()[(int)g[2 + 3 * u]], -g[3 + 3 * u] * dqdT);
-  for (int u = 0; u < np; ++u) atomicAdd(&L.dwdT()[(int)g[14 + 3 * u]], g[15 + 3 * u] * dqdT);
+  for (int u = 0; u < np; ++u) atomicAdd(&L.dwdT()[(int)g[GEN_P + 3 * u]], g[GEN_P + 1 + 3 * u] * dqdT);
   for (int side = 0; side < 2; ++side) {
     const int ns = side == 0 ? nr : np;
-    const double* sl = g + (side == 0 ? 2 : 14);
+    const double* sl = g + (side == 0 ? 2 : GEN_P);
     const double kk = side == 0 ? e.mfac * e.kf : -e.mfac * e.kr;
     if (kk == 0.0) continue;
     for (int s = 0; s < ns; ++s) {
@@ -151,7 +151,7 @@ __device__ __noinline__ void gen_jac_terms(const MechView& V, const RunCtx& R, i
       const double dqw = kk * d * V.rwt()[j];
       double* col = lds_at<double>(oJ) + (1 + j) * LDJ + 1;
       for (int u = 0; u < nr; ++u) atomicAdd(&col[(int)g[2 + 3 * u]], -g[3 + 3 * u] * dqw * V.wt()[(int)g[2 + 3 * u]]);
-      for (int u = 0; u < np; ++u) atomicAdd(&col[(int)g[14 + 3 * u]], g[15 + 3 * u] * dqw * V.wt()[(int)g[14 + 3 * u]]);
+      for (int u = 0; u < np; ++u) atomicAdd(&col[(int)g[GEN_P + 3 * u]], g[GEN_P + 1 + 3 * u] * dqw * V.wt()[(int)g[GEN_P + 3 * u]]);
     }
   }
 }
@@ -259,9 +259,9 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
                                    R.plnf, R.gfac, g);
         const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < GEN_SLOTS; ++u) {
           if (u < (int)g[0]) atomicAdd(&L.wdot()[(int)g[2 + 3 * u]], -g[3 + 3 * u] * q);
-          if (u < (int)g[1]) atomicAdd(&L.wdot()[(int)g[14 + 3 * u]], g[15 + 3 * u] * q);
+          if (u < (int)g[1]) atomicAdd(&L.wdot()[(int)g[GEN_P + 3 * u]], g[GEN_P + 1 + 3 * u] * q);
         }
       }
     }

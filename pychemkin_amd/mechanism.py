@@ -58,7 +58,7 @@ FALL_TROE3 = 2
 FALL_TROE4 = 3
 FALL_SRI = 4
 
-MAX_SLOTS = 4  # distinct species per reaction side on the device tables
+MAX_SLOTS = 8  # distinct species per reaction side in the flat tables (CKMI_SLOTS in include/ckmi.h)
 
 # Gas constant of the activation-energy conversion.  Chemkin's interpreter converts E of the
 # REACTIONS block with its own RU = 8.314510e7 erg/mol-K (RUC = RU / 4.184e7 = 1.98721558

@@ -1,6 +1,7 @@
 """Every reaction form the small-mechanism kernels support, in batch reactors with more than 63
 species (the workgroup-per-reactor kernel's extended variant, ckmi_big.hip big_reactor_kernel<NB,
-true>): PLOG, chemically activated (HIGH/), FORD / RORD orders and non-integral coefficients.
+true>): PLOG, chemically activated (HIGH/), FORD / RORD orders, non-integral coefficients and reactions
+with 5-8 distinct species on a side.
 
 Round 2 rejected all of these above 63 species.  Mechanism: data/gri30_tracer161_ext_chem.inp
 (data/make_big_ext_mechanism.py: the 161-species stand-in with the PLOG / HIGH / FORD
@@ -38,8 +39,9 @@ def _Y(mech, phi, frac=0.2):
     X[:, mech.species.index("O2")] = 2.0
     X[:, mech.species.index("N2")] = 7.52 * (1.0 - frac)
     # the tracer charge spread over the species the extended reactions touch
-    for sp, w in (("AX1", 0.5), ("AX20", 0.1), ("AX40", 0.1), ("AX90", 0.1), ("AX91", 0.1), ("AX100", 0.05),
-                  ("AX101", 0.05)):
+    wide = tuple((f"AX{k}", 0.02) for k in (60, 61, 62, 63, 64, 70, 71, 72, 73, 74))
+    for sp, w in (("AX1", 0.3), ("AX20", 0.1), ("AX40", 0.1), ("AX90", 0.1), ("AX91", 0.1), ("AX100", 0.05),
+                  ("AX101", 0.05)) + wide:
         X[:, mech.species.index(sp)] = 7.52 * frac * w
     Y = X * mech.wt
     return Y / Y.sum(axis=1, keepdims=True)
@@ -50,6 +52,7 @@ def test_extended_big_mechanism_tables(ext):
     t = mech.to_tables()
     assert mech.KK == 161 and (t["rtype"] == 3).sum() == 8 and (t["rtype"] == 4).sum() == 4
     assert np.any(t["ford"] != t["rnu"])
+    assert t["nr"].max() == 6 and t["np"].max() == 6  # the wide tracer reactions (CKMI_SLOTS = 8)
 
 
 @pytest.mark.parametrize("problem", [1, 2])
@@ -72,7 +75,7 @@ def test_extended_big_reactors_match_oracle(ext, problem):
         assert r.status == 0 and res["stats"][i, 6] == 0, (i, res["stats"][i].tolist())
         assert r.tau > 0 and abs(res["tau"][i] / r.tau - 1) < 1e-4, (i, res["tau"][i], r.tau)
         assert abs(res["T"][i] / r.T - 1) < 1e-4
-        for sp in MAJOR + ("AX21", "AX41", "AX92", "AX102"):
+        for sp in MAJOR + ("AX21", "AX41", "AX92", "AX102", "AX65", "AX75"):
             k = mech.species.index(sp)
             assert abs(res["Y"][i, k] - Ye[k]) <= 1e-4 * max(abs(Ye[k]), 1e-3), (i, sp)
         assert abs(res["Y"][i].sum() - 1.0) < 1e-8

@@ -50,7 +50,7 @@ def test_nasa7_continuity_at_tmid(mech):
 
 
 def test_tables_layout(tables):
-    assert tables["rsp"].shape == (325, 4) and tables["arr"].shape == (325, 3)
+    assert tables["rsp"].shape == (325, 8) and tables["arr"].shape == (325, 3)  # CKMI_SLOTS = 8
     assert tables["thermo"].shape == (53, 17)
     assert tables["eff_ptr"].shape == (326,)
     # E/R of H+O2<=>O+OH: 17041 cal/mol / RUC, Chemkin's activation-energy gas constant

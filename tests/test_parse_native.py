@@ -130,15 +130,25 @@ def test_both_parsers_reject_malformed_input(what):
         _native.parse_mechanism(text, _thermo_text())
 
 
-def test_more_than_four_species_per_side_is_rejected_loudly():
+def test_five_species_per_side_parse_and_nine_are_rejected():
+    """Up to CKMI_SLOTS = 8 distinct species on a side (round 2: 4); more is rejected loudly by both."""
     from pychemkin_amd import _native
     from pychemkin_amd.mechanism import Mechanism, MechanismError
 
     text = MINI.replace("END\nREACTIONS", "END\nREACTIONS\nH2+O2+OH+H+O<=>2H2O+O2          1.0E+10 0.0 0.0", 1)
-    with pytest.raises(MechanismError, match="more than 4"):
-        Mechanism(text, _thermo_text()).to_tables()
-    with pytest.raises(_native.NativeError, match="more than 4"):
-        _native.parse_mechanism(text, _thermo_text())
+    m = Mechanism(text, _thermo_text())
+    _assert_same(m, _native.parse_mechanism(text, _thermo_text()))
+    assert m.to_tables()["nr"][0] == 5
+    th = _thermo_text().splitlines()
+    i_ar = next(i for i, t in enumerate(th) if t.startswith("AR "))
+    wide_th = "THERMO\n" + th[1] + "\n" + "".join(
+        "\n".join([f"AR{k}".ljust(18) + th[i_ar][18:]] + th[i_ar + 1:i_ar + 4]) + "\n" for k in range(10)) + "END\n"
+    wide = ("ELEMENTS AR END\nSPECIES " + " ".join(f"AR{k}" for k in range(10)) + " END\nREACTIONS\n"
+            + "+".join(f"AR{k}" for k in range(9)) + "=>9AR9    1.0 0.0 0.0\nEND\n")
+    with pytest.raises(MechanismError, match="more than 8"):
+        Mechanism(wide, wide_th).to_tables()
+    with pytest.raises(_native.NativeError, match="more than 8"):
+        _native.parse_mechanism(wide, wide_th)
 
 
 def test_kin_preprocess_reports_parse_errors_without_a_gpu(tmp_path):
