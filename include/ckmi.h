@@ -266,6 +266,28 @@ int ckmi_lu_solve_batched(int32_t nsys, int32_t n, const double* LU, const int32
                           void* stream);
 const char* ckmi_lu_last_error(void);
 
+/* Viscosity: replaces KINGetViscosity (chemkin_wrapper.py:407-412) and
+ * KINGetMixtureViscosity (:442-448), evaluated by the reference's closed library from the
+ * transport file preprocessed by KINPreProcess (itran = 1, chemistry.py:636-687).
+ *   ckmi_transport_fit      host only: params [KK][6] = geometry, eps/k [K], sigma [A], dipole [D],
+ *                           polarizability [A^3], Zrot (TRANLIB columns) -> fits [KK][4], the
+ *                           coefficients of ln eta_k [g/(cm s)] as a cubic in ln T, least squares
+ *                           on 50 temperatures in [tlow, thigh]
+ *   ckmi_transport_create   uploads the fits and the Wilke tables onto the mechanism's device
+ *   ckmi_species_viscosity  T [n] -> eta [KK][n]                          (device pointers)
+ *   ckmi_mixture_viscosity  T [n], Y [KK][n] mass fractions -> eta [n]    (device pointers, Wilke) */
+typedef struct ckmi_transport ckmi_transport;
+/* fit interval of KINPreProcess (and of pychemkin_amd/transport.py) */
+#define CKMI_VISC_FIT_TLOW 300.0
+#define CKMI_VISC_FIT_THIGH 3500.0
+int ckmi_transport_fit(int32_t KK, const double* wt, const double* params, double tlow, double thigh, double* fits);
+int ckmi_transport_create(const ckmi_mech* mech, const double* fits, ckmi_transport** out);
+int ckmi_transport_destroy(ckmi_transport* tr);
+int ckmi_transport_fits(const ckmi_transport* tr, double* fits);
+int ckmi_species_viscosity(const ckmi_transport* tr, int32_t n, const double* T, double* visc, void* stream);
+int ckmi_mixture_viscosity(const ckmi_transport* tr, int32_t n, const double* T, const double* Y, double* visc,
+                           void* stream);
+
 #ifdef __cplusplus
 }
 #endif

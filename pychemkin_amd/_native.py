@@ -95,6 +95,12 @@ PROTOTYPES = {
     "ckmi_parsed_desc": (ct.c_int, [_P, ct.POINTER(MechDesc)]),
     "ckmi_parsed_symbols": (ct.c_int, [_P, _P, _P, _P, _P]),
     "ckmi_parsed_equation": (ct.c_int, [_P, ct.c_int32, ct.c_char_p, ct.c_int32, ct.POINTER(ct.c_int32)]),
+    "ckmi_transport_fit": (ct.c_int, [ct.c_int32, _P, _P, ct.c_double, ct.c_double, _P]),
+    "ckmi_transport_create": (ct.c_int, [_P, _P, ct.POINTER(_P)]),
+    "ckmi_transport_destroy": (ct.c_int, [_P]),
+    "ckmi_transport_fits": (ct.c_int, [_P, _P]),
+    "ckmi_species_viscosity": (ct.c_int, [_P, ct.c_int32, _P, _P, _P]),
+    "ckmi_mixture_viscosity": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P]),
 }
 LU_NMAX = 192
 
@@ -450,6 +456,71 @@ class DeviceMechanism:
             res["t_save"] = ts
             res["y_save"] = ys
         return res
+
+
+def transport_fit(wt: np.ndarray, params: np.ndarray, tlow: float, thigh: float) -> np.ndarray:
+    """Viscosity fits [KK][4] (ln eta_k as a cubic in ln T) from TRANLIB parameters [KK][6]; host only."""
+    wt = np.ascontiguousarray(wt, dtype=np.float64)
+    params = np.ascontiguousarray(params, dtype=np.float64)
+    KK = wt.shape[0]
+    if params.shape != (KK, 6):
+        raise NativeError(f"transport parameters must be [{KK}][6], got {params.shape}")
+    fits = np.zeros((KK, 4))
+    _check(lib().ckmi_transport_fit(KK, wt.ctypes.data, params.ctypes.data, float(tlow), float(thigh),
+                                    fits.ctypes.data), "ckmi_transport_fit")
+    return fits
+
+
+class DeviceTransport:
+    """Viscosity fits and Wilke tables of one DeviceMechanism, on its GPU (wraps ckmi_transport)."""
+
+    def __init__(self, dm: "DeviceMechanism", fits: np.ndarray):
+        self.dm = dm
+        self.KK = dm.KK
+        fits = np.ascontiguousarray(fits, dtype=np.float64)
+        if fits.shape != (self.KK, 4):
+            raise NativeError(f"viscosity fits must be [{self.KK}][4], got {fits.shape}")
+        h = _P()
+        with torch.cuda.device(dm.device):
+            _check(lib().ckmi_transport_create(dm.handle, fits.ctypes.data, ct.byref(h)), "ckmi_transport_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().ckmi_transport_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def fits(self) -> np.ndarray:
+        out = np.zeros((self.KK, 4))
+        _check(lib().ckmi_transport_fits(self._h, out.ctypes.data), "ckmi_transport_fits")
+        return out
+
+    def species_viscosity(self, T) -> torch.Tensor:
+        """T[n] -> eta[KK][n] [g/(cm s)] (device tensor)."""
+        T = self.dm._dev(T).reshape(-1)
+        n = T.numel()
+        out = torch.empty((self.KK, n), dtype=torch.float64, device=self.dm.device)
+        with torch.cuda.device(self.dm.device):
+            _check(lib().ckmi_species_viscosity(self._h, n, _ptr(T), _ptr(out), _stream_ptr(self.dm.device)),
+                   "ckmi_species_viscosity")
+        return out
+
+    def mixture_viscosity(self, T, Y_soa) -> torch.Tensor:
+        """T[n], Y[KK][n] mass fractions -> eta[n] [g/(cm s)] (Wilke; device tensor)."""
+        T = self.dm._dev(T).reshape(-1)
+        n = T.numel()
+        Y = self.dm._dev(Y_soa).reshape(self.KK, n)
+        out = torch.empty(n, dtype=torch.float64, device=self.dm.device)
+        with torch.cuda.device(self.dm.device):
+            _check(lib().ckmi_mixture_viscosity(self._h, n, _ptr(T), _ptr(Y), _ptr(out), _stream_ptr(self.dm.device)),
+                   "ckmi_mixture_viscosity")
+        return out
 
 
 def set_reactor_path(path: int) -> None:

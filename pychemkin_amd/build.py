@@ -13,6 +13,7 @@ BIG_SRC = os.path.join(HERE, "csrc", "ckmi_big.hip")  # workgroup-per-reactor in
 KIN_SRC = os.path.join(HERE, "csrc", "ckmi_kin.cpp")  # KIN-compatible host shims (include/ckmi_kin.h)
 JIT_SRC = os.path.join(HERE, "csrc", "ckmi_jit.cpp")  # mechanism-specialised ROP kernel generator (hipRTC)
 PARSE_SRC = os.path.join(HERE, "csrc", "ckmi_parse.cpp")  # native Chemkin-II interpreter (KINPreProcess)
+TRAN_SRC = os.path.join(HERE, "csrc", "ckmi_transport.hip")  # viscosity fits + species / mixture viscosity
 DEPS = [os.path.join(HERE, "csrc", f) for f in ("ckmi_device.hpp", "ckmi_reactor.hpp", "ckmi_image.hpp",
                                                 "ckmi_run.hpp", "ckmi_internal.hpp")] + [
     os.path.join(HERE, "..", "include", "ckmi.h"), os.path.join(HERE, "..", "include", "ckmi_kin.h")]
@@ -48,7 +49,7 @@ def _stale(target: str, sources) -> bool:
 
 
 def needs_build() -> bool:
-    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC, JIT_SRC, PARSE_SRC] + DEPS)
+    return _stale(OUT, [SRC, LU_SRC, BIG_SRC, KIN_SRC, JIT_SRC, PARSE_SRC, TRAN_SRC] + DEPS)
 
 
 PROF_OUT = os.path.join(HERE, "_lib", "libckmi_prof.so")  # diagnostic phase-timer build
@@ -88,6 +89,9 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     parse_obj = os.path.join(OBJ_DIR, "ckmi_parse.o")
     if force or _stale(parse_obj, [PARSE_SRC] + DEPS):
         jobs.append((PARSE_SRC, parse_obj, KIN_FLAGS))
+    tran_obj = os.path.join(OBJ_DIR, "ckmi_transport.o")
+    if force or _stale(tran_obj, [TRAN_SRC] + DEPS):
+        jobs.append((TRAN_SRC, tran_obj, LU_FLAGS))
     tag = "main" if default else os.path.splitext(os.path.basename(out))[0]
     main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
     if force or (not default and not prof) or _stale(main_obj, [SRC] + DEPS):
@@ -96,7 +100,7 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
         for f in [pool.submit(_compile, s, o, fl, verbose) for s, o, fl in jobs]:
             f.result()
     cmd = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out, main_obj, lu_obj, big_obj, kin_obj, jit_obj,
-           parse_obj,
+           parse_obj, tran_obj,
            "-L/opt/rocm/lib", "-lhiprtc", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

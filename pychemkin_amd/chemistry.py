@@ -11,6 +11,9 @@ Drop-in for the reference's ``Chemistry`` on the batch-reactor path:
   SpeciesComposition     NCF element counts (chemistry.py:1472-1522)
   get_reaction_parameters / set_reaction_AFactor / get_reaction_AFactor (1-based, as the
                          reference, chemistry.py:1604-1724), get_gas_reaction_string
+  tranfile / preprocess_transportdata / verify_transport_data   transport data read at
+                         preprocess (chemistry.py:402-480,636-687,794-808): viscosity fits for
+                         Mixture.mixture_viscosity / species_Visc (transport.py)
 Deviations: errors raise exceptions instead of exit(); get_specindex
 accepts index 0 (H2 in GRI-3.0); real-gas EOS is not supported (ideal gas only).
 """
@@ -22,6 +25,7 @@ from typing import Dict, List, Optional
 import numpy as np
 
 from . import device as _device
+from . import transport as _transport
 from .constants import R_GAS
 from .logger import logger
 from .mechanism import Mechanism
@@ -75,6 +79,9 @@ class Chemistry:
         self._mech: Optional[Mechanism] = None
         self._version = 0
         self.userealgas = False
+        self._inline_transport = False
+        self._tran_params: Optional[np.ndarray] = None  # [KK][6] TRANLIB parameters
+        self._vfits: Optional[np.ndarray] = None        # [KK][4] viscosity fits
 
     def __deepcopy__(self, memo):
         # chemistry sets are shared, global objects in the reference (chemistry.py:46-51)
@@ -105,6 +112,35 @@ class Chemistry:
     def tranfile(self, filename: str):
         self._tranfile = filename
 
+    def preprocess_transportdata(self) -> None:
+        """Process the transport data: the ``tranfile``, or without one the ``TRANSPORT ALL`` block of
+        the mechanism file (chemistry.py:450-480)."""
+        self._inline_transport = True
+
+    def verify_transport_data(self) -> bool:
+        """True once transport data have been processed (chemistry.py:794-808)."""
+        return self._vfits is not None
+
+    @property
+    def transport_parameters(self) -> np.ndarray:
+        """[KK][6] TRANLIB parameters (geometry, eps/k, sigma, dipole, polarizability, Zrot)."""
+        if self._tran_params is None:
+            raise ChemistryError("no transport data processed")
+        return self._tran_params.copy()
+
+    @property
+    def viscosity_fits(self) -> np.ndarray:
+        """[KK][4] coefficients of ln eta_k [g/(cm s)] in powers of ln T."""
+        if self._vfits is None:
+            raise ChemistryError("no transport data processed")
+        return self._vfits.copy()
+
+    def device_transport(self, device_index: int = None):
+        """The viscosity tables of this chemistry set on a GPU (created on first use)."""
+        if self._vfits is None:
+            raise ChemistryError("no transport data processed")
+        return _device.device_transport(self, device_index)
+
     @property
     def surffile(self) -> str:
         return self._surffile
@@ -133,7 +169,23 @@ class Chemistry:
             raise ChemistryError(f"gas mechanism file not found: {self._chemfile!r}")
         if self._thermfile and not os.path.isfile(self._thermfile):
             raise ChemistryError(f"thermodynamic data file not found: {self._thermfile!r}")
+        if self._tranfile and not os.path.isfile(self._tranfile):
+            raise ChemistryError(f"transport data file not found: {self._tranfile!r}")
         self._mech = Mechanism.from_files(self._chemfile, self._thermfile or None)
+        self._tran_params = self._vfits = None
+        tran_text = ""
+        if self._tranfile:
+            with open(self._tranfile) as f:
+                tran_text = f.read()
+        elif self._inline_transport:
+            with open(self._chemfile) as f:
+                tran_text = _transport.inline_transport_block(f.read())
+            if not tran_text:
+                raise ChemistryError("preprocess_transportdata(): the mechanism file has no TRANSPORT block")
+        if tran_text:
+            self._tran_params = _transport.species_params(_transport.parse_transport_text(tran_text),
+                                                         self._mech.species)
+            self._vfits = _transport.viscosity_fits(self._mech.wt, self._tran_params)
         self._version += 1
         if self._chemset_index < 0:
             self._chemset_index = len(_chemistry_sets)

@@ -46,6 +46,7 @@ struct ChemSet {
   std::vector<std::string> equations;   // reaction strings (KINPreProcess sets; KINGetGasReactionString)
   double* dbuf = nullptr;               // device scratch for single-state calls
   size_t dbuf_n = 0;
+  ckmi_transport* tran = nullptr;       // viscosity fits (KINPreProcess with itran = 1)
 };
 std::vector<ChemSet*> g_sets;  // chemistry set id = index + 1
 int g_active = 0;
@@ -460,6 +461,7 @@ int ckmi_kin_release(int32_t chemset) {
   ChemSet* s = get_set(&chemset);
   if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
   if (s->dbuf) (void)hipFree(s->dbuf);
+  ckmi_transport_destroy(s->tran);
   ckmi_mech_destroy(s->mech);
   delete s;
   g_sets[chemset - 1] = nullptr;
@@ -782,24 +784,122 @@ int KINAll0D_GetGasSolnResponse(int* nreac, int* npts, int* KK, double* t, doubl
 }
 
 
+}  // extern "C"
+
+namespace {
+// ---------------------------------------------------------------- transport data (TRANLIB format)
+bool read_text(const char* path, std::string& out) {
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return false;
+  out.clear();
+  char buf[1 << 14];
+  size_t n;
+  while ((n = std::fread(buf, 1, sizeof(buf), f)) > 0) out.append(buf, n);
+  std::fclose(f);
+  return true;
+}
+
+// the lines between a "TRANSPORT [ALL]" line and the next "END" line of a mechanism file
+std::string inline_transport_block(const std::string& text) {
+  std::istringstream in(text);
+  std::string line, out;
+  bool on = false;
+  while (std::getline(in, line)) {
+    std::istringstream ls(line.substr(0, line.find('!')));
+    std::string w;
+    ls >> w;
+    w = upper(w);
+    if (!on) {
+      if (w.rfind("TRAN", 0) == 0) on = true;
+    } else if (w == "END") {
+      return out;
+    } else {
+      out += line + "\n";
+    }
+  }
+  return on ? out : std::string();
+}
+
+// TRANLIB records (name, geometry, eps/k, sigma, dipole, polarizability, Zrot; '!' comments; the
+// first record of a species wins) -> [KK][6] in mechanism order; every species needs one.  The
+// grammar of pychemkin_amd/transport.py parse_transport_text.
+bool transport_params(const std::string& text, const std::vector<std::string>& names, std::vector<double>& params,
+                      std::string& why) {
+  std::map<std::string, std::vector<double>> rec;
+  std::istringstream in(text);
+  std::string line;
+  int ln = 0;
+  while (std::getline(in, line)) {
+    ++ln;
+    std::istringstream ls(line.substr(0, line.find('!')));
+    std::vector<std::string> tok;
+    std::string w;
+    while (ls >> w) tok.push_back(w);
+    if (tok.empty()) continue;
+    const std::string key = upper(tok[0]);
+    if (key.rfind("TRAN", 0) == 0 || key == "END") continue;
+    if (tok.size() < 7) {
+      why = "transport line " + std::to_string(ln) + ": expected 7 fields";
+      return false;
+    }
+    std::vector<double> v(6);
+    for (int j = 0; j < 6; ++j) {
+      char* e = nullptr;
+      v[j] = std::strtod(tok[1 + j].c_str(), &e);
+      if (!e || *e) {
+        why = "transport line " + std::to_string(ln) + ": bad number " + tok[1 + j];
+        return false;
+      }
+    }
+    if (v[0] != 0.0 && v[0] != 1.0 && v[0] != 2.0) {
+      why = "transport line " + std::to_string(ln) + ": geometry must be 0, 1 or 2";
+      return false;
+    }
+    rec.emplace(key, v);
+  }
+  params.assign(6 * names.size(), 0.0);
+  for (size_t k = 0; k < names.size(); ++k) {
+    auto it = rec.find(upper(names[k]));
+    if (it == rec.end()) {
+      why = "no transport data for species " + names[k];
+      return false;
+    }
+    std::copy(it->second.begin(), it->second.end(), params.begin() + 6 * k);
+  }
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
 // ---------------------------------------------------------------- mechanism preprocessing
 // KINPreProcess (chemkin_wrapper.py:303-316, chemistry.py:675-687): parse chem.inp + therm.dat with
 // the native interpreter (ckmi_parse.cpp), build the device tables and return the chemistry-set
-// index.  Surface chemistry is out of scope (isurf must be 0).  With itran = 1 the transport file
-// must exist and is kept for reference (transport properties are not computed on this path).  The
-// summary file, when named, receives the element / species / reaction listing; the link files of
-// the closed library are not written (the tables stay in this process).
+// index.  Surface chemistry is out of scope (isurf must be 0).  With itran = 1 the transport data
+// come from the transport file, or, when it does not exist, from the TRANSPORT block of the
+// mechanism file (chemistry.py:450-480 preprocess_transportdata); their viscosity fits are made
+// here (ckmi_transport_fit) and uploaded with the mechanism (KINGetViscosity /
+// KINGetMixtureViscosity).  The summary file, when named, receives the element / species /
+// reaction listing; the link files of the closed library are not written (the tables stay in this
+// process).
 int KINPreProcess(int* isurf, int* itran, char* chem, char* surf, char* therm, char* tran, char* gaslink,
                   char* surflink, char* tranlink, char* summary, int* chemset) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   (void)surf, (void)gaslink, (void)surflink, (void)tranlink;
   if (!chem || !chemset) return fail(CKMI_ERR_ARG, "KINPreProcess: null mechanism file or chemistry-set pointer");
   if (isurf && *isurf != 0) return fail(CKMI_ERR_UNSUPPORTED, "surface chemistry is not supported on this path");
+  std::string tran_text;
   if (itran && *itran != 0) {
-    if (!tran || !*tran) return fail(CKMI_ERR_ARG, "KINPreProcess: transport requested without a transport file");
-    FILE* f = std::fopen(tran, "r");
-    if (!f) return fail(CKMI_ERR_ARG, std::string("cannot read transport file ") + tran);
-    std::fclose(f);
+    if (tran && *tran && read_text(tran, tran_text)) {
+    } else {
+      std::string chem_text;
+      if (!read_text(chem, chem_text)) return fail(CKMI_ERR_ARG, std::string("cannot read mechanism file ") + chem);
+      tran_text = inline_transport_block(chem_text);
+      if (tran_text.empty())
+        return fail(CKMI_ERR_ARG, std::string("KINPreProcess: transport requested, but neither the transport file ") +
+                                      (tran ? tran : "") + " nor a TRANSPORT block in the mechanism file exists");
+    }
   }
   ckmi_parsed* p = nullptr;
   int rc = ckmi_parse_files(chem, therm, &p);
@@ -826,6 +926,22 @@ int KINPreProcess(int* isurf, int* itran, char* chem, char* surf, char* therm, c
   }
   ckmi_parsed_free(p);
   if (rc) return rc;
+  if (!tran_text.empty()) {
+    std::vector<double> params;
+    std::string why;
+    if (!transport_params(tran_text, s->names, params, why)) {
+      ckmi_kin_release(cs);
+      return fail(CKMI_ERR_ARG, "KINPreProcess: " + why);
+    }
+    std::vector<double> fits((size_t)4 * KK);
+    rc = ckmi_transport_fit(KK, s->wt.data(), params.data(), CKMI_VISC_FIT_TLOW, CKMI_VISC_FIT_THIGH, fits.data());
+    if (!rc) rc = ckmi_transport_create(s->mech, fits.data(), &s->tran);
+    if (rc) {
+      const std::string msg = ckmi_last_error();
+      ckmi_kin_release(cs);
+      return fail(rc, "KINPreProcess: " + msg);
+    }
+  }
   *chemset = cs;
   if (summary && *summary) {
     FILE* f = std::fopen(summary, "w");
@@ -839,6 +955,45 @@ int KINPreProcess(int* isurf, int* itran, char* chem, char* surf, char* therm, c
     }
   }
   return CKMI_OK;
+}
+
+// KINGetViscosity (chemkin_wrapper.py:407-412, mixture.py:1860-1883): species viscosities
+// [g/(cm s)] at T from the fits made by KINPreProcess (itran = 1)
+int KINGetViscosity(int* chemset, double* T, double* visc) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !visc || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  if (!s->tran) return fail(CKMI_ERR_ARG, "no transport data processed (KINPreProcess with itran = 1)");
+  const int KK = s->KK;
+  int rc = ensure_scratch(s, 1 + (size_t)KK);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, T, sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  rc = ckmi_species_viscosity(s->tran, 1, s->dbuf, s->dbuf + 1, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  return hip_ok(hipMemcpy(visc, s->dbuf + 1, KK * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+}
+
+// KINGetMixtureViscosity (chemkin_wrapper.py:442-448, mixture.py:1943-1977): Wilke mixture
+// viscosity [g/(cm s)].  The composition argument is read as MASS fractions, as mixture.py:1967
+// passes them (the CONV golden's state-viscocity is reproduced to <= 5e-4 that way and misses by
+// 1.3 % when the array is read as mole fractions; tests/test_transport.py).
+int KINGetMixtureViscosity(int* chemset, double* T, double* Y, double* visc) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !Y || !visc || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  if (!s->tran) return fail(CKMI_ERR_ARG, "no transport data processed (KINPreProcess with itran = 1)");
+  const int KK = s->KK;
+  int rc = ensure_scratch(s, 2 + (size_t)KK);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  std::vector<double> in(1 + KK);
+  in[0] = *T;
+  std::copy(Y, Y + KK, in.begin() + 1);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  rc = ckmi_mixture_viscosity(s->tran, 1, s->dbuf, s->dbuf + 1, s->dbuf + 1 + KK, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  return hip_ok(hipMemcpy(visc, s->dbuf + 1 + KK, sizeof(double), hipMemcpyDeviceToHost), "D2H");
 }
 
 // KINGetGasReactionString (chemkin_wrapper.py:365-371, chemistry.py:1759-1781): 1-based reaction index
@@ -1090,10 +1245,8 @@ int KINAll0D_CalculateInput(int* lout, int* chemset, char* lines, int* nlines, i
 // PFR, engines, flames) and return CKMI_ERR_UNSUPPORTED with a message.
 #define CKMI_OUT_OF_SCOPE(name, what, ...) \
   int name(__VA_ARGS__) { return fail(CKMI_ERR_UNSUPPORTED, #name ": " what " is not on this path"); }
-CKMI_OUT_OF_SCOPE(KINGetViscosity, "transport", int*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetConductivity, "transport", int*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetDiffusionCoeffs, "transport", int*, double*, double*, double*)
-CKMI_OUT_OF_SCOPE(KINGetMixtureViscosity, "transport", int*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetMixtureConductivity, "transport", int*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetMixtureDiffusionCoeffs, "transport", int*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetOrdinaryDiffusionCoeffs, "transport", int*, double*, double*, double*, double*)

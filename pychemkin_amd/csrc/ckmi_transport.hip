@@ -1,0 +1,250 @@
+// ckmi_transport.hip -- pure-species and mixture viscosity on gfx950.
+//
+// The reference reads a Chemkin transport file at preprocess (chemistry.py:636-687, itran = 1) and
+// its closed library evaluates viscosities on demand: KINGetViscosity (species, mixture.py:1860-1883)
+// and KINGetMixtureViscosity (mixture.py:1943-1977), the latter on every saved point of a reactor
+// solution in the reference's own tests (CONV.py:176-190).  Restated method (TRANFIT / TRANLIB):
+//
+//   fit (host, once per mechanism):
+//     eta_k(T) = 5/16 sqrt(pi m_k kB T) / (pi sigma_k^2 Omega22*(T / eps_k, delta*_k)),
+//     Omega22* = 1.16145 T*^-0.14874 + 0.52487 e^(-0.7732 T*) + 2.16178 e^(-2.43787 T*) + 0.2 delta*^2 / T*
+//     (Neufeld-Janzen-Aziz correlation of the Lennard-Jones table, Brokaw's polar term), and
+//     ln eta_k = sum_n a_kn (ln T)^n, n < 4, least squares (Householder QR) on 50 temperatures
+//     equally spaced in [tlow, thigh];
+//   evaluate (device, one state per lane):
+//     eta_k = exp(poly), eta = sum_k X_k eta_k / sum_j X_j Phi_kj (Wilke),
+//     Phi_kj = A_kj (1 + s_k B_kj / s_j)^2, s = sqrt(eta), A_kj = (1 + W_k / W_j)^-1/2 / sqrt 8,
+//     B_kj = (W_j / W_k)^1/4 (A, B precomputed per mechanism, read by wave-uniform scalar loads).
+//
+// Layout: SoA like the ROP kernel (Y[KK][n], lane = state).  Per lane the species vectors X_j and
+// 1 / s_j live in a per-thread LDS column ([KK][block] doubles, conflict-free), so the KK^2 Wilke
+// double loop reads its lane's vectors from LDS and the (k, j) table entries from the scalar cache.
+// Bound: FP64 VALU (KK^2 x 6 FLOP per state); HBM traffic is (KK + 2) x 8 B per state.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <cmath>
+#include <string>
+#include <vector>
+
+#include "../../include/ckmi.h"
+#include "ckmi_internal.hpp"
+
+struct ckmi_transport {
+  int device = 0;
+  int KK = 0;
+  double* fits = nullptr;  // device [KK][4]
+  double* A = nullptr;     // device [KK][KK]
+  double* B = nullptr;     // device [KK][KK]
+  const double* wt = nullptr;  // the mechanism's device weights
+  std::vector<double> fits_host;
+};
+
+namespace {
+
+constexpr double KB = 1.380649e-16;       // erg / K
+constexpr double NA = 6.02214076e23;
+constexpr double DEBYE = 1e-18;           // esu cm
+constexpr double ANGSTROM = 1e-8;         // cm
+constexpr int FIT_NPTS = 50;
+constexpr int FIT_ORDER = 4;
+
+int fail(int code, const std::string& msg) { return ckmi::set_error(code, msg); }
+
+double omega22(double tstar, double dstar) {
+  return 1.16145 * std::pow(tstar, -0.14874) + 0.52487 * std::exp(-0.77320 * tstar) +
+         2.16178 * std::exp(-2.43787 * tstar) + 0.2 * dstar * dstar / tstar;
+}
+
+// least squares min |V c - y| for the FIT_NPTS x FIT_ORDER Vandermonde matrix V by Householder QR
+void lsq_qr(double (*V)[FIT_ORDER], double* y, double* c) {
+  constexpr int m = FIT_NPTS, n = FIT_ORDER;
+  for (int j = 0; j < n; ++j) {
+    double nrm = 0.0;
+    for (int i = j; i < m; ++i) nrm += V[i][j] * V[i][j];
+    nrm = std::sqrt(nrm);
+    const double alpha = V[j][j] > 0 ? -nrm : nrm;
+    double v[m];
+    for (int i = 0; i < m; ++i) v[i] = i < j ? 0.0 : V[i][j];
+    v[j] -= alpha;
+    double vv = 0.0;
+    for (int i = j; i < m; ++i) vv += v[i] * v[i];
+    if (vv == 0.0) continue;
+    for (int k = j; k < n; ++k) {
+      double s = 0.0;
+      for (int i = j; i < m; ++i) s += v[i] * V[i][k];
+      s = 2.0 * s / vv;
+      for (int i = j; i < m; ++i) V[i][k] -= s * v[i];
+    }
+    double s = 0.0;
+    for (int i = j; i < m; ++i) s += v[i] * y[i];
+    s = 2.0 * s / vv;
+    for (int i = j; i < m; ++i) y[i] -= s * v[i];
+  }
+  for (int j = n - 1; j >= 0; --j) {
+    double s = y[j];
+    for (int k = j + 1; k < n; ++k) s -= V[j][k] * c[k];
+    c[j] = s / V[j][j];
+  }
+}
+
+__global__ void species_viscosity_kernel(int KK, int n, const double* __restrict__ fits, const double* __restrict__ T,
+                                         double* __restrict__ visc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = log(T[i]);
+  for (int k = 0; k < KK; ++k) {
+    const double* a = fits + 4 * k;
+    visc[(size_t)k * n + i] = exp(fma(x, fma(x, fma(x, a[3], a[2]), a[1]), a[0]));
+  }
+}
+
+// one state per lane; dynamic LDS: X [KK][blockDim] then 1/sqrt(eta) [KK][blockDim]
+__global__ void mixture_viscosity_kernel(int KK, int n, const double* __restrict__ fits, const double* __restrict__ A,
+                                         const double* __restrict__ B, const double* __restrict__ wt,
+                                         const double* __restrict__ T, const double* __restrict__ Y,
+                                         double* __restrict__ visc) {
+  extern __shared__ double tv_lds[];
+  const int bs = blockDim.x, t = threadIdx.x;
+  const int i = blockIdx.x * bs + t;
+  const bool live = i < n;
+  const int ii = live ? i : 0;
+  double* Xs = tv_lds + t;            // Xs[k * bs]
+  double* Rs = tv_lds + KK * bs + t;  // Rs[k * bs] = 1 / sqrt(eta_k)
+  const double x = log(T[ii]);
+  // x_k = Y_k / W_k: the Wilke ratio is homogeneous of degree 0 in X, so the normalisation
+  // sum_j x_j cancels between each numerator and its denominator
+  for (int k = 0; k < KK; ++k) {
+    const double xk = Y[(size_t)k * n + ii] / wt[k];
+    Xs[k * bs] = xk;
+    const double* a = fits + 4 * k;
+    Rs[k * bs] = exp(-0.5 * fma(x, fma(x, fma(x, a[3], a[2]), a[1]), a[0]));
+  }
+  double mix = 0.0;
+  for (int k = 0; k < KK; ++k) {
+    const double xk = Xs[k * bs];
+    if (xk == 0.0) continue;  // X_k eta_k / den_k = 0 (den_k >= X_k A_kk 4 > 0 otherwise)
+    const double rk = Rs[k * bs];
+    const double sk = 1.0 / rk;
+    const double* Ak = A + (size_t)k * KK;
+    const double* Bk = B + (size_t)k * KK;
+    double den = 0.0;
+    for (int j = 0; j < KK; ++j) {
+      const double f = fma(sk * Rs[j * bs], Bk[j], 1.0);
+      den = fma(Xs[j * bs] * Ak[j], f * f, den);
+    }
+    mix += xk * (sk * sk) / den;
+  }
+  if (live) visc[i] = mix;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ckmi_transport_fit(int32_t KK, const double* wt, const double* params, double tlow, double thigh, double* fits) {
+  if (KK <= 0 || !wt || !params || !fits) return fail(CKMI_ERR_ARG, "ckmi_transport_fit: bad argument");
+  if (!(tlow > 0.0) || !(thigh > tlow)) return fail(CKMI_ERR_ARG, "ckmi_transport_fit: need 0 < tlow < thigh");
+  for (int k = 0; k < KK; ++k) {
+    const double* p = params + 6 * k;
+    const double eps = p[1], sig = p[2] * ANGSTROM, mu = p[3] * DEBYE;
+    if (!(eps > 0.0) || !(sig > 0.0) || !(wt[k] > 0.0))
+      return fail(CKMI_ERR_ARG, "ckmi_transport_fit: species " + std::to_string(k) + " needs eps/k > 0, sigma > 0, W > 0");
+    const double dstar = 0.5 * mu * mu / (eps * KB * sig * sig * sig);
+    const double m = wt[k] / NA;
+    double V[FIT_NPTS][FIT_ORDER], y[FIT_NPTS];
+    for (int i = 0; i < FIT_NPTS; ++i) {
+      const double T = tlow + (thigh - tlow) * i / (FIT_NPTS - 1);
+      const double eta = (5.0 / 16.0) * std::sqrt(M_PI * m * KB * T) / (M_PI * sig * sig * omega22(T / eps, dstar));
+      const double x = std::log(T);
+      V[i][0] = 1.0;
+      for (int j = 1; j < FIT_ORDER; ++j) V[i][j] = V[i][j - 1] * x;
+      y[i] = std::log(eta);
+    }
+    lsq_qr(V, y, fits + FIT_ORDER * k);
+  }
+  return CKMI_OK;
+}
+
+int ckmi_transport_create(const ckmi_mech* m, const double* fits, ckmi_transport** out) {
+  if (!m || !fits || !out) return fail(CKMI_ERR_ARG, "ckmi_transport_create: null argument");
+  const int KK = m->KK;
+  std::vector<double> W(KK), A((size_t)KK * KK), B((size_t)KK * KK);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != m->device) (void)hipSetDevice(m->device);
+  auto* t = new ckmi_transport();
+  t->device = m->device;
+  t->KK = KK;
+  t->wt = m->d.wt;
+  t->fits_host.assign(fits, fits + (size_t)FIT_ORDER * KK);
+  int rc = CKMI_OK;
+  if (hipMemcpy(W.data(), m->d.wt, sizeof(double) * KK, hipMemcpyDeviceToHost) != hipSuccess) {
+    rc = fail(CKMI_ERR_HIP, "ckmi_transport_create: reading the mechanism's weights failed");
+  } else {
+    for (int k = 0; k < KK; ++k)
+      for (int j = 0; j < KK; ++j) {
+        A[(size_t)k * KK + j] = 1.0 / (std::sqrt(8.0) * std::sqrt(1.0 + W[k] / W[j]));
+        B[(size_t)k * KK + j] = std::sqrt(std::sqrt(W[j] / W[k]));
+      }
+    if (hipMalloc(&t->fits, sizeof(double) * FIT_ORDER * KK) != hipSuccess ||
+        hipMalloc(&t->A, sizeof(double) * KK * KK) != hipSuccess || hipMalloc(&t->B, sizeof(double) * KK * KK) != hipSuccess ||
+        hipMemcpy(t->fits, fits, sizeof(double) * FIT_ORDER * KK, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(t->A, A.data(), sizeof(double) * KK * KK, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(t->B, B.data(), sizeof(double) * KK * KK, hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(CKMI_ERR_HIP, "ckmi_transport_create: device allocation / upload failed");
+  }
+  if (prev >= 0 && prev != m->device) (void)hipSetDevice(prev);
+  if (rc != CKMI_OK) {
+    ckmi_transport_destroy(t);
+    return rc;
+  }
+  *out = t;
+  return CKMI_OK;
+}
+
+int ckmi_transport_destroy(ckmi_transport* t) {
+  if (!t) return CKMI_OK;
+  (void)hipFree(t->fits);
+  (void)hipFree(t->A);
+  (void)hipFree(t->B);
+  delete t;
+  return CKMI_OK;
+}
+
+int ckmi_transport_fits(const ckmi_transport* t, double* fits) {
+  if (!t || !fits) return fail(CKMI_ERR_ARG, "ckmi_transport_fits: null argument");
+  std::copy(t->fits_host.begin(), t->fits_host.end(), fits);
+  return CKMI_OK;
+}
+
+int ckmi_species_viscosity(const ckmi_transport* t, int32_t n, const double* T, double* visc, void* stream) {
+  if (!t || n < 0 || !T || !visc) return fail(CKMI_ERR_ARG, "ckmi_species_viscosity: bad argument");
+  if (n == 0) return CKMI_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(species_viscosity_kernel, dim3((n + bs - 1) / bs), dim3(bs), 0, (hipStream_t)stream, t->KK, n,
+                     t->fits, T, visc);
+  if (hipGetLastError() != hipSuccess) return fail(CKMI_ERR_HIP, "species_viscosity_kernel launch failed");
+  return CKMI_OK;
+}
+
+int ckmi_mixture_viscosity(const ckmi_transport* t, int32_t n, const double* T, const double* Y, double* visc,
+                           void* stream) {
+  if (!t || n < 0 || !T || !Y || !visc) return fail(CKMI_ERR_ARG, "ckmi_mixture_viscosity: bad argument");
+  if (n == 0) return CKMI_OK;
+  // one wave per block up to 150 species (<= 150 KB of LDS), half a wave above
+  const int bs = t->KK <= 150 ? 64 : 32;
+  const size_t lds = sizeof(double) * 2 * (size_t)t->KK * bs;
+  if (lds > 160 * 1024) return fail(CKMI_ERR_UNSUPPORTED, "ckmi_mixture_viscosity: more than 255 species");
+  if (lds > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)mixture_viscosity_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+          hipSuccess)
+    return fail(CKMI_ERR_HIP, "ckmi_mixture_viscosity: LDS attribute failed");
+  hipLaunchKernelGGL(mixture_viscosity_kernel, dim3((n + bs - 1) / bs), dim3(bs), lds, (hipStream_t)stream, t->KK, n,
+                     t->fits, t->A, t->B, t->wt, T, Y, visc);
+  if (hipGetLastError() != hipSuccess) return fail(CKMI_ERR_HIP, "mixture_viscosity_kernel launch failed");
+  return CKMI_OK;
+}
+
+}  // extern "C"

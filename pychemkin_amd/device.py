@@ -29,6 +29,29 @@ def device_mechanism(chem, device_index: int = None):
 
 
 def drop(chem) -> None:
+    for k in [k for k in _tcache if k[0] == id(chem)]:
+        _tcache.pop(k).close()
     for k in [k for k in _cache if k[0] == id(chem)]:
         dm = _cache.pop(k)
         dm.close()
+
+
+_tcache: Dict[Tuple[int, int], object] = {}
+
+
+def device_transport(chem, device_index: int = None):
+    """The chemistry set's viscosity fits + Wilke tables on a GPU (one ckmi_transport per device)."""
+    import torch
+
+    from . import _native
+
+    if device_index is None:
+        device_index = torch.cuda.current_device()
+    dm = device_mechanism(chem, device_index)
+    key = (id(chem), int(device_index))
+    dt = _tcache.get(key)
+    if dt is None or dt.version != chem._version:
+        dt = _native.DeviceTransport(dm, chem._vfits)
+        dt.version = chem._version
+        _tcache[key] = dt
+    return dt

@@ -3,7 +3,8 @@
 Drop-in subset of ``Mixture`` used by the batch-reactor path:
 state (temperature, pressure, volume, X, Y), composition conversion and normalisation,
 WTM, RHO, concentration, HML/CPBL, ROP, RxnRates, massROP, volHRR, list_ROP,
-list_reaction_rates, X/Y_by_Equivalence_Ratio, list_composition, validate.
+list_reaction_rates, X/Y_by_Equivalence_Ratio, list_composition, validate,
+mixture_viscosity and species_Visc (transport data preprocessed, mixture.py:1860-1977).
 
 Kinetics and mixture thermo go through the GPU kernels (ckmi_rop_thermo,
 ckmi_reaction_rates, ckmi_species_thermo) with a batch of one state, exactly as the
@@ -281,6 +282,39 @@ class Mixture:
     def species_H(self) -> np.ndarray:
         self._need_TP()
         return self._chem.SpeciesH(self._temp)
+
+    @property
+    def transport_data(self) -> int:
+        """1 if the chemistry set has processed transport data (mixture.py:108)."""
+        return 1 if self._chem.verify_transport_data() else 0
+
+    def _need_transport(self):
+        if not self.transport_data:
+            raise MixtureError("no transport data processed")
+        if not self._Tset:
+            raise MixtureError("mixture temperature [K] is not provided")
+
+    def species_Visc(self) -> np.ndarray:
+        """Species viscosities [g/(cm s)] at the mixture temperature (KINGetViscosity, mixture.py:1860-1883)."""
+        import torch
+
+        self._need_transport()
+        dt = self._chem.device_transport()
+        T = torch.tensor([self._temp], dtype=torch.float64, device=dt.dm.device)
+        return dt.species_viscosity(T)[:, 0].cpu().numpy()
+
+    def mixture_viscosity(self) -> float:
+        """Mixture viscosity [g/(cm s)] (KINGetMixtureViscosity with the mass fractions,
+        mixture.py:1943-1977; Wilke's rule on the GPU)."""
+        import torch
+
+        self._need_transport()
+        if not (self._Xset or self._Yset):
+            raise MixtureError("mixture composition is not provided")
+        dt = self._chem.device_transport()
+        T = torch.tensor([self._temp], dtype=torch.float64, device=dt.dm.device)
+        Y = torch.as_tensor(self.Y.reshape(self._KK, 1).copy(), dtype=torch.float64, device=dt.dm.device)
+        return float(dt.mixture_viscosity(T, Y)[0].item())
 
     def massROP(self) -> np.ndarray:
         """Species mass rates of production [g/cm3-s]."""

@@ -1,0 +1,162 @@
+"""Viscosity kernels (ckmi_species_viscosity / ckmi_mixture_viscosity) against the numpy restatement
+and the reference's viscosity goldens, through the batched ABI, the drop-in Mixture and KIN calls."""
+import ctypes as ct
+import os
+
+import numpy as np
+import pytest
+
+from conftest import CHEM, P_ATM, ROOT, THERM, ch4_air_Y, golden, within
+
+pytestmark = pytest.mark.gpu
+
+TRAN = os.path.join(ROOT, "data", "grimech30_transport.dat")
+
+
+@pytest.fixture(scope="module")
+def tr():
+    from oracle import transport_ref
+
+    return transport_ref
+
+
+@pytest.fixture(scope="module")
+def chem_tr():
+    import pychemkin_amd as ck
+
+    c = ck.Chemistry(chem=CHEM, therm=THERM, tran=TRAN, label="GRI 3.0")
+    assert c.preprocess() == 0
+    return c
+
+
+def _states(rng, KK, n):
+    T = rng.uniform(250.0, 4000.0, n)
+    Y = rng.dirichlet(0.3 * np.ones(KK), n)
+    Y[: n // 8, : KK // 2] = 0.0  # exact zeros (pure species and species-free states)
+    Y[: n // 8] /= Y[: n // 8].sum(axis=1, keepdims=True)
+    return T, Y
+
+
+def test_species_and_mixture_viscosity_match_restatement(chem_tr, mech, tr):
+    dt = chem_tr.device_transport()
+    rng = np.random.default_rng(7)
+    n = 5000
+    T, Y = _states(rng, mech.KK, n)
+    eta = dt.species_viscosity(T).cpu().numpy()
+    ref = tr.species_viscosity(T, chem_tr.viscosity_fits).T
+    assert np.max(np.abs(eta / ref - 1)) < 1e-13
+    mix = dt.mixture_viscosity(T, Y.T.copy()).cpu().numpy()
+    mref = tr.mixture_viscosity(T, tr.mole_fractions(Y, mech.wt), mech.wt, chem_tr.viscosity_fits)
+    assert np.all(np.isfinite(mix))
+    assert np.max(np.abs(mix / mref - 1)) < 1e-12
+    # a pure species is its own viscosity
+    k = mech.species.index("N2")
+    Yp = np.zeros((3, mech.KK))
+    Yp[:, k] = 1.0
+    Tp = np.array([300.0, 1000.0, 2500.0])
+    pure = tr.species_viscosity(Tp, chem_tr.viscosity_fits)[:, k]
+    assert np.allclose(dt.mixture_viscosity(Tp, Yp.T.copy()).cpu().numpy(), pure, rtol=1e-13, atol=0)
+
+
+def test_large_mechanism_half_wave_blocks(big_mech, tr):
+    """KK > 150 runs the 32-lane block form (LDS 2 KK x 32 doubles): the 161-species stand-in with the
+    tracers given argon's Lennard-Jones parameters."""
+    from pychemkin_amd import _native
+
+    with open(TRAN) as f:
+        data = tr.parse_transport(f.read())
+    params = np.array([data.get(s.upper(), data["AR"]) for s in big_mech.species], dtype=np.float64)
+    fits = _native.transport_fit(big_mech.wt, params, 300.0, 3500.0)
+    dm = _native.DeviceMechanism(big_mech.to_tables())
+    dt = _native.DeviceTransport(dm, fits)
+    rng = np.random.default_rng(3)
+    T, Y = _states(rng, big_mech.KK, 777)
+    mix = dt.mixture_viscosity(T, Y.T.copy()).cpu().numpy()
+    mref = tr.mixture_viscosity(T, tr.mole_fractions(Y, big_mech.wt), big_mech.wt, fits)
+    assert np.max(np.abs(mix / mref - 1)) < 1e-12
+
+
+def test_simple_air_golden_through_drop_in(chem_tr):
+    import pychemkin_amd as ck
+
+    g = golden("simple")
+    air = ck.Mixture(chem_tr)
+    air.pressure = 1.0 * P_ATM
+    air.temperature = 300.0
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    v = air.mixture_viscosity() * 100.0
+    assert abs(v / g["state-viscosity"][0] - 1) < 1.5e-3  # +1.1e-3, parity partial (tests/test_transport.py)
+    visc = air.species_Visc()
+    assert visc.shape == (chem_tr.KK,) and np.all(visc > 0)
+
+
+def test_conv_golden_viscosity_through_drop_in_reactor(chem_tr):
+    """CONV.py:62-190 on the GPU: the RCM run, then Mixture.mixture_viscosity() of every saved point."""
+    import pychemkin_amd as ck
+
+    g = golden("CONV")
+    chem = chem_tr
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    m = ck.Mixture(chem)
+    m.X_by_Equivalence_Ratio(chem, fuel.X, air.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"], 0.7)
+    m.temperature = 800.0
+    m.pressure = 3 * P_ATM
+    r = ck.GivenVolumeBatchReactor_EnergyConservation(m, label="RCM")
+    r.volume = 10.0
+    r.time = 0.1
+    r.tolerances = (1e-10, 1e-8)
+    r.force_nonnegative = True
+    r.timestep_for_saving_solution = 0.01
+    r.set_volume_profile([0.0, 0.01, 2.0], [10.0, 4.0, 4.0])
+    r.set_ignition_delay(method="T_inflection")
+    assert r.run() == 0
+    r.process_solution()
+    n = len(r.get_solution_variable_profile("temperature"))
+    v = np.array([r.get_solution_mixture_at_index(i).mixture_viscosity() for i in range(n)])
+    gv = np.asarray(g["state-viscocity"])
+    assert np.all(within(v, gv, *g["tolerance-var"]))
+    assert np.max(np.abs(v / gv - 1)) < 6e-4
+
+
+def test_kin_preprocess_with_transport_file(mech, chem_tr, tr, oracle):
+    """chemistry.py:636-687 with itran = 1 -> KINGetViscosity / KINGetMixtureViscosity (mass fractions)."""
+    from pychemkin_amd import kin
+
+    L = kin.bind()
+    cs = ct.c_int(0)
+    one = ct.c_int(1)
+    zero = ct.c_int(0)
+    names = [CHEM, "", THERM, TRAN, "chem.asc", "surf.asc", "tran.asc", ""]
+    rc = L.KINPreProcess(ct.byref(zero), ct.byref(one), *[ct.c_char_p(x.encode()) for x in names], ct.byref(cs))
+    assert rc == 0, kin.last_error()
+    try:
+        visc = np.zeros(mech.KK)
+        assert L.KINGetViscosity(ct.byref(cs), ct.byref(ct.c_double(1500.0)), visc) == 0
+        assert np.max(np.abs(visc / tr.species_viscosity([1500.0], chem_tr.viscosity_fits)[0] - 1)) < 1e-13
+        g = golden("CONV")
+        Y0 = ch4_air_Y(mech, 0.7)[0]
+        _, _, (ts, ys, ps, vs) = oracle.reactor(800.0, 3 * P_ATM, 10.0, Y0, t_save=np.asarray(g["state-time"]),
+                                                problem=2, energy=1, t_end=0.1, atol=1e-10, rtol=1e-8, nneg=True,
+                                                ign_mode="TIFP", profile=([0.0, 0.01, 2.0], [10.0, 4.0, 4.0]))
+        out = []
+        for i in range(len(ts)):
+            v = ct.c_double(0.0)
+            Y = np.ascontiguousarray(ys[i, 1:])
+            assert L.KINGetMixtureViscosity(ct.byref(cs), ct.byref(ct.c_double(ys[i, 0])), Y, ct.byref(v)) == 0
+            out.append(v.value)
+        gv = np.asarray(g["state-viscocity"])
+        assert np.all(within(np.array(out), gv, *g["tolerance-var"]))
+        assert np.max(np.abs(np.array(out) / gv - 1)) < 6e-4
+    finally:
+        kin.release(cs.value)
+    # without transport data the viscosity calls fail with a message
+    rc = L.KINPreProcess(ct.byref(zero), ct.byref(zero), *[ct.c_char_p(x.encode()) for x in names], ct.byref(cs))
+    assert rc == 0
+    try:
+        assert L.KINGetViscosity(ct.byref(cs), ct.byref(ct.c_double(1500.0)), np.zeros(mech.KK)) != 0
+        assert b"transport" in L.ckmi_kin_last_error()
+    finally:
+        kin.release(cs.value)
