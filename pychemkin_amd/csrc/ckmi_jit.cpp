@@ -13,8 +13,12 @@
 //
 // The source depends only on the mechanism's structure; lnA lives in the parameter block, so
 // ckmi_set_afactor updates it in place without recompiling.  Compiled code objects are cached
-// per process by source text.  Mechanisms with PLOG or chemically activated reactions keep the
-// generic kernel.
+// per process by source text.  Every reaction form of the device image is covered: elementary,
+// third-body, Lindemann / Troe / SRI falloff, chemically activated, PLOG (rows in the parameter
+// block, bracketing row picked per lane), Chebyshev (coefficients in the parameter block, the
+// recursions unrolled), Landau-Teller (+ RLT), explicit REV, and general reactions (FORD / RORD
+// orders, non-integral coefficients: C^o by the conc_pow rule of oracle/ckoracle.c, K_c from the
+// real coefficients).
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -79,6 +83,12 @@ __device__ __forceinline__ int jbb() {
   asm volatile("s_mov_b32 %0, 1" : "=s"(f));
   return f;
 }
+// C^o for a reaction order outside {0, 1, 2, 3} (oracle/ckoracle.c conc_pow): below 1 the chord
+// CFLOOR^(o-1) C under CFLOOR = 1e-14 (negative C included), otherwise C^o; above 1, 0 for C <= 0
+__device__ __forceinline__ double jcpow_lt1(double c, double o, double chord) {
+  return c < 1e-14 ? chord * c : jexp(o * log(c));
+}
+__device__ __forceinline__ double jcpow_gt1(double c, double o) { return c > 0.0 ? jexp(o * log(c)) : 0.0; }
 __device__ __forceinline__ double jrcp(double x) {
   double y = __builtin_amdgcn_rcp(x);
   double e = fma(-x, y, 1.0);
@@ -118,21 +128,34 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
   int wpe = eg ? 1 : 2;  // waves per SIMD the register allocation is held to
   if (const char* w = std::getenv("CKMI_JIT_WAVES")) wpe = std::max(1, std::atoi(w));
 
+  // general reactions: a non-integral coefficient or an order that differs from it (wide reactions
+  // with integral coefficients and default orders take the unit-coefficient path below)
+  std::vector<char> gen(II, 0);
+  bool any_plog = false, any_cheb = false, any_lt = false, any_gen = false;
   for (int i = 0; i < II; ++i) {
-    if (d->rtype[i] == CKMI_RXN_PLOG || d->rtype[i] == CKMI_RXN_CHEMACT || d->rtype[i] == CKMI_RXN_CHEB ||
-        d->rtype[i] == CKMI_RXN_LT) {
-      why = "PLOG / chemically activated / Chebyshev / Landau-Teller reactions";
-      return false;
-    }
-    if (rxn_general(d, i)) {
-      why = "FORD / RORD orders or non-integral stoichiometric coefficients";
-      return false;
-    }
-    if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_FALLOFF) {
+    const int t = d->rtype[i];
+    if (t < CKMI_RXN_ELEMENTARY || t > CKMI_RXN_LT) {
       why = "reaction type";
       return false;
     }
+    if ((t == CKMI_RXN_PLOG || t == CKMI_RXN_CHEB) && (!d->plog_ptr || !d->plog_par)) {
+      why = "PLOG / Chebyshev reaction without its table";
+      return false;
+    }
+    any_plog |= t == CKMI_RXN_PLOG;
+    any_cheb |= t == CKMI_RXN_CHEB;
+    any_lt |= t == CKMI_RXN_LT;
+    for (int u = 0; u < d->nr[i]; ++u) {
+      const double nu = d->rnu[CKMI_SLOTS * i + u];
+      if (nu != std::floor(nu) || nu < 1.0 || (d->ford && d->ford[CKMI_SLOTS * i + u] != nu)) gen[i] = 1;
+    }
+    for (int u = 0; u < d->np[i]; ++u) {
+      const double nu = d->pnu[CKMI_SLOTS * i + u];
+      if (nu != std::floor(nu) || nu < 1.0 || (d->rord && d->rord[CKMI_SLOTS * i + u] != nu)) gen[i] = 1;
+    }
+    any_gen |= gen[i] != 0;
   }
+  if (any_gen) eg = 0;  // the general reactions' K_c reads g_k / RT from e_k
   const int TH = KK, RX = TH + 15 * KK;
   prm.assign(RX + PRM_RX * II, 0.0);
   lnA_off.assign(II, 0);
@@ -146,16 +169,25 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
     }
   }
   // species of each reaction (unit-coefficient expansion) and the emission order
+  // rs / ps: unit-coefficient expansion (species repeated nu times); general reactions list each
+  // slot species once (their coefficients and orders are read from the slots)
   std::vector<std::vector<int>> rs(II), ps(II), used(II);
+  auto uses_m = [&](int i) {
+    const int t = d->rtype[i];
+    return t == CKMI_RXN_THIRDBODY || t == CKMI_RXN_FALLOFF || t == CKMI_RXN_CHEMACT;
+  };
   for (int i = 0; i < II; ++i) {
-    for (int u = 0; u < d->nr[i]; ++u)
-      for (int c = 0; c < (int)std::lround(d->rnu[CKMI_SLOTS * i + u]); ++c) rs[i].push_back(d->rsp[CKMI_SLOTS * i + u]);
-    for (int u = 0; u < d->np[i]; ++u)
-      for (int c = 0; c < (int)std::lround(d->pnu[CKMI_SLOTS * i + u]); ++c) ps[i].push_back(d->psp[CKMI_SLOTS * i + u]);
+    for (int u = 0; u < d->nr[i]; ++u) {
+      const int n = gen[i] ? 1 : (int)std::lround(d->rnu[CKMI_SLOTS * i + u]);
+      for (int c = 0; c < n; ++c) rs[i].push_back(d->rsp[CKMI_SLOTS * i + u]);
+    }
+    for (int u = 0; u < d->np[i]; ++u) {
+      const int n = gen[i] ? 1 : (int)std::lround(d->pnu[CKMI_SLOTS * i + u]);
+      for (int c = 0; c < n; ++c) ps[i].push_back(d->psp[CKMI_SLOTS * i + u]);
+    }
     std::vector<int> u = rs[i];
     u.insert(u.end(), ps[i].begin(), ps[i].end());
-    if (d->rtype[i] == CKMI_RXN_FALLOFF && d->tbsp[i] >= 0) u.push_back(d->tbsp[i]);
-    if (d->rtype[i] == CKMI_RXN_THIRDBODY && d->tbsp[i] >= 0) u.push_back(d->tbsp[i]);
+    if (uses_m(i) && d->tbsp[i] >= 0) u.push_back(d->tbsp[i]);
     std::sort(u.begin(), u.end());
     u.erase(std::unique(u.begin(), u.end()), u.end());
     used[i] = u;
@@ -191,6 +223,10 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
        "  const size_t s = live ? s0 : n - 1;\n  const size_t ns = n;\n";
   o << "  const double T = Tv[s], P = Pv[s];\n  const double lnT = log(T), invT = 1.0 / T;\n";
   o << "  const double rtp = CKJ_RU * T * (1.0 / 1.01325e6), prt = 1.01325e6 / (CKJ_RU * T);\n";
+  if (any_plog) o << "  const double lnP = log(P);\n";
+  if (any_cheb) o << "  const double lg10P = log(P) * 0.43429448190325176;\n";
+  if (any_lt) o << "  const double t13 = jexp(lnT * (-1.0 / 3.0)), t23 = t13 * t13;\n";
+  if (any_gen) o << "  const double lnPRT = log(prt);\n";
   o << "  double syw = 0.0, cpm = 0.0, hm = 0.0;\n";
   o << "  double";
   for (int k = 0; k < KK; ++k) o << (k ? "," : "") << " c" << k << ", e" << k << ", r" << k << ", w" << k;
@@ -200,7 +236,7 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
   std::vector<int> grp(II, -1);
   std::vector<char> effsp(KK, 0);
   for (int i = 0; i < II; ++i) {
-    if (d->rtype[i] == CKMI_RXN_ELEMENTARY || d->tbsp[i] >= 0) continue;
+    if (!uses_m(i) || d->tbsp[i] >= 0) continue;
     std::vector<std::pair<int, double>> key;
     for (int p = d->eff_ptr[i]; p < d->eff_ptr[i + 1]; ++p)
       if (d->eff_val[p] != 1.0) key.push_back({d->eff_sp[p], d->eff_val[p] - 1.0});
@@ -283,6 +319,7 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
     const int o0 = RX + PRM_RX * i;
     lnA_off[i] = o0;
     const int type = d->rtype[i], ft = d->ftype[i];
+    const bool fall = type == CKMI_RXN_FALLOFF || type == CKMI_RXN_CHEMACT;
     prm[o0 + 0] = d->arr[3 * i];
     prm[o0 + 1] = d->arr[3 * i + 1];
     prm[o0 + 2] = d->arr[3 * i + 2];
@@ -290,39 +327,97 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
     prm[o0 + 4] = d->low[3 * i + 1];
     prm[o0 + 5] = d->low[3 * i + 2];
     for (int c = 0; c < 5; ++c) prm[o0 + 6 + c] = d->fpar[5 * i + c];
-    if (ft == CKMI_FALL_TROE3 || ft == CKMI_FALL_TROE4) {  // exp(-T / T***), exp(-T / T*): store 1/T
+    if (fall && (ft == CKMI_FALL_TROE3 || ft == CKMI_FALL_TROE4)) {  // exp(-T / T***), exp(-T / T*): store 1/T
       prm[o0 + 7] = 1.0 / prm[o0 + 7];
       prm[o0 + 8] = 1.0 / prm[o0 + 8];
-    } else if (ft == CKMI_FALL_SRI) {
+    } else if (fall && ft == CKMI_FALL_SRI) {
       prm[o0 + 8] = 1.0 / prm[o0 + 8];
     }
     prm[o0 + 11] = d->revp[3 * i];
     prm[o0 + 12] = d->revp[3 * i + 1];
     prm[o0 + 13] = d->revp[3 * i + 2];
     o << "  { // reaction " << i + 1 << "\n";
-    std::string lk = "prm[" + std::to_string(o0) + "]";
-    const bool aonly = d->arr[3 * i + 1] == 0.0 && d->arr[3 * i + 2] == 0.0;
-    if (d->arr[3 * i + 1] != 0.0) lk += " + prm[" + std::to_string(o0 + 1) + "] * lnT";
-    if (d->arr[3 * i + 2] != 0.0) lk += " - prm[" + std::to_string(o0 + 2) + "] * invT";
-    if (aonly) {  // k = A: slot 1 holds A itself (kept in step with ln A by ckmi_set_afactor)
-      prm[o0 + 1] = std::exp(d->arr[3 * i]);
-      aonly_off.push_back(o0);
-      o << "    const double lkinf = " << lk << ";\n    const double kfi = prm[" << o0 + 1 << "];\n";
+    auto P_ = [&](int off) { return "prm[" + std::to_string(off) + "]"; };
+    if (type == CKMI_RXN_PLOG) {
+      // rows (ln P, ln A, b, E/R) ascending in P; the bracketing pair [j, j + 1] is the count of
+      // interior rows below ln P (oracle plog_rate's search), ln k linear in ln P, clamped outside
+      const int r0 = d->plog_ptr[i], n = d->plog_ptr[i + 1] - r0;
+      const int ab = (int)prm.size();
+      for (int q = 0; q < 4 * n; ++q) prm.push_back(d->plog_par[4 * r0 + q]);
+      o << "    int j = 0;\n";
+      for (int q = 1; q <= n - 2; ++q) o << "    j += lnP > " << P_(ab + 4 * q) << " ? 1 : 0;\n";
+      o << "    const double* t0 = prm + " << ab << " + 4 * j;\n";
+      o << "    const double lk0 = t0[1] + t0[2] * lnT - t0[3] * invT;\n";
+      if (n == 1) {
+        o << "    const double lkinf = lk0;\n";
+      } else {
+        o << "    const double lk1 = t0[5] + t0[6] * lnT - t0[7] * invT;\n";
+        o << "    const double w = fmin(fmax((lnP - t0[0]) / (t0[4] - t0[0]), 0.0), 1.0);\n";
+        o << "    const double lkinf = lk0 + w * (lk1 - lk0);\n";
+      }
+      o << "    const double kfi = jexp(lkinf);\n";
+    } else if (type == CKMI_RXN_CHEB) {
+      // rows (NT, NP), (Tmin, Tmax, Pmin, Pmax [atm]), a[t][p]: Tr, Pr as affine maps of 1/T and
+      // log10 P, both Chebyshev recursions unrolled (oracle cheb_rate)
+      const double* r = d->plog_par + 4 * d->plog_ptr[i];
+      const int nt = (int)r[0], npc = (int)r[1];
+      const double iTmin = 1.0 / r[4], iTmax = 1.0 / r[5];
+      const double lPmin = std::log10(r[6] * 1.01325e6), lPmax = std::log10(r[7] * 1.01325e6);
+      const int ab = (int)prm.size();
+      prm.push_back(2.0 / (iTmax - iTmin));
+      prm.push_back(-(iTmin + iTmax) / (iTmax - iTmin));
+      prm.push_back(2.0 / (lPmax - lPmin));
+      prm.push_back(-(lPmin + lPmax) / (lPmax - lPmin));
+      for (int q = 0; q < nt * npc; ++q) prm.push_back(r[8 + q]);
+      o << "    const double Tr = fma(" << P_(ab) << ", invT, " << P_(ab + 1) << ");\n";
+      o << "    const double Pr = fma(" << P_(ab + 2) << ", lg10P, " << P_(ab + 3) << ");\n";
+      for (int q = 0; q < npc; ++q) {
+        if (q == 0) o << "    const double cp0 = 1.0;\n";
+        else if (q == 1) o << "    const double cp1 = Pr;\n";
+        else o << "    const double cp" << q << " = 2.0 * Pr * cp" << q - 1 << " - cp" << q - 2 << ";\n";
+      }
+      for (int t = 0; t < nt; ++t) {
+        if (t == 0) o << "    const double ct0 = 1.0;\n";
+        else if (t == 1) o << "    const double ct1 = Tr;\n";
+        else o << "    const double ct" << t << " = 2.0 * Tr * ct" << t - 1 << " - ct" << t - 2 << ";\n";
+      }
+      o << "    double lk = 0.0;\n";
+      for (int t = 0; t < nt; ++t) {
+        o << "    { double row = 0.0;";
+        for (int q = 0; q < npc; ++q) o << " row += " << P_(ab + 4 + t * npc + q) << " * cp" << q << ";";
+        o << " lk += ct" << t << " * row; }\n";
+      }
+      o << "    const double lkinf = lk * 2.302585092994046;\n    const double kfi = jexp(lkinf);\n";
     } else {
-      o << "    const double lkinf = " << lk << ";\n    const double kfi = jexp(lkinf);\n";
+      std::string lk = P_(o0);
+      const bool aonly = type != CKMI_RXN_LT && d->arr[3 * i + 1] == 0.0 && d->arr[3 * i + 2] == 0.0;
+      if (d->arr[3 * i + 1] != 0.0) lk += " + " + P_(o0 + 1) + " * lnT";
+      if (d->arr[3 * i + 2] != 0.0) lk += " - " + P_(o0 + 2) + " * invT";
+      if (type == CKMI_RXN_LT) lk += " + " + P_(o0 + 3) + " * t13 + " + P_(o0 + 4) + " * t23";
+      if (aonly) {  // k = A: slot 1 holds A itself (kept in step with ln A by ckmi_set_afactor)
+        prm[o0 + 1] = std::exp(d->arr[3 * i]);
+        aonly_off.push_back(o0);
+        o << "    const double lkinf = " << lk << ";\n    const double kfi = " << P_(o0 + 1) << ";\n";
+      } else {
+        o << "    const double lkinf = " << lk << ";\n    const double kfi = jexp(lkinf);\n";
+      }
     }
     std::string mc;
-    if (type != CKMI_RXN_ELEMENTARY) mc = d->tbsp[i] >= 0 ? "c" + std::to_string(d->tbsp[i]) : "M" + std::to_string(grp[i]);
-    if (type == CKMI_RXN_FALLOFF) {
+    if (uses_m(i)) mc = d->tbsp[i] >= 0 ? "c" + std::to_string(d->tbsp[i]) : "M" + std::to_string(grp[i]);
+    if (fall) {
+      // falloff: the slot's Arrhenius is k_inf and LOW k0, Pr = k0 [M] / k_inf, k = k_inf Pr / (1 + Pr) F;
+      // chemically activated: the slot's Arrhenius is k0 and HIGH k_inf, Pr = k0 [M] / k_inf,
+      // k = k0 F / (1 + Pr)
+      const bool ca = type == CKMI_RXN_CHEMACT;
       o << "    const double Mc = " << mc << ";\n";
-      o << "    const double lnPr = (prm[" << o0 + 3 << "] + prm[" << o0 + 4 << "] * lnT - prm[" << o0 + 5
-        << "] * invT) - lkinf + log(Mc > 1e-300 ? Mc : 1e-300);\n";
+      o << "    const double lnlim = " << P_(o0 + 3) << " + " << P_(o0 + 4) << " * lnT - " << P_(o0 + 5) << " * invT;\n";
+      o << "    const double lnPr = " << (ca ? "lkinf - lnlim" : "lnlim - lkinf") << " + log(Mc > 1e-300 ? Mc : 1e-300);\n";
       o << "    const double Pr = jexp(lnPr);\n    double F = 1.0;\n";
       if (ft == CKMI_FALL_TROE3 || ft == CKMI_FALL_TROE4) {
         o << "    {\n      const double lPr = fmax(lnPr * 0.43429448190325176, -300.0);\n";
-        o << "      const double fa = prm[" << o0 + 6 << "];\n";
-        o << "      double Fc = (1.0 - fa) * jexp(-T * prm[" << o0 + 7 << "]) + fa * jexp(-T * prm[" << o0 + 8 << "]);\n";
-        if (ft == CKMI_FALL_TROE4) o << "      Fc += jexp(-prm[" << o0 + 9 << "] * invT);\n";
+        o << "      const double fa = " << P_(o0 + 6) << ";\n";
+        o << "      double Fc = (1.0 - fa) * jexp(-T * " << P_(o0 + 7) << ") + fa * jexp(-T * " << P_(o0 + 8) << ");\n";
+        if (ft == CKMI_FALL_TROE4) o << "      Fc += jexp(-" << P_(o0 + 9) << " * invT);\n";
         o << "      const double lnFc = log(Fc > 1e-300 ? Fc : 1e-300);\n";
         o << "      const double lFc = lnFc * 0.43429448190325176;\n";
         o << "      const double c = -0.4 - 0.67 * lFc, nn = 0.75 - 1.27 * lFc;\n";
@@ -331,18 +426,61 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
       } else if (ft == CKMI_FALL_SRI) {
         o << "    {\n      const double lPr = fmax(lnPr * 0.43429448190325176, -300.0);\n";
         o << "      const double X = 1.0 / (1.0 + lPr * lPr);\n";
-        o << "      F = prm[" << o0 + 9 << "] * pow(prm[" << o0 + 6 << "] * exp(-prm[" << o0 + 7
-          << "] * invT) + exp(-T * prm[" << o0 + 8 << "]), X) * pow(T, prm[" << o0 + 10 << "]);\n    }\n";
+        o << "      F = " << P_(o0 + 9) << " * pow(" << P_(o0 + 6) << " * exp(-" << P_(o0 + 7)
+          << " * invT) + exp(-T * " << P_(o0 + 8) << "), X) * pow(T, " << P_(o0 + 10) << ");\n    }\n";
       }
-      o << "    const double kf = kfi * (Pr / (1.0 + Pr)) * F;\n";
+      o << "    const double kf = " << (ca ? "kfi * (1.0 / (1.0 + Pr)) * F" : "kfi * (Pr / (1.0 + Pr)) * F") << ";\n";
     } else {
       o << "    const double kf = kfi;\n";
     }
-    o << "    double q = kf * (" << prod(rs[i], "c") << ");\n";
+    // concentration products: unit-coefficient products, or C^order per slot (general reactions)
+    auto cpow = [&](int k, double ord) -> std::string {
+      const std::string c = "c" + std::to_string(k);
+      if (ord == 0.0) return "1.0";
+      if (ord == 1.0) return c;
+      if (ord == 2.0) return "(" + c + " * " + c + ")";
+      if (ord == 3.0) return "(" + c + " * " + c + " * " + c + ")";
+      if (ord < 1.0) return "jcpow_lt1(" + c + ", " + lit(ord) + ", " + lit(std::pow(1e-14, ord - 1.0)) + ")";
+      return "jcpow_gt1(" + c + ", " + lit(ord) + ")";
+    };
+    std::string pf, pr;
+    if (gen[i]) {
+      for (int u = 0; u < d->nr[i]; ++u) {
+        const double nu = d->rnu[CKMI_SLOTS * i + u];
+        pf += (u ? " * " : "") + cpow(d->rsp[CKMI_SLOTS * i + u], d->ford ? d->ford[CKMI_SLOTS * i + u] : nu);
+      }
+      for (int u = 0; u < d->np[i]; ++u) {
+        const double nu = d->pnu[CKMI_SLOTS * i + u];
+        pr += (u ? " * " : "") + cpow(d->psp[CKMI_SLOTS * i + u], d->rord ? d->rord[CKMI_SLOTS * i + u] : nu);
+      }
+      if (pf.empty()) pf = "1.0";
+      if (pr.empty()) pr = "1.0";
+    } else {
+      pf = prod(rs[i], "c");
+      pr = prod(ps[i], "c");
+    }
+    o << "    double q = kf * (" << pf << ");\n";
     if (d->rev[i]) {
       if (d->has_rev[i]) {
-        o << "    double kr = jexp(prm[" << o0 + 11 << "] + prm[" << o0 + 12 << "] * lnT - prm[" << o0 + 13 << "] * invT);\n";
-        if (type == CKMI_RXN_FALLOFF) o << "    kr *= kf / kfi;\n";
+        std::string rl = P_(o0 + 11) + " + " + P_(o0 + 12) + " * lnT - " + P_(o0 + 13) + " * invT";
+        if (type == CKMI_RXN_LT) rl += " + " + P_(o0 + 6) + " * t13 + " + P_(o0 + 7) + " * t23";  // RLT
+        o << "    double kr = jexp(" << rl << ");\n";
+        if (fall) o << "    kr *= kf / kfi;\n";
+      } else if (gen[i]) {
+        // K_c from the real coefficients: kr = kf exp(sum nu'' g - sum nu' g - dnu ln(Patm / RT))
+        std::string dg;
+        double dnu = 0.0;
+        for (int u = 0; u < d->np[i]; ++u) {
+          const double nu = d->pnu[CKMI_SLOTS * i + u];
+          dg += " + " + lit(nu) + " * e" + std::to_string(d->psp[CKMI_SLOTS * i + u]);
+          dnu += nu;
+        }
+        for (int u = 0; u < d->nr[i]; ++u) {
+          const double nu = d->rnu[CKMI_SLOTS * i + u];
+          dg += " - " + lit(nu) + " * e" + std::to_string(d->rsp[CKMI_SLOTS * i + u]);
+          dnu -= nu;
+        }
+        o << "    const double kr = kf * jexp(0.0" << dg << " - " << lit(dnu) << " * lnPRT);\n";
       } else {
         // exp(dG) as products of exp(g_p) exp(-g_r) taken in (product, reactant) pairs, so that no
         // partial product leaves the FP64 range; (RT / Patm)^dnu for the mole change
@@ -367,17 +505,22 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
         for (int j = 0; j < std::abs(dnu); ++j) f += dnu > 0 ? " * rtp" : " * prt";
         o << "    const double kr = kf * (" << f << ");\n";
       }
-      o << "    q -= kr * (" << prod(ps[i], "c") << ");\n";
+      o << "    q -= kr * (" << pr << ");\n";
     }
     if (type == CKMI_RXN_THIRDBODY) o << "    q *= " << mc << ";\n";
-    std::map<int, int> net;
-    for (int k : rs[i]) net[k] -= 1;
-    for (int k : ps[i]) net[k] += 1;
+    std::map<int, double> net;
+    if (gen[i]) {
+      for (int u = 0; u < d->nr[i]; ++u) net[d->rsp[CKMI_SLOTS * i + u]] -= d->rnu[CKMI_SLOTS * i + u];
+      for (int u = 0; u < d->np[i]; ++u) net[d->psp[CKMI_SLOTS * i + u]] += d->pnu[CKMI_SLOTS * i + u];
+    } else {
+      for (int k : rs[i]) net[k] -= 1.0;
+      for (int k : ps[i]) net[k] += 1.0;
+    }
     for (auto& kv : net) {
-      if (kv.second == 0) continue;
-      if (kv.second == 1) o << "    w" << kv.first << " += q;\n";
-      else if (kv.second == -1) o << "    w" << kv.first << " -= q;\n";
-      else o << "    w" << kv.first << " = fma(" << lit((double)kv.second) << ", q, w" << kv.first << ");\n";
+      if (kv.second == 0.0) continue;
+      if (kv.second == 1.0) o << "    w" << kv.first << " += q;\n";
+      else if (kv.second == -1.0) o << "    w" << kv.first << " -= q;\n";
+      else o << "    w" << kv.first << " = fma(" << lit(kv.second) << ", q, w" << kv.first << ");\n";
     }
     o << "  }\n";
     for (int k : used[i])

@@ -107,20 +107,58 @@ def test_jit_zero_and_trace_compositions(tables, oracle, mech, jit_path):
     assert np.max(np.abs(w - wo) / scale) < 1e-11
 
 
-def test_jit_unavailable_for_plog_mechanism(jit_path):
-    """PLOG / chemically activated reactions: no specialised kernel; path 2 fails loudly, the
-    automatic path uses the generic kernel."""
-    from conftest import THERM
-    from test_plog import PLOG_CHEM
+EXT = {
+    "plog": ("gri30_plog_chem.inp", "grimech30_thermo.dat"),
+    "cheb": ("gri30_cheb_chem.inp", "grimech30_thermo.dat"),
+    "ford": ("gri30_ford_chem.inp", "grimech30_thermo.dat"),
+    "ext161": ("gri30_tracer161_ext_chem.inp", "gri30_tracer161_thermo.dat"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(EXT))
+def test_jit_every_reaction_form_matches_oracle(jit_path, name):
+    """PLOG (bracketing row per lane), Chebyshev, Landau-Teller (+ RLT), chemically activated, FORD /
+    RORD / fractional orders (the conc_pow rule) and wide reactions on the specialised kernel: same
+    bar as GRI-3.0 (1e-11 of the state's largest |wdot|), including states below the order floor."""
+    import os
+
+    from conftest import ROOT
+    from oracle.oracle import Oracle
 
     from pychemkin_amd import _native
     from pychemkin_amd.mechanism import Mechanism
 
-    pm = Mechanism.from_files(PLOG_CHEM, THERM)
-    dm = _native.DeviceMechanism(pm.to_tables())
+    chem, therm = EXT[name]
+    m = Mechanism.from_files(os.path.join(ROOT, "data", chem), os.path.join(ROOT, "data", therm))
+    dm = _native.DeviceMechanism(m.to_tables())
+    orc = Oracle(m)
+    n = 1500
+    rng = np.random.default_rng(11)
+    T = rng.uniform(300.0, 3000.0, n)
+    P = P_ATM * 10.0 ** rng.uniform(-2.5, 2.5, n)  # PLOG / Chebyshev clamps and extrapolation
+    Y = rng.dirichlet(0.5 * np.ones(m.KK), n).T.copy()
+    Y[:, :200] *= rng.uniform(0.0, 1.0, (m.KK, 200)) < 0.3  # exact zeros: C^o at and below the floor
+    Y[:, :200] /= np.maximum(Y[:, :200].sum(axis=0, keepdims=True), 1e-300)
+    Y[:, 0] = 0.0
+    Y[m.species.index("N2"), 0] = 1.0
+    w, cp, h = (x.cpu().numpy() for x in dm.rop_thermo(T, P, Y))
+    assert _jit_state(dm) == 1
+    wo, cpo, ho = orc.rop_batch(T, P, Y)
+    assert np.all(np.isfinite(w))
+    scale = np.maximum(np.max(np.abs(wo), axis=0, keepdims=True), 1e-300)
+    assert np.max(np.abs(w - wo) / scale) < 1e-11
+    assert np.max(np.abs(cp / cpo - 1)) < 1e-12
+
+
+def test_jit_disabled_fails_loudly_on_forced_path(jit_path, tables, monkeypatch):
+    """CKMI_ROP_JIT=0 at mechanism creation: path 2 raises, the automatic path runs the generic kernel."""
+    from pychemkin_amd import _native
+
+    monkeypatch.setenv("CKMI_ROP_JIT", "0")
+    dm = _native.DeviceMechanism(tables)
     assert _jit_state(dm) == -1
-    T, P, Y = _states(pm.KK, 70000, seed=3)
-    with pytest.raises(_native.NativeError):
+    T, P, Y = _states(int(tables["KK"]), 70000, seed=3)
+    with pytest.raises(_native.NativeError, match="CKMI_ROP_JIT"):
         dm.rop_thermo(T, P, Y)
     _native.set_rop_path(0)
     w = dm.rop_thermo(T, P, Y)[0].cpu().numpy()
