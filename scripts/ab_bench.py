@@ -67,15 +67,18 @@ print(json.dumps({"ms": e0.elapsed_time(e1) / 3, "wsum": float(wdot[:, :1000].ab
 
 
 def main():
-    libs = [a for a in sys.argv[1:] if a.endswith(".so")]
+    # a library argument may carry environment settings for its runs: lib.so@CKMI_JIT_ORDER=0@CKMI_JIT_WAVES=3
+    libs = [a for a in sys.argv[1:] if a.split("@")[0].endswith(".so")]
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
     rop = "--rop" in sys.argv
     n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else (4_000_000 if rop else 16384)
     out = {lib: [] for lib in libs}
     for _ in range(reps):
         for lib in libs:
-            env = dict(os.environ, CKMI_LIB=os.path.abspath(lib),
-                       AB_TAU_REF=os.path.join(ROOT, "gpurun_out", "ab_tau_%s.npy" % os.path.basename(libs[0])))
+            path, *sets = lib.split("@")
+            env = dict(os.environ, CKMI_LIB=os.path.abspath(path),
+                       AB_TAU_REF=os.path.join(ROOT, "gpurun_out", "ab_tau_%s.npy" % os.path.basename(libs[0].split("@")[0])))
+            env.update(kv.split("=", 1) for kv in sets)
             r = subprocess.run([sys.executable, "-c", (ROP_CHILD if rop else CHILD) % (ROOT, n)], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
