@@ -224,7 +224,13 @@ int ckmi_reaction_rates(const ckmi_mech* mech, int32_t n, const double* T, const
                         double* qf, double* qr, void* stream);
 
 /* Batched closed homogeneous reactors.
- *   problem[n]   1 CONP (given pressure), 2 CONV (given volume)
+ *   problem[n]   1 CONP (given pressure), 2 CONV (given volume), 3 plug flow (PFR: the integration
+ *                variable is the distance x [cm]; t_end / t_save / profiles / tau are in cm; V0 is the
+ *                inlet velocity [cm/s] and Vend the outlet velocity; constant flow area; the pressure
+ *                from the inviscid momentum equation P + rho u^2 = P0 + rho0 u0^2, or the PPRO
+ *                profile in x; replaces KINAll0D_SetupPFRInputs + KINAll0D_Calculate,
+ *                chemkin_wrapper.py / flowreactors/PFR.py:498-512.  Wall heat-loss fields are not
+ *                applied to plug-flow reactors; the front ends reject them.)
  *   T0, P0, V0   [n] initial temperature [K], pressure [dyn/cm2], volume [cm3]
  *   Y0           [n][KK] initial mass fractions (reactor-major)
  *   tau          [n] ignition delay [s] (-1 if not detected)

@@ -301,6 +301,7 @@ typedef struct {
   double V0, P0, T0;
   int nfe, nje;
   double tsel; /* midpoint of the current integration segment (pwl_eval) */
+  double G, Pm; /* plug flow (problem 3): mass flux rho0 u0 [g/cm2-s], momentum constant P0 + G u0 */
 } rctx;
 
 /* piecewise-linear profile at t; the linear piece is the one containing tsel, the midpoint of
@@ -335,6 +336,25 @@ static double prof2_value(const cko_cfg* c, double t, double tsel, double base, 
   return v;
 }
 
+/* Plug-flow reactor (problem 3, Chemkin PLUG without surface chemistry, constant flow area): the
+ * independent variable is the distance x [cm] and dy/dx = (rho / G) dy/dt of a constant-pressure
+ * batch reactor at the local state, G = rho u the constant mass flux.  The pressure follows the
+ * inviscid momentum equation A dP/dx + mdot du/dx = 0, i.e. P + G u = P0 + G u0 with u = G / rho =
+ * G R T / (P Wbar): the subsonic root of P^2 - Pm P + G^2 R T / Wbar = 0.  With a PPRO profile the
+ * pressure is given instead (MOMEN OFF, PFR.py:515-518) and its dP/dx enters the energy equation as
+ * u dP/dx; the u dP/dx of the momentum equation and the kinetic energy are dropped there (both
+ * O(u^2 / (cp T)), 5e-8 relative at the plugflow golden's 27 cm/s). */
+static double pfr_pressure(const rctx* c, double t, double tsel, double T, double Wbar, double* dPdx) {
+  if (c->cfg->nprof > 0 && c->cfg->prof_kind == 0) {
+    double P;
+    pwl_eval(c->cfg->prof_t, c->cfg->prof_v, c->cfg->nprof, t, tsel, &P, dPdx);
+    return P;
+  }
+  *dPdx = 0.0;
+  const double q = c->G * c->G * RU * T / Wbar;
+  return 0.5 * (c->Pm + sqrt(c->Pm * c->Pm - 4.0 * q));
+}
+
 static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J) {
   const cko_mech* m = c->m;
   const int KK = m->KK, n = KK + 1;
@@ -345,9 +365,16 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
   const double* Y = y + 1;
   double C[NMAX], cp_R[NMAX], h_RT[NMAX], s_R[NMAX], g_RT[NMAX], Ctot;
   double rho, P, V, dVdt = 0.0, dPdt = 0.0;
-  const int conp = (c->problem == 1);
+  const int pfr = (c->problem == 3);
+  const int conp = (c->problem == 1) || pfr;
   double Wbar = mean_wt(m, Y);
-  if (conp) {
+  if (pfr) {
+    double dPdx;
+    P = pfr_pressure(c, t, c->tsel, T, Wbar, &dPdx);
+    rho = P * Wbar / (RU * T);
+    V = c->G / rho; /* the local velocity */
+    dPdt = V * dPdx;
+  } else if (conp) {
     profile_eval(c->cfg, t, c->tsel, c->P0, &P, &dPdt);
     rho = P * Wbar / (RU * T);
     V = c->mass_density0 * c->V0 / rho;
@@ -451,6 +478,13 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
       for (int k = 0; k < KK; ++k) J[(1 + k) * n] = dwdT[k] * m->wt[k] * rinv + (conp ? f[1 + k] * invT : 0.0);
     }
   }
+  if (pfr) { /* d/dx = (rho / G) d/dt; the Jacobian keeps the batch form scaled alike */
+    const double sx = rho / c->G;
+    if (c->cfg->energy == 1 || !tpro) f[0] *= sx;  /* a TPRO profile is already T(x) */
+    for (int k = 0; k < KK; ++k) f[1 + k] *= sx;
+    if (J)
+      for (int i = 0; i < n * n; ++i) J[i] *= sx;
+  }
   c->nfe++;
   if (J) c->nje++;
 }
@@ -458,6 +492,10 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
 void cko_rhs_jac(const cko_mech* m, const cko_cfg* cfg, double t, const double* y, double mass_density0,
                  double V0, double P0, double* f, double* J) {
   rctx c = {m, cfg, cfg->problem, mass_density0, V0, P0, y[0], 0, 0, t};
+  if (cfg->problem == 3) { /* plug flow: V0 = inlet velocity, mass_density0 = inlet density */
+    c.G = mass_density0 * V0;
+    c.Pm = P0 + c.G * V0;
+  }
   reactor_rhs(&c, t, y, f, J);
 }
 
@@ -1038,7 +1076,11 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   double Vstart = V0;
   if (cfg->problem == 2 && cfg->nprof > 0 && cfg->prof_kind == 0) Vstart = cfg->prof_v[0];
   rctx ctx = {m, cfg, cfg->problem, rho0, Vstart, P0, T0, 0, 0};
-  if (cfg->problem == 1 && cfg->nprof > 0 && cfg->prof_kind == 0) ctx.P0 = cfg->prof_v[0];
+  if ((cfg->problem == 1 || cfg->problem == 3) && cfg->nprof > 0 && cfg->prof_kind == 0) ctx.P0 = cfg->prof_v[0];
+  if (cfg->problem == 3) { /* plug flow: V0 is the inlet velocity u0 [cm/s] */
+    ctx.G = ctx.P0 * Wbar0 / (RU * T0) * V0;
+    ctx.Pm = ctx.P0 + ctx.G * V0;
+  }
   b->ctx = &ctx;
   const double tend = cfg->t_end;
   const double hmax = cfg->hmax > 0.0 ? cfg->hmax : tend / 100.0;
@@ -1113,7 +1155,10 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
       dky_vec(b, t_save[isave], ys);
       for (int i = 0; i < n; ++i) y_save[(size_t)isave * n + i] = ys[i];
       double Wb = mean_wt(m, ys + 1), rho, P, V, d;
-      if (cfg->problem == 1) {
+      if (cfg->problem == 3) {
+        P = pfr_pressure(&ctx, t_save[isave], t_save[isave], ys[0], Wb, &d);
+        V = ctx.G / (P * Wb / (RU * ys[0])); /* velocity */
+      } else if (cfg->problem == 1) {
         profile_eval(cfg, t_save[isave], t_save[isave], ctx.P0, &P, &d);
         rho = P * Wb / (RU * ys[0]);
         V = rho0 * Vstart / rho;
@@ -1174,7 +1219,10 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
     res->t_end = tf;
     res->T = yf[0];
     double Wb = mean_wt(m, yf + 1), d;
-    if (cfg->problem == 1) {
+    if (cfg->problem == 3) {
+      res->P = pfr_pressure(&ctx, tf, tf, yf[0], Wb, &d);
+      res->V = ctx.G / (res->P * Wb / (RU * yf[0]));
+    } else if (cfg->problem == 1) {
       profile_eval(cfg, tf, tf, ctx.P0, &res->P, &d);
       res->V = rho0 * Vstart / (res->P * Wb / (RU * yf[0]));
     } else {

@@ -1,7 +1,8 @@
 """pychemkin_amd -- MI355X-native batched batch-reactor engine with a PyChemkin-compatible API.
 
 Drop-in names for the reference's batch-reactor path (``ansys.chemkin``, __init__.py:37-81):
-Chemistry, Mixture, the four closed-homogeneous batch reactors, constants, logger; plus the
+Chemistry, Mixture, the four closed-homogeneous batch reactors, constants, logger, the inlet Stream
+and the plug-flow reactors (``pychemkin_amd.flowreactors.PFR``, on the same kernels); plus the
 batched entry point BatchSweep.  Numerics run in hand-written gfx950 HIP kernels
 (libckmi.so, include/ckmi.h).  Units are cgs as the reference sets with KINSetUnitSystem(1).
 """
@@ -27,6 +28,7 @@ from .constants import (
     Air,
     air,
 )
+from .inlet import Stream
 from .logger import logger
 from .mixture import (Mixture, adiabatic_mixing, calculate_mixture_temperature_from_enthalpy, interpolate_mixtures,
                       isothermal_mixing)

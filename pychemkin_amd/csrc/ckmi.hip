@@ -60,7 +60,10 @@ __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, dou
   const double T = bcast(yl, 0);
   const double Wb = 1.0 / wave_sum(isp ? yl * M.rwt()[lane - 1] : 0.0);
   double d;
-  if (R.conp) {
+  if (R.pfr) {
+    P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, t, T, Wb, d);
+    V = R.G / (P * Wb / (RU * T));  // velocity
+  } else if (R.conp) {
     profile_eval(R.cfg, R.npv, t, t, R.P0, P, d);
     const double rho = P * Wb / (RU * T);
     V = R.rho0 * R.V0 / rho;
@@ -195,7 +198,8 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           if (lane == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + lane - 1];
           const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
-          R.conp = (prob == 1);
+          R.pfr = (prob == 3);
+          R.conp = (prob == 1 || prob == 3);
           R.energy = cfg->energy;
           R.npv = cfg->prof_kind == 0 ? cfg->nprof : 0;
           R.ntp = (cfg->prof_kind == 1 && cfg->energy == 2) ? cfg->nprof : 0;
@@ -203,6 +207,10 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           R.V0 = (!R.conp && R.npv > 0) ? cfg->prof_v[0] : io.V0[r];
           R.P0 = (R.conp && R.npv > 0) ? cfg->prof_v[0] : P0;
           R.mass = R.rho0 * R.V0;
+          if (R.pfr) {  // plug flow: V0 is the inlet velocity u0 [cm/s]
+            R.G = R.P0 * Wbar0 / (RU * T0) * R.V0;
+            R.Pm = R.P0 + R.G * R.V0;
+          }
           R.gfac = cfg->gfac;
           R.qloss = cfg->qloss;
           R.htc = cfg->htc;

@@ -812,7 +812,13 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
   const double Wbar = 1.0 / sumYW;
   const int conp = R.conp;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
-  if (conp) {
+  if (R.pfr) {  // plug flow in x (ckmi_reactor.hpp pfr_pressure)
+    double dPdx;
+    P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, R.tsel, T, Wbar, dPdx);
+    rho = P * Wbar / (RU * T);
+    V_ = R.G / rho;
+    dPdt = V_ * dPdx;
+  } else if (conp) {
     profile_eval(R.cfg, R.npv, t, R.tsel, R.P0, P, dPdt);
     rho = P * Wbar / (RU * T);
     V_ = R.rho0 * R.V0 / rho;
@@ -821,6 +827,7 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
     rho = R.rho0 * R.V0 / V_;
     P = rho * RU * T / Wbar;
   }
+  const float jsx = R.pfr ? (float)(rho / R.G) : 1.0f;  // plug flow: d/dx = (rho / G) d/dt
   const double lnT = log(T), invT = 1.0 / T, lnPRT = LN_PATM_RU - lnT;
   double* C = lds_at<double>(L.C);
   double* gRT = lds_at<double>(L.gRT);
@@ -924,12 +931,13 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
     if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
     if (R.na > 0) pwl_eval(R.a_t, R.a_v, R.na, t, R.tsel, area, dummy);
     mcp = R.mass * cpm;
-    q1 = R.htc * area * ERG_PER_CAL;
-    fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
+    q1 = R.pfr ? 0.0 : R.htc * area * ERG_PER_CAL;  // plug flow: no wall heat loss on this path
+    if (!R.pfr) fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
     if (tid == 0) fl = fT;
   } else if (tid == 0) {
     fl = dTdt_given;  // 0 without TPRO
   }
+  if (R.pfr && (tid != 0 || R.energy == 1 || R.ntp == 0)) fl *= rho / R.G;  // a TPRO profile is T(x)
   if (!with_j) return fl;
 
   // ---------------- Jacobian: column 0 (d/dT) and J[0][0]
@@ -937,12 +945,12 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
   const double dws = isp ? ((dw0[s] + dw0[KKp + s]) + (dw0[2 * KKp + s] + dw0[3 * KKp + s])) : 0.0;
   const double JkT = isp ? dws * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;
   if (isp) {
-    Jg[jslot(tid, 0, NB)] = (float)JkT;
+    Jg[jslot(tid, 0, NB)] = (float)JkT * jsx;
     lds_at<double>(L.ek)[s] = ekv;
   }
   if (R.energy == 1) {
     const double s2 = bsum(B, ck * fY + ekv * JkT, wid, lane);  // also orders the ek writes
-    if (tid == 0) Jg[0] = (float)(-s2 / cpm - q1 / mcp);
+    if (tid == 0) Jg[0] = (float)(-s2 / cpm - q1 / mcp) * jsx;
   } else {
     if (tid == 0) Jg[0] = 0.0f;
     __syncthreads();
@@ -1005,7 +1013,7 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
     __syncthreads();
     for (int idx = tid; idx < jcb * NT; idx += NT) {
       const int col = c0 + idx / NT, row = idx % NT;
-      if (col < n && row < n) Jg[jslot(row, col, NB)] = (float)jb[(col - c0) * LDJ + row];
+      if (col < n && row < n) Jg[jslot(row, col, NB)] = (float)jb[(col - c0) * LDJ + row] * jsx;
     }
     __syncthreads();
   }
@@ -1100,7 +1108,8 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           if (tid == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + tid - 1];
           const double Wbar0 = 1.0 / bsum(B, isp ? yl * V.rwt()[tid - 1] : 0.0, wid, lane);
-          R.conp = (prob == 1);
+          R.pfr = (prob == 3);
+          R.conp = (prob == 1 || prob == 3);
           R.energy = cfg->energy;
           R.npv = cfg->prof_kind == 0 ? cfg->nprof : 0;
           R.ntp = (cfg->prof_kind == 1 && cfg->energy == 2) ? cfg->nprof : 0;
@@ -1108,6 +1117,10 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           R.V0 = (!R.conp && R.npv > 0) ? cfg->prof_v[0] : io.V0[r];
           R.P0 = (R.conp && R.npv > 0) ? cfg->prof_v[0] : P0;
           R.mass = R.rho0 * R.V0;
+          if (R.pfr) {  // plug flow: V0 is the inlet velocity u0 [cm/s]
+            R.G = R.P0 * Wbar0 / (RU * T0) * R.V0;
+            R.Pm = R.P0 + R.G * R.V0;
+          }
           R.gfac = cfg->gfac;
           R.qloss = cfg->qloss;
           R.htc = cfg->htc;
@@ -1663,7 +1676,10 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           const double sYW = bsum_bcast(B, isp ? yf * V.rwt()[tid - 1] : 0.0, Tf, 0, tid, wid, lane);
           const double Wb = 1.0 / sYW;
           double Pf, Vf, d;
-          if (R.conp) {
+          if (R.pfr) {
+            Pf = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, tf, tf, Tf, Wb, d);
+            Vf = R.G / (Pf * Wb / (RU * Tf));
+          } else if (R.conp) {
             profile_eval(R.cfg, R.npv, tf, tf, R.P0, Pf, d);
             Vf = R.rho0 * R.V0 / (Pf * Wb / (RU * Tf));
           } else {

@@ -64,8 +64,10 @@ struct Profile {
 // the one configured 0-D reactor (KINAll0D_*), as in the reference's native library
 struct Reactor0D {
   int chemset = 0, problem = 0, energy = 0;
+  int reactortype = 1;  // 1 batch, 3 plug flow (problem 3 of ckmi_reactor_run: x [cm] is the variable)
   bool setup = false, inputs = false;
   double t_end = 0, T0 = 0, P0 = 0, V0 = 0, qloss = 0;
+  double x0 = 0;        // plug flow: start position [cm] (output positions are x0 + the integration variable)
   std::vector<double> Y0;
   std::vector<std::pair<std::string, std::string>> kw;  // keyword, value text (in order)
   std::vector<Profile> prof;
@@ -173,8 +175,11 @@ int species_index(const ChemSet* s, const std::string& name) {
 // and everything else rejected with a message.
 const char* const KW_DEVICE[] = {"ATOL", "RTOL", "HO", "STPT", "NNEG", "TIFP", "DTIGN", "TLIM", "KLIM", "IGN_STOP",
                                  "DTSV", "ADAP", "ASTEPS", "AVAR", "AVALUE", "GFAC", "QLOS", "HTC", "TAMB", "AREAQ",
-                                 "MAXIT", "NSTP"};
-const char* const KW_NOEFFECT[] = {"DELT", "VOL", "AREA", "NADAP", "NO_SDOUTPUT_WRITE", "NO_XMLOUTPUT_WRITE"};
+                                 "MAXIT", "NSTP", "DXMX"};
+// RTIME (residence time output), MOMEN (the momentum equation is always on unless PPRO is given) and
+// AREAF (the flow area comes with KINAll0D_SetupPFRInputs' diameter) are the plug-flow reactor's
+const char* const KW_NOEFFECT[] = {"DELT", "VOL", "AREA", "NADAP", "NO_SDOUTPUT_WRITE", "NO_XMLOUTPUT_WRITE",
+                                   "RTIME", "MOMEN", "AREAF"};
 int keyword_class(const std::string& k) {
   for (const char* x : KW_DEVICE)
     if (k == x) return 1;
@@ -200,7 +205,7 @@ int apply_keywords(const ChemSet* s, ckmi_reactor_cfg& c, double& dtsv, bool& ad
     if (k == "ATOL") ok = num(c.atol);
     else if (k == "RTOL") ok = num(c.rtol);
     else if (k == "HO") ok = num(c.h0);
-    else if (k == "STPT") ok = num(c.hmax);
+    else if (k == "STPT" || k == "DXMX") ok = num(c.hmax);
     else if (k == "NNEG") c.nneg = 1;
     else if (k == "TIFP") c.ign_mode = 1;
     else if (k == "DTIGN") { c.ign_mode = 2; ok = num(c.ign_val); }
@@ -241,7 +246,8 @@ int apply_profiles(ckmi_reactor_cfg& c) {
     if (np < 1 || np > 64) return fail(CKMI_ERR_ARG, "profile " + p.key + " must have 1..64 points");
     if (p.key == "VPRO" || p.key == "PPRO" || p.key == "TPRO") {
       if (p.key == "VPRO" && g_r.problem != 2) return fail(CKMI_ERR_ARG, "VPRO needs a given-volume (CONV) reactor");
-      if (p.key == "PPRO" && g_r.problem != 1) return fail(CKMI_ERR_ARG, "PPRO needs a given-pressure (CONP) reactor");
+      if (p.key == "PPRO" && g_r.problem != 1 && g_r.problem != 3)
+        return fail(CKMI_ERR_ARG, "PPRO needs a given-pressure (CONP) or plug-flow reactor");
       if (p.key == "TPRO" && g_r.energy != 2) return fail(CKMI_ERR_ARG, "TPRO needs a fixed-temperature reactor");
       c.nprof = np;
       c.prof_kind = p.key == "TPRO" ? 1 : 0;
@@ -298,7 +304,20 @@ int run_reactor(ChemSet* s) {
   int rc = apply_keywords(s, c, dtsv, adap);
   if (!rc) rc = apply_profiles(c);
   if (rc) return rc;
-  const std::vector<double> ts = save_times(g_r.t_end, dtsv);
+  const bool pfr = g_r.problem == 3;
+  std::vector<double> ts;
+  if (pfr) {
+    // plug flow: DTSV [s] becomes the distance DTSV u0 between saved points, and the points are
+    // 0, dx, 2 dx, ... <= the length (the reference's plugflow golden: 373 points, no end point)
+    if (c.qloss != 0.0 || c.htc != 0.0 || c.nprof2 > 0)
+      return fail(CKMI_ERR_UNSUPPORTED, "wall heat loss of a plug-flow reactor is not on this path");
+    bool have_dtsv = false;
+    for (const auto& kv : g_r.kw) have_dtsv = have_dtsv || kv.first == "DTSV";
+    const double dx = have_dtsv ? dtsv * g_r.V0 : g_r.t_end / 100.0;
+    for (int i = 0; i * dx <= g_r.t_end * (1.0 + 1e-12); ++i) ts.push_back(std::min(i * dx, g_r.t_end));
+  } else {
+    ts = save_times(g_r.t_end, dtsv);
+  }
   const int nsave = (int)ts.size();
   const int max_adap = adap ? MAX_ADAP : 0;
   (void)hipSetDevice(s->device);
@@ -384,7 +403,7 @@ int run_reactor(ChemSet* s) {
   for (int k = 0; k < KK; ++k) sw0 += g_r.Y0[k] / s->wt[k];
   const Profile* pp = nullptr;
   for (const Profile& p : g_r.prof)
-    if ((g_r.problem == 1 && p.key == "PPRO") || (g_r.problem == 2 && p.key == "VPRO")) pp = &p;
+    if (((g_r.problem == 1 || pfr) && p.key == "PPRO") || (g_r.problem == 2 && p.key == "VPRO")) pp = &p;
   const double Vs = (g_r.problem == 2 && pp) ? pp->y.front() : hin[2];
   const double rho0 = g_r.P0 / (RU * g_r.T0 * sw0);
   g_r.t.clear(), g_r.T.clear(), g_r.P.clear(), g_r.V.clear(), g_r.Y.clear();
@@ -393,14 +412,19 @@ int run_reactor(ChemSet* s) {
     double sw = 0.0;
     for (int k = 0; k < KK; ++k) sw += pt.second[1 + k] / s->wt[k];
     double P, V;
-    if (g_r.problem == 1) {
+    if (pfr) {  // momentum (ckmi.h problem 3) or PPRO; V = the velocity
+      const double Pin = pp ? pp->y.front() : g_r.P0;
+      const double G = Pin / (RU * g_r.T0 * sw0) * g_r.V0, Pm = Pin + G * g_r.V0;
+      P = pp ? pwl(pp->x, pp->y, t) : 0.5 * (Pm + std::sqrt(Pm * Pm - 4.0 * G * G * RU * T * sw));
+      V = G / (P / (RU * T * sw));
+    } else if (g_r.problem == 1) {
       P = pp ? pwl(pp->x, pp->y, t) : g_r.P0;
       V = rho0 * Vs / (P / (RU * T * sw));
     } else {
       V = pp ? pwl(pp->x, pp->y, t) : Vs;
       P = (rho0 * Vs / V) * RU * T * sw;
     }
-    g_r.t.push_back(t);
+    g_r.t.push_back(pfr ? g_r.x0 + t : t);
     g_r.T.push_back(T);
     g_r.P.push_back(P);
     g_r.V.push_back(V);
@@ -663,13 +687,15 @@ int KINAll0D_Setup(int* chemset, int* reactortype, int* problem, int* energy, in
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   (void)npsr, (void)ninlets, (void)nzones;
   if (!get_set(chemset)) return fail(CKMI_ERR_ARG, "unknown chemistry set");
-  if (!reactortype || *reactortype != 1) return fail(CKMI_ERR_UNSUPPORTED, "only closed batch reactors (type 1)");
+  if (!reactortype || (*reactortype != 1 && *reactortype != 3))
+    return fail(CKMI_ERR_UNSUPPORTED, "only closed batch reactors (type 1) and plug-flow reactors (type 3)");
   if (!solver || *solver != 1) return fail(CKMI_ERR_UNSUPPORTED, "only the transient solver (1)");
   if (!problem || (*problem != 1 && *problem != 2)) return fail(CKMI_ERR_ARG, "problem must be 1 (CONP) or 2 (CONV)");
   if (!energy || (*energy != 1 && *energy != 2)) return fail(CKMI_ERR_ARG, "energy must be 1 (ENRG) or 2 (TGIV)");
   g_r = Reactor0D();
   g_r.chemset = *chemset;
-  g_r.problem = *problem;
+  g_r.reactortype = *reactortype;
+  g_r.problem = *reactortype == 3 ? 3 : *problem;  // PFR.py:75 sets CONP; x is the variable (problem 3)
   g_r.energy = *energy;
   g_r.setup = true;
   return CKMI_OK;
@@ -688,12 +714,47 @@ int KINAll0D_SetupBatchInputs(int* chemset, double* t_end, double* T, double* P,
   (void)area, (void)site, (void)bulk;  // reactive surface area, site / bulk fractions: no surface chemistry
   ChemSet* s = get_set(chemset);
   if (!s || !g_r.setup || *chemset != g_r.chemset) return fail(CKMI_ERR_ARG, "KINAll0D_Setup first");
+  if (g_r.reactortype != 1) return fail(CKMI_ERR_ARG, "KINAll0D_SetupBatchInputs on a plug-flow reactor");
   if (!t_end || !T || !P || !Y || !(*t_end > 0.0) || !(*T > 0.0) || !(*P > 0.0))
     return fail(CKMI_ERR_ARG, "TIME, temperature and pressure must be > 0");
   g_r.t_end = *t_end;
   g_r.T0 = *T;
   g_r.P0 = *P;
   g_r.V0 = V ? *V : 0.0;
+  g_r.qloss = qloss ? *qloss : 0.0;
+  g_r.Y0.assign(Y, Y + s->KK);
+  g_r.kw.clear();
+  g_r.prof.clear();
+  g_r.inputs = true;
+  g_r.done = false;
+  return CKMI_OK;
+}
+
+// KINAll0D_SetupPFRInputs (chemkin_wrapper.py:643-656, flowreactors/PFR.py:498-512): start position,
+// end position (XEND) [cm], inlet T [K] and P [dyn/cm2], heat loss, diameter [cm], site / bulk
+// fractions (no surface chemistry), inlet mass flow rate [g/s], inlet mass fractions.  The reactor
+// runs as problem 3 of ckmi_reactor_run: x - x0 is the integration variable and the inlet velocity
+// mdot / (rho A), A = pi d^2 / 4, the per-reactor V0.
+int KINAll0D_SetupPFRInputs(int* chemset, double* x0, double* xend, double* T, double* P, double* qloss,
+                            double* diam, double* site, double* bulk, double* mdot, double* Y) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  (void)site, (void)bulk;
+  ChemSet* s = get_set(chemset);
+  if (!s || !g_r.setup || *chemset != g_r.chemset) return fail(CKMI_ERR_ARG, "KINAll0D_Setup first");
+  if (g_r.reactortype != 3) return fail(CKMI_ERR_ARG, "KINAll0D_SetupPFRInputs needs reactor type 3 (PFR)");
+  if (!x0 || !xend || !T || !P || !diam || !mdot || !Y || !(*xend > *x0) || !(*T > 0.0) || !(*P > 0.0) ||
+      !(*diam > 0.0) || !(*mdot > 0.0))
+    return fail(CKMI_ERR_ARG, "PFR inputs: XEND > start, T, P, diameter and mass flow rate must be > 0");
+  double sw = 0.0;
+  for (int k = 0; k < s->KK; ++k) sw += Y[k] / s->wt[k];
+  if (!(sw > 0.0)) return fail(CKMI_ERR_ARG, "PFR inlet composition sums to zero");
+  const double rho = *P / (RU * *T * sw);
+  const double area = 3.14159265358979323846 * *diam * *diam / 4.0;
+  g_r.x0 = *x0;
+  g_r.t_end = *xend - *x0;
+  g_r.T0 = *T;
+  g_r.P0 = *P;
+  g_r.V0 = *mdot / (rho * area);
   g_r.qloss = qloss ? *qloss : 0.0;
   g_r.Y0.assign(Y, Y + s->KK);
   g_r.kw.clear();
@@ -1259,8 +1320,6 @@ CKMI_OUT_OF_SCOPE(KINCalculateEqGasWithOption, "the equilibrium solver", int*, i
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupPSRReactorInputs, "the PSR model", int*, int*, double*, double*, double*, double*,
                   double*, double*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupPSRInletInputs, "the PSR model", int*, int*, int*, double*, double*, double*)
-CKMI_OUT_OF_SCOPE(KINAll0D_SetupPFRInputs, "the PFR model", int*, double*, double*, double*, double*, double*,
-                  double*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupHCCIInputs, "the HCCI engine model", int*, double*, double*, double*, double*,
                   double*, double*, double*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupHCCIZoneInputs, "the HCCI engine model", int*, int*, double*, double*)

@@ -47,6 +47,8 @@ constexpr int LDJ = WAVE + 1;  // leading dimension of the shared J scratch (odd
 
 struct RunCtx {
   int conp, energy;
+  int pfr;                   // problem 3: plug flow in x [cm] (conp = 1 as well)
+  double G, Pm;              // plug flow: mass flux rho0 u0, momentum constant P0 + G u0
   int npv;     // VPRO / PPRO profile points (0 = constant V / P)
   int ntp;     // TPRO profile points (given-temperature runs, 0 = T from the state)
   int pslot;   // device slot of the reaction whose A is perturbed (-1 none), and ln(factor)
@@ -77,6 +79,19 @@ __device__ __forceinline__ void pwl_eval(const double* x, const double* y, int n
   const double s = (y[j + 1] - y[j]) / (x[j + 1] - x[j]);
   v = y[j] + s * (t - x[j]);
   dvdt = s;
+}
+// Plug flow (problem 3, oracle/ckoracle.c pfr_pressure): the pressure from the inviscid momentum
+// equation P + G u = Pm (u = G R T / (P Wbar), the subsonic root), or the PPRO profile in x.
+__device__ __forceinline__ double pfr_pressure(const ckmi_reactor_cfg* c, int npv, double G, double Pm, double t,
+                                               double tsel, double T, double Wbar, double& dPdx) {
+  if (npv > 0) {
+    double P;
+    pwl_eval(c->prof_t, c->prof_v, npv, t, tsel, P, dPdx);
+    return P;
+  }
+  dPdx = 0.0;
+  const double q = G * G * RU * T / Wbar;
+  return 0.5 * (Pm + sqrt(Pm * Pm - 4.0 * q));
 }
 // VPRO / PPRO / TPRO slot
 __device__ __forceinline__ void profile_eval(const ckmi_reactor_cfg* c, int nprof, double t, double tsel, double base,
@@ -191,7 +206,13 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const double Wbar = 1.0 / sumYW;
   const int conp = R.conp;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
-  if (conp) {
+  if (R.pfr) {
+    double dPdx;
+    P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, R.tsel, T, Wbar, dPdx);
+    rho = P * Wbar / (RU * T);
+    V_ = R.G / rho;  // the local velocity
+    dPdt = V_ * dPdx;
+  } else if (conp) {
     profile_eval(R.cfg, R.npv, t, R.tsel, R.P0, P, dPdt);
     rho = P * Wbar / (RU * T);
     V_ = R.rho0 * R.V0 / rho;
@@ -363,8 +384,8 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
     if (R.na > 0) pwl_eval(R.a_t, R.a_v, R.na, t, R.tsel, area, dummy);
     const double mcp = R.mass * cpm;
-    const double q1 = R.htc * area * ERG_PER_CAL;
-    fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
+    const double q1 = R.pfr ? 0.0 : R.htc * area * ERG_PER_CAL;  // plug flow: no wall heat loss on this path
+    if (!R.pfr) fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
     if (lane == 0) fl = fT;
     if (with_j) {
       const double JkT = isp ? L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;
@@ -388,6 +409,14 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     if (with_j && isp) Jsh[1 + s] = L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0);
   }
   wave_lds_sync();
+  if (R.pfr) {  // d/dx = (rho / G) d/dt (a TPRO profile is already T(x)); the Jacobian alike
+    const double sx = rho / R.G;
+    if (lane != 0 || R.energy == 1 || R.ntp == 0) fl *= sx;
+    if (with_j) {
+      for (int idx = lane; idx < ncol * LDJ; idx += WAVE) Jsh[idx] *= sx;
+      wave_lds_sync();
+    }
+  }
   SUB_PHASE(2);
 #undef SUB_PHASE
   return fl;

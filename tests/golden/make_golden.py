@@ -22,6 +22,7 @@ KEEP = {
     "adiabaticflametemperature": None,
     "equilibriumcomposition": None,
     "mixturemixing": None,
+    "plugflow": None,
 }
 
 if __name__ == "__main__":

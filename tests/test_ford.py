@@ -221,13 +221,15 @@ def test_ford_changes_ignition(fmech, forc, oracle, mech):
     assert abs(r1.tau / r0.tau - 1) > 1e-4
 
 
-def test_ford_specialised_rop_kernel_declines(fmech):
-    """The hipRTC state-per-lane kernel only expresses unit-coefficient slots: the generator
-    declines FORD mechanisms (host-only call, no GPU), which then run the generic kernel."""
+def test_ford_specialised_rop_kernel_emits_orders(fmech):
+    """Round 3: the hipRTC state-per-lane kernel covers FORD / RORD orders and non-integral
+    coefficients (round 2 declined them): the fractional orders take the conc_pow rule of the oracle
+    (jcpow_lt1: the chord below 1e-14), K_c the real coefficients (host-only call, no GPU; the GPU
+    parity is tests/test_gpu_rop_jit.py)."""
     from pychemkin_amd import _native
 
-    with pytest.raises(_native.NativeError, match="FORD"):
-        _native.rop_jit_source(fmech.to_tables())
+    src = _native.rop_jit_source(fmech.to_tables())
+    assert "jcpow_lt1(" in src and "lnPRT" in src
 
 
 # ------------------------------------------------------------------ GPU
