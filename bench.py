@@ -16,12 +16,14 @@ Secondary lines in the same JSON object (each sharded over the ranks, max-over-r
        kernel, strong scaling
   rop  configs[1]: ROP + thermo of 10M random (T, P, Y) states
   lu / rop_161sp: configs[4] components (batched MFMA LU, 161-species ROP)
+  rop_ext161  the specialised ROP kernel on the extended 161-species stand-in (PLOG, HIGH, FORD /
+       RORD, fractional and wide reactions: every reaction form since round 3)
 Each carries a roofline object (algorithmic FLOPs from the solver statistics, pychemkin_amd/perf.py,
 over the kernel time measured with HIP events on the launch stream) and, on rank 0 at N = 1, a
 CPU baseline: the oracle C restatement (OpenMP) timed on a bounded sample of the same workload on
 this host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu,rop161,ropext]
 
 Launch: under torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one
 rank.  Run directly with --gpus N > 1, bench.py is its own launcher: it starts N child processes
@@ -448,7 +450,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reactors", type=int, default=0, help="override the headline reactors per GPU (0 = full 65,536)")
     ap.add_argument("--sub-reactors", type=int, default=0, help="cap the c4 / c5 shards (0 = full sweeps)")
-    ap.add_argument("--lines", default="c3,c4,c5,rop,lu,rop161",
+    ap.add_argument("--lines", default="c3,c4,c5,rop,lu,rop161,ropext",
                     help="comma list of: c3 (headline, always run), c4, c5, rop, lu, rop161")
     ap.add_argument("--rop-states", type=int, default=10_000_000)
     ap.add_argument("--lu-systems", type=int, default=16384)
@@ -542,6 +544,16 @@ def main():
         rop_big = rop_line(dev, bm, count_ops(bm.to_tables()), args.big_states, rank, world, 0,
                            kernel_name="rop_kernel<0,3>", traffic_key="rop_161sp",
                            label=f"synthetic GRI-3.0 + tracers, KK = {bm.KK}, II = {bm.II}")
+    rop_ext = None
+    if "ropext" in lines and rank == 0 and args.big_states > 0:
+        # every reaction form on the specialised kernel: PLOG, HIGH, FORD / RORD, fractional and wide
+        # reactions (count_ops prices a PLOG / general reaction like an Arrhenius one: a lower bound)
+        em = Mechanism.from_files(os.path.join(ROOT, "data", "gri30_tracer161_ext_chem.inp"),
+                                  os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat"))
+        rop_ext = rop_line(dev, em, count_ops(em.to_tables()), args.big_states, rank, world, 0,
+                           kernel_name="rop_kernel<0,3,true>", traffic_key="rop_ext",
+                           label=f"data/gri30_tracer161_ext (PLOG, HIGH, FORD/RORD, fractional, wide), KK = {em.KK}, "
+                                 f"II = {em.II}")
 
     if rank == 0:
         line = {
@@ -573,6 +585,7 @@ def main():
             "rop": rop,
             "lu": lu,
             "rop_161sp": rop_big,
+            "rop_ext161": rop_ext,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
