@@ -396,8 +396,8 @@ class DeviceMechanism:
         max_adap > 0 with cfg.asteps > 0: adaptive solution points (t_adap, y_adap, n_adap)."""
         if not isinstance(problem, torch.Tensor):
             pv = np.asarray(problem)
-            if pv.size and not np.all((pv == 1) | (pv == 2)):
-                raise NativeError("problem must be 1 (CONP) or 2 (CONV) for every reactor")
+            if pv.size and not np.all((pv == 1) | (pv == 2) | (pv == 3)):
+                raise NativeError("problem must be 1 (CONP), 2 (CONV) or 3 (plug flow) for every reactor")
         T0 = self._dev(T0).reshape(-1)
         n = T0.numel()
         P0 = self._dev(P0).reshape(-1)

@@ -219,6 +219,10 @@ int apply_keywords(const ChemSet* s, ckmi_reactor_cfg& c, double& dtsv, bool& ad
     else if (k == "DELT" || k == "VOL" || k == "AREA" || k == "NADAP" || k == "NO_SDOUTPUT_WRITE" ||
              k == "NO_XMLOUTPUT_WRITE")
       ok = v.empty() || num(x);  // print interval, volume / area (given by SetupBatchInputs), output files
+    else if (k == "RTIME" || k == "MOMEN") {  // plug flow: residence time output; momentum equation
+      const std::string u = upper(trim(v));
+      ok = g_r.problem == 3 && (u.empty() || u == "ON" || (k == "MOMEN" && u == "OFF"));
+    } else if (k == "AREAF") ok = g_r.problem == 3 && num(x) && x > 0.0;  // the area comes with the diameter
     else if (k == "ADAP") adap = true;
     else if (k == "ASTEPS") { ok = num(x) && x >= 1.0; c.asteps = (int)x; }
     else if (k == "AVAR") {

@@ -10,4 +10,7 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest status $rc: stop"; exit $rc
 timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 --lines c3 > gpurun_out/bench_c3_r03g.json \
   2> gpurun_out/bench_c3_r03g.err
 rc2=$?; head -c 700 gpurun_out/bench_c3_r03g.json; echo; tail -3 gpurun_out/bench_c3_r03g.err
-exit $(( rc != 0 ? rc : rc2 ))
+if [ $rc2 -ne 0 ]; then exit $rc2; fi
+timeout -k 10 200 python3 scripts/c3_stats.py > gpurun_out/c3_stats_r03g.log 2>&1
+rc3=$?; tail -2 gpurun_out/c3_stats_r03g.log
+exit $(( rc != 0 ? rc : rc3 ))
