@@ -53,6 +53,7 @@ __device__ unsigned long long* g_phase_buf = nullptr;
 #endif
 
 // ---------------------------------------------------------------- reactor kernel
+template <bool PF>
 __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, double t, double yl, int lane, double& P,
                                          double& V) {
   const int KK = M.KK;
@@ -60,7 +61,7 @@ __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, dou
   const double T = bcast(yl, 0);
   const double Wb = 1.0 / wave_sum(isp ? yl * M.rwt()[lane - 1] : 0.0);
   double d;
-  if (R.pfr) {
+  if (PF && R.pfr) {
     P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, t, T, Wb, d);
     V = R.G / (P * Wb / (RU * T));  // velocity
   } else if (R.conp) {
@@ -104,11 +105,17 @@ __host__ __device__ constexpr int jscratch_bytes() {
 // over 8 waves with the FP64 inverse, MI355X, although the 168-VGPR allocation spills ~28 values
 // per step to scratch); 8 (2 per SIMD) with the FP64 inverse (256 VGPRs).
 __host__ __device__ constexpr int rwaves(bool f64) { return f64 ? 8 : 12; }
-// PL: the mechanism has PLOG / chemically activated / general reactions; F64: FP64-stored inverse
+// PL: the mechanism has PLOG / chemically activated / general reactions; F64: FP64-stored inverse.
+// Plug flow (problem 3) is compiled into the FP64-inverse variants only (PF = F64): its branches
+// cost the FP32-inverse variant, the configs[2] kernel, 12 B of scratch per lane and 0.5 % of its
+// rate.  sel: 0 integrate every reactor, 1 skip the plug-flow reactors, 2 only those (the host
+// pairs a sel 1 launch of an FP32-inverse variant with a sel 2 launch of an FP64 one).
+enum { SEL_ALL = 0, SEL_NO_PFR = 1, SEL_PFR = 2 };
 template <int N, bool PL = false, bool F64 = false>
 __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage img, const DevCfg* __restrict__ dcfg,
-                                                               int nreact, int* __restrict__ queue,
+                                                               int nreact, int sel, int* __restrict__ queue,
                                                                double* __restrict__ jws, ReactorIO io) {
+  constexpr bool PF = F64;
   const ckmi_reactor_cfg* __restrict__ cfg = &dcfg->c;
   const int oJ = img.bytes;
   const int olock = oJ + align16(8 * N * LDJ);
@@ -189,8 +196,9 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             st = ST_EXIT;
             break;
           }
-          c.r = r;
           const int prob = io.problem[r];
+          if (PF ? (sel == SEL_PFR && prob != 3) : prob == 3) break;  // the other launch's reactor
+          c.r = r;
           // TPRO runs start at the profile's initial temperature
           const double T0 = (cfg->prof_kind == 1 && cfg->energy == 2 && cfg->nprof > 0) ? cfg->prof_v[0] : io.T0[r];
           const double P0 = io.P0[r];
@@ -198,7 +206,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           if (lane == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + lane - 1];
           const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
-          R.pfr = (prob == 3);
+          R.pfr = PF && prob == 3;
           R.conp = (prob == 1 || prob == 3);
           R.energy = cfg->energy;
           R.npv = cfg->prof_kind == 0 ? cfg->nprof : 0;
@@ -767,7 +775,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           }
           if (g.mode == 1 || g.mode == 4) g.tau = ign_peak_time(g);
           double Pf, Vf;
-          state_PV(V, R, tf, yf, lane, Pf, Vf);
+          state_PV<PF>(V, R, tf, yf, lane, Pf, Vf);
           const int r = c.r;
           // a run that ended early (IGN_STOP, solver failure) has no solution after tf: its
           // remaining DTSV rows are NaN, never stale memory (the host trims them)
@@ -821,7 +829,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
 #endif
 #ifdef CKMI_PHASE_TIMERS
     unsigned long long sub[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    fe = reactor_rhs<PL>(V, R, t_e, y_e, L, oJ, lane, N, with_j, sub);
+    fe = reactor_rhs<PL, PF>(V, R, t_e, y_e, L, oJ, lane, N, with_j, sub);
     ph[with_j ? PH_JAC : PH_RHS] += __builtin_amdgcn_s_memtime() - t0;
     if (!with_j) {
       ph[5] += sub[0];
@@ -833,7 +841,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
       }
     }
 #else
-    fe = reactor_rhs<PL>(V, R, t_e, y_e, L, oJ, lane, N, with_j);
+    fe = reactor_rhs<PL, PF>(V, R, t_e, y_e, L, oJ, lane, N, with_j);
 #endif
   }
 #undef REQUEST_F
@@ -1243,7 +1251,9 @@ int stage_cfg(const DevCfg& dc, DevCfg* dst, hipStream_t stream) {
 }
 
 template <int N, bool PL = false, bool F64 = false>
-int launch_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO& io, hipStream_t stream) {
+int launch_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO& io, hipStream_t stream,
+                    int sel = SEL_ALL) {
+  if (!F64 && sel != SEL_NO_PFR) return fail(CKMI_ERR_ARG, "internal: FP32-inverse reactor launch must skip plug flow");
   constexpr int RWAVES = rwaves(F64);
   const size_t lds = reactor_lds_bytes<N, F64>(m);
   static thread_local std::map<int, int> max_lds_set;
@@ -1267,8 +1277,8 @@ int launch_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO
   int rc = stage_cfg(dc, dcfg, stream);
   if (rc == CKMI_OK) {
     HIP_CHECK(hipMemsetAsync(queue, 0, sizeof(int), stream));
-    hipLaunchKernelGGL((reactor_kernel<N, PL, F64>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, dcfg, n, queue,
-                       (double*)ws, io);
+    hipLaunchKernelGGL((reactor_kernel<N, PL, F64>), dim3(grid), dim3(RWAVES * WAVE), lds, stream, m->img, dcfg, n, sel,
+                       queue, (double*)ws, io);
     HIP_CHECK(hipGetLastError());
   }
   HIP_CHECK(hipFreeAsync(ws, stream));
@@ -1827,11 +1837,24 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   const int rpath = g_reactor_path.load();
   const bool f64 = rpath == 2 || (rpath != 3 && (cfg->rtol < 1e-9 || m->has_general));
   const hipStream_t st = (hipStream_t)stream;
+  // An FP32-inverse launch skips the plug-flow reactors and an FP64-inverse launch of the same size
+  // follows it for them (it pulls and drops the other indices: ~0.1 ms per 65,536 reactors when
+  // there are none); the problem array is device memory, so the host cannot tell in advance.
+  const int no_pf = SEL_NO_PFR;
   if (nvar > 64 || rpath == 1) rc = launch_big_reactors(m, n, dc, io, st);
-  else if (m->has_plog) rc = f64 ? launch_reactors<64, true, true>(m, n, dc, io, st) : launch_reactors<64, true>(m, n, dc, io, st);
-  else if (nvar <= 32 && !f64) rc = launch_reactors<32>(m, n, dc, io, st);
-  else if (nvar <= 54) rc = f64 ? launch_reactors<54, false, true>(m, n, dc, io, st) : launch_reactors<54>(m, n, dc, io, st);
-  else rc = f64 ? launch_reactors<64, false, true>(m, n, dc, io, st) : launch_reactors<64>(m, n, dc, io, st);
+  else if (m->has_plog) {
+    rc = f64 ? launch_reactors<64, true, true>(m, n, dc, io, st) : launch_reactors<64, true>(m, n, dc, io, st, no_pf);
+    if (!rc && !f64) rc = launch_reactors<64, true, true>(m, n, dc, io, st, SEL_PFR);
+  } else if (nvar <= 54) {
+    if (f64) rc = launch_reactors<54, false, true>(m, n, dc, io, st);
+    else {
+      rc = nvar <= 32 ? launch_reactors<32>(m, n, dc, io, st, no_pf) : launch_reactors<54>(m, n, dc, io, st, no_pf);
+      if (!rc) rc = launch_reactors<54, false, true>(m, n, dc, io, st, SEL_PFR);
+    }
+  } else {
+    rc = f64 ? launch_reactors<64, false, true>(m, n, dc, io, st) : launch_reactors<64>(m, n, dc, io, st, no_pf);
+    if (!rc && !f64) rc = launch_reactors<64, false, true>(m, n, dc, io, st, SEL_PFR);
+  }
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;

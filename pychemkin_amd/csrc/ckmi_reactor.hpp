@@ -176,7 +176,8 @@ __device__ __noinline__ void gen_jac_terms(const MechView& V, const RunCtx& R, i
 // caller holds its lock).  Same formulation as oracle/ckoracle.c reactor_rhs().  with_j is a
 // run-time (wave-uniform) flag and the Jacobian terms are a second pass over the reactions,
 // so the integrator has a single RHS call site and the register peak is that of one pass.
-template <bool PL>
+// PF: plug flow compiled in (problem 3); without it R.pfr is never read and the branches vanish
+template <bool PL, bool PF>
 __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R, double t, double yl,
                                               const WaveLds& L, int oJ, int lane, int ncol, bool with_j
 #ifdef CKMI_PHASE_TIMERS
@@ -205,8 +206,9 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const double sumYW = wave_sum(Yk * rw);
   const double Wbar = 1.0 / sumYW;
   const int conp = R.conp;
+  const bool pfr = PF && R.pfr;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
-  if (R.pfr) {
+  if (pfr) {
     double dPdx;
     P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, R.tsel, T, Wbar, dPdx);
     rho = P * Wbar / (RU * T);
@@ -384,8 +386,8 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
     if (R.na > 0) pwl_eval(R.a_t, R.a_v, R.na, t, R.tsel, area, dummy);
     const double mcp = R.mass * cpm;
-    const double q1 = R.pfr ? 0.0 : R.htc * area * ERG_PER_CAL;  // plug flow: no wall heat loss on this path
-    if (!R.pfr) fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
+    const double q1 = pfr ? 0.0 : R.htc * area * ERG_PER_CAL;  // plug flow: no wall heat loss on this path
+    if (!pfr) fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
     if (lane == 0) fl = fT;
     if (with_j) {
       const double JkT = isp ? L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;
@@ -409,7 +411,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     if (with_j && isp) Jsh[1 + s] = L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0);
   }
   wave_lds_sync();
-  if (R.pfr) {  // d/dx = (rho / G) d/dt (a TPRO profile is already T(x)); the Jacobian alike
+  if (pfr) {  // d/dx = (rho / G) d/dt (a TPRO profile is already T(x)); the Jacobian alike
     const double sx = rho / R.G;
     if (lane != 0 || R.energy == 1 || R.ntp == 0) fl *= sx;
     if (with_j) {

@@ -52,7 +52,9 @@ def test_plugflow_golden_through_kin_calls(mech):
         d = lambda v: ct.byref(ct.c_double(v))  # noqa: E731
         assert L.KINAll0D_Setup(ct.byref(cs), i(3), i(1), i(2), i(1), i(1), np.zeros(1, np.int32), i(0)) == 0
         Y0 = feed_Y(mech)
-        rho = P_IN / (8.314472e7 * T_IN) / np.sum(Y0 / mech.wt)
+        from pychemkin_amd.constants import R_GAS
+
+        rho = P_IN / (R_GAS * T_IN) / np.sum(Y0 / mech.wt)  # the engine's gas constant
         mdot = rho * np.pi * DIAM ** 2 / 4 * U_IN
         assert L.KINAll0D_SetupPFRInputs(ct.byref(cs), d(0.0), d(LENGTH), d(T_IN), d(P_IN), d(0.0), d(DIAM),
                                          np.zeros(1), np.zeros(1), d(mdot), Y0) == 0, kin.last_error()
