@@ -26,6 +26,8 @@ def main():
         for row in csv.DictReader(open(f)):
             k = row["Kernel_Name"]
             kind = ("big_reactor" if "big_reactor_kernel" in k else            # configs[4] (c5 line)
+                    # the FP64-inverse companion launch that runs (here: skips) the plug-flow reactors
+                    reactor_key + "_pfr_launch" if re.search(r"(^|[^_])reactor_kernel<\d+, (true|false), true>", k) else
                     reactor_key if re.search(r"(^|[^_])reactor_kernel", k) else  # configs[2] / [3] (c3 / c4)
                     "rop" if re.search(r"rop_kernel<0, 1[,>]", k) else        # GRI-3.0 (KK <= 63), generic
                     "rop_161sp" if re.search(r"rop_kernel<0, 3[,>]", k) else  # synthetic 161-species, generic
@@ -39,7 +41,7 @@ def main():
             acc[kind][cname].append(v)
     out = {}
     for kind, c in acc.items():
-        if kind == "reactor_c4":  # the c4 run's tiny headline dispatches are dropped: largest dispatch only
+        if kind.startswith("reactor_c4"):  # the c4 run's tiny headline dispatches are dropped: largest dispatch only
             fetch = 2.0 * 1024 * max(c["FETCH_SIZE"])
             write = 1024 * max(c["WRITE_SIZE"])
             out[kind] = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write, "dispatches": 1}
