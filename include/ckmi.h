@@ -132,7 +132,32 @@ typedef struct {
   int32_t nprof3;      /* AEXT area profile [cm2] beside a QPRO in the second slot (prof2_kind 1): the */
   double prof3_t[64];  /* heat loss is then QPRO(t) + HTC AEXT(t) (T - TAMB) (batchreactor.py:2005-2067); */
   double prof3_v[64];  /* 0 = none (<= 64) */
+  /* problem 4 (single-zone IC engine, KINAll0D_SetupHCCIInputs, engines/HCCI.py): CKMI_ENG_* parameters */
+  double eng[20];
+  /* [KK][8] device: ln-T cubics of ln eta_k [g/(cm s)] (0..3, ckmi_transport_fit) and ln lambda_k
+   * [erg/(cm s K)] (4..7, ckmi_conductivity_fit) for the engine's ICHX wall heat transfer (else NULL) */
+  const double* tran;
 } ckmi_reactor_cfg;
+
+/* engine parameter block (ckmi_reactor_cfg.eng; oracle/ckoracle.h CKO_ENG_* is the same layout) */
+#define CKMI_ENG_CA0 0      /* DEG0 crank angle at t = 0 [deg] */
+#define CKMI_ENG_RPM 1      /* RPM */
+#define CKMI_ENG_CMPR 2     /* CMPR compression ratio */
+#define CKMI_ENG_BORE 3     /* BORE [cm] */
+#define CKMI_ENG_STROKE 4   /* STRK [cm] */
+#define CKMI_ENG_LOLR 5     /* connecting rod length / crank radius */
+#define CKMI_ENG_POLEN 6    /* POLEN piston pin offset [cm] */
+#define CKMI_ENG_HTMODEL 7  /* 0 adiabatic, 1 ICHX (Nu = a Re^b Pr^c, tran required) */
+#define CKMI_ENG_HTA 8
+#define CKMI_ENG_HTB 9
+#define CKMI_ENG_HTC 10
+#define CKMI_ENG_TWALL 11   /* [K] */
+#define CKMI_ENG_C11 12     /* GVEL Woschni C11 C12 C2 swirl ratio */
+#define CKMI_ENG_C12 13
+#define CKMI_ENG_C2 14
+#define CKMI_ENG_SWIRL 15
+#define CKMI_ENG_CYBAR 16   /* cylinder-head (clearance) surface / bore area */
+#define CKMI_ENG_PSBAR 17   /* piston-head surface / bore area */
 
 /* Optional per-reactor inputs / outputs of ckmi_reactor_run_ex (any pointer may be NULL). */
 typedef struct {
@@ -230,7 +255,10 @@ int ckmi_reaction_rates(const ckmi_mech* mech, int32_t n, const double* T, const
  *                from the inviscid momentum equation P + rho u^2 = P0 + rho0 u0^2, or the PPRO
  *                profile in x; replaces KINAll0D_SetupPFRInputs + KINAll0D_Calculate,
  *                chemkin_wrapper.py / flowreactors/PFR.py:498-512.  Wall heat-loss fields are not
- *                applied to plug-flow reactors; the front ends reject them.)
+ *                applied to plug-flow reactors; the front ends reject them.),
+ *                4 single-zone IC engine (closed, V(t) from the slider-crank of cfg->eng, V0 ignored;
+ *                ICHX / Woschni wall heat transfer replaces QLOS / HTC; KK + 1 <= 64 only;
+ *                replaces KINAll0D_SetupHCCIInputs + KINAll0D_Calculate, engines/HCCI.py:1105-1239)
  *   T0, P0, V0   [n] initial temperature [K], pressure [dyn/cm2], volume [cm3]
  *   Y0           [n][KK] initial mass fractions (reactor-major)
  *   tau          [n] ignition delay [s] (-1 if not detected)
@@ -287,6 +315,12 @@ typedef struct ckmi_transport ckmi_transport;
 #define CKMI_VISC_FIT_TLOW 300.0
 #define CKMI_VISC_FIT_THIGH 3500.0
 int ckmi_transport_fit(int32_t KK, const double* wt, const double* params, double tlow, double thigh, double* fits);
+/* Thermal conductivity fits (host only; the engine's wall heat transfer, problem 4): lambda_k
+ * [erg/(cm s K)] by the Warnatz form of TRANFIT (eta_k, the self-diffusion rho D_kk / eta_k, Zrot with
+ * Parker's correction, Cv from the NASA-7 thermo [KK][17] of ckmi_mech_desc) -> fits [KK][4] of
+ * ln lambda_k as a cubic in ln T on the same grid as ckmi_transport_fit. */
+int ckmi_conductivity_fit(int32_t KK, const double* wt, const double* params, const double* thermo, double tlow,
+                          double thigh, double* fits);
 int ckmi_transport_create(const ckmi_mech* mech, const double* fits, ckmi_transport** out);
 int ckmi_transport_destroy(ckmi_transport* tr);
 int ckmi_transport_fits(const ckmi_transport* tr, double* fits);

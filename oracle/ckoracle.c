@@ -302,6 +302,7 @@ typedef struct {
   int nfe, nje;
   double tsel; /* midpoint of the current integration segment (pwl_eval) */
   double G, Pm; /* plug flow (problem 3): mass flux rho0 u0 [g/cm2-s], momentum constant P0 + G u0 */
+  double gam0;  /* engine (problem 4): cp / cv of the initial charge (motored pressure) */
 } rctx;
 
 /* piecewise-linear profile at t; the linear piece is the one containing tsel, the midpoint of
@@ -355,6 +356,80 @@ static double pfr_pressure(const rctx* c, double t, double tsel, double T, doubl
   return 0.5 * (c->Pm + sqrt(c->Pm * c->Pm - 4.0 * q));
 }
 
+/* Single-zone IC engine (problem 4: Chemkin's ICEN problem, KINAll0D_SetupHCCIInputs, engines/HCCI.py,
+ * engine.py:128-223): a closed constant-mass reactor whose volume follows the slider-crank with a
+ * piston-pin offset e = -POLEN, the crank angle measured from the offset engine's own top dead centre
+ * (theta = CA + asin(e / (L + a))), the clearance volume from the actual stroke
+ * (sqrt((L + a)^2 - e^2) - sqrt((L - a)^2 - e^2)) and the compression ratio.  This form reproduces the
+ * hcciengine golden's volume column to 1e-14 (tests/test_engine.py); with e = 0 it is the textbook
+ * V = Vc [1 + (CR - 1)/2 (R + 1 - cos theta - sqrt(R^2 - sin^2 theta))]. */
+#define CKO_PI 3.14159265358979323846
+static void engine_volume(const double* e, double t, double* V, double* dVdt) {
+  const double B = e[CKO_ENG_BORE], a = 0.5 * e[CKO_ENG_STROKE], L = e[CKO_ENG_LOLR] * a, ee = -e[CKO_ENG_POLEN];
+  const double Ab = 0.25 * CKO_PI * B * B;
+  const double st = sqrt((L + a) * (L + a) - ee * ee), sb = sqrt((L - a) * (L - a) - ee * ee);
+  const double Vc = Ab * (st - sb) / (e[CKO_ENG_CMPR] - 1.0);
+  const double omega = e[CKO_ENG_RPM] * (2.0 * CKO_PI / 60.0);            /* rad/s */
+  const double th = (e[CKO_ENG_CA0] + 6.0 * e[CKO_ENG_RPM] * t) * (CKO_PI / 180.0) + asin(ee / (L + a));
+  const double sn = sin(th), cs = cos(th);
+  const double u = a * sn - ee, r = sqrt(L * L - u * u);
+  *V = Vc + Ab * (st - (a * cs + r));
+  if (dVdt) *dVdt = Ab * (a * sn + u * a * cs / r) * omega;
+}
+static double engine_displacement(const double* e) {
+  const double B = e[CKO_ENG_BORE], a = 0.5 * e[CKO_ENG_STROKE], L = e[CKO_ENG_LOLR] * a, ee = -e[CKO_ENG_POLEN];
+  return 0.25 * CKO_PI * B * B * (sqrt((L + a) * (L + a) - ee * ee) - sqrt((L - a) * (L - a) - ee * ee));
+}
+
+/* Wall heat loss coefficient h A [erg/K-s] of the ICHX correlation Nu = h B / lambda = a Re^b Pr^c,
+ * Re = rho w B / mu, Pr = cp mu / lambda, with the Woschni gas velocity
+ * w = (C11 + C12 v_swirl / Sp) Sp + C2 Vd T_i / (P_i V_i) max(P - P_motored, 0), Sp = 2 S N the mean piston
+ * speed, v_swirl = swirl ratio x crank angular speed x B / 2, P_motored = P_i (V_i / V)^gamma_i (gamma_i of
+ * the initial charge); wall area = (CYBAR + PSBAR) A_bore + pi B (V - Vc) / A_bore (CYBAR taken as the
+ * clearance surface, the liner as swept above it).  mu: Wilke mixture of the species fits; lambda:
+ * 0.5 (sum X lambda + 1 / sum X / lambda) (cfg->tran).  The published form of Chemkin's engine heat
+ * transfer (engine.py:766-924 sets its keywords; the correlation runs in the closed library): the
+ * hcciengine golden's pressure is met only in part (tests/test_engine.py). */
+static double engine_hA(const rctx* c, double T, double P, double rho, double V, const double* Y, double cpmass) {
+  const double* e = c->cfg->eng;
+  const cko_mech* m = c->m;
+  const int KK = m->KK;
+  const double* tf = c->cfg->tran;
+  const double lnT = log(T);
+  double X[NMAX], mu[NMAX], lam[NMAX], sx = 0.0;
+  for (int k = 0; k < KK; ++k) {
+    X[k] = Y[k] / m->wt[k];
+    sx += X[k];
+    const double* f = tf + 8 * k;
+    mu[k] = exp(f[0] + lnT * (f[1] + lnT * (f[2] + lnT * f[3])));
+    lam[k] = exp(f[4] + lnT * (f[5] + lnT * (f[6] + lnT * f[7])));
+  }
+  double mum = 0.0, l1 = 0.0, l2 = 0.0;
+  for (int k = 0; k < KK; ++k) X[k] /= sx;
+  for (int k = 0; k < KK; ++k) {
+    double d = 0.0;
+    for (int j = 0; j < KK; ++j) {
+      const double q = 1.0 + sqrt(mu[k] / mu[j]) * pow(m->wt[j] / m->wt[k], 0.25);
+      d += X[j] * q * q / sqrt(8.0 * (1.0 + m->wt[k] / m->wt[j]));
+    }
+    mum += X[k] * mu[k] / d;
+    l1 += X[k] * lam[k];
+    l2 += X[k] / lam[k];
+  }
+  const double lamm = 0.5 * (l1 + 1.0 / l2);
+  const double B = e[CKO_ENG_BORE], Ab = 0.25 * CKO_PI * B * B;
+  const double Sp = 2.0 * e[CKO_ENG_STROKE] * e[CKO_ENG_RPM] / 60.0;
+  const double vsw = e[CKO_ENG_SWIRL] * e[CKO_ENG_RPM] * (2.0 * CKO_PI / 60.0) * 0.5 * B;
+  const double Vd = engine_displacement(e), Vc = Vd / (e[CKO_ENG_CMPR] - 1.0);
+  const double Pmot = c->P0 * pow(c->V0 / V, c->gam0);
+  const double w = (e[CKO_ENG_C11] + e[CKO_ENG_C12] * vsw / Sp) * Sp +
+                   e[CKO_ENG_C2] * Vd * c->T0 / (c->P0 * c->V0) * fmax(P - Pmot, 0.0);
+  const double Re = rho * w * B / mum, Pr = cpmass * mum / lamm;
+  const double h = e[CKO_ENG_HTA] * pow(Re, e[CKO_ENG_HTB]) * pow(Pr, e[CKO_ENG_HTC]) * lamm / B;
+  const double area = (e[CKO_ENG_CYBAR] + e[CKO_ENG_PSBAR]) * Ab + CKO_PI * B * (V - Vc) / Ab;
+  return h * area;
+}
+
 static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J) {
   const cko_mech* m = c->m;
   const int KK = m->KK, n = KK + 1;
@@ -366,9 +441,14 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
   double C[NMAX], cp_R[NMAX], h_RT[NMAX], s_R[NMAX], g_RT[NMAX], Ctot;
   double rho, P, V, dVdt = 0.0, dPdt = 0.0;
   const int pfr = (c->problem == 3);
+  const int eng = (c->problem == 4);
   const int conp = (c->problem == 1) || pfr;
   double Wbar = mean_wt(m, Y);
-  if (pfr) {
+  if (eng) {
+    engine_volume(c->cfg->eng, t, &V, &dVdt);
+    rho = c->mass_density0 * c->V0 / V;
+    P = rho * RU * T / Wbar;
+  } else if (pfr) {
     double dPdx;
     P = pfr_pressure(c, t, c->tsel, T, Wbar, &dPdx);
     rho = P * Wbar / (RU * T);
@@ -458,8 +538,18 @@ static void reactor_rhs(rctx* c, double t, const double* y, double* f, double* J
     const double mcp = c->mass_density0 * c->V0 * cpm;
     const double qloss = prof2_value(c->cfg, t, c->tsel, c->cfg->qloss, 1);
     const double area = prof2_value(c->cfg, t, c->tsel, c->cfg->areaq, 2);
-    const double q1 = c->cfg->htc * area * ERG_PER_CAL;
-    fT -= (qloss * ERG_PER_CAL + q1 * (T - c->cfg->tamb)) / mcp;
+    double q1 = c->cfg->htc * area * ERG_PER_CAL;
+    if (eng) { /* engine wall heat transfer replaces the QLOS / HTC terms */
+      q1 = 0.0;
+      if ((int)c->cfg->eng[CKO_ENG_HTMODEL] == 1) {
+        double cpmass = 0.0;
+        for (int k = 0; k < KK; ++k) cpmass += Y[k] * cp_R[k] * RU / m->wt[k];
+        q1 = engine_hA(c, T, P, rho, V, Y, cpmass);
+        fT -= q1 * (T - c->cfg->eng[CKO_ENG_TWALL]) / mcp;
+      }
+    } else {
+      fT -= (qloss * ERG_PER_CAL + q1 * (T - c->cfg->tamb)) / mcp;
+    }
     f[0] = fT;
     if (J) {
       for (int k = 0; k < KK; ++k) J[(1 + k) * n] = dwdT[k] * m->wt[k] * rinv + (conp ? f[1 + k] * invT : 0.0);
@@ -1075,7 +1165,14 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   const double rho0 = P0 * Wbar0 / (RU * T0);
   double Vstart = V0;
   if (cfg->problem == 2 && cfg->nprof > 0 && cfg->prof_kind == 0) Vstart = cfg->prof_v[0];
+  if (cfg->problem == 4) engine_volume(cfg->eng, 0.0, &Vstart, NULL);
   rctx ctx = {m, cfg, cfg->problem, rho0, Vstart, P0, T0, 0, 0};
+  if (cfg->problem == 4) {
+    double cp_R[NMAX], h_RT[NMAX], s_R[NMAX], cpm = 0.0;
+    cko_thermo(m, T0, cp_R, h_RT, s_R);
+    for (int k = 0; k < KK; ++k) cpm += Y0[k] * cp_R[k] / m->wt[k];
+    ctx.gam0 = cpm / (cpm - 1.0 / Wbar0);
+  }
   if ((cfg->problem == 1 || cfg->problem == 3) && cfg->nprof > 0 && cfg->prof_kind == 0) ctx.P0 = cfg->prof_v[0];
   if (cfg->problem == 3) { /* plug flow: V0 is the inlet velocity u0 [cm/s] */
     ctx.G = ctx.P0 * Wbar0 / (RU * T0) * V0;
@@ -1155,7 +1252,10 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
       dky_vec(b, t_save[isave], ys);
       for (int i = 0; i < n; ++i) y_save[(size_t)isave * n + i] = ys[i];
       double Wb = mean_wt(m, ys + 1), rho, P, V, d;
-      if (cfg->problem == 3) {
+      if (cfg->problem == 4) {
+        engine_volume(cfg->eng, t_save[isave], &V, NULL);
+        P = (rho0 * Vstart / V) * RU * ys[0] / Wb;
+      } else if (cfg->problem == 3) {
         P = pfr_pressure(&ctx, t_save[isave], t_save[isave], ys[0], Wb, &d);
         V = ctx.G / (P * Wb / (RU * ys[0])); /* velocity */
       } else if (cfg->problem == 1) {
@@ -1219,7 +1319,10 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
     res->t_end = tf;
     res->T = yf[0];
     double Wb = mean_wt(m, yf + 1), d;
-    if (cfg->problem == 3) {
+    if (cfg->problem == 4) {
+      engine_volume(cfg->eng, tf, &res->V, NULL);
+      res->P = (rho0 * Vstart / res->V) * RU * yf[0] / Wb;
+    } else if (cfg->problem == 3) {
       res->P = pfr_pressure(&ctx, tf, tf, yf[0], Wb, &d);
       res->V = ctx.G / (res->P * Wb / (RU * yf[0]));
     } else if (cfg->problem == 1) {

@@ -74,7 +74,26 @@ typedef struct {
   int nprof3;       /* AEXT [cm2] beside a QPRO second profile (prof2_kind 1), 0 = none */
   const double* prof3_t;
   const double* prof3_v;
+  const double* eng;  /* problem 4 (single-zone IC engine): CKO_ENG_N parameters, CKO_ENG_* layout */
+  const double* tran; /* [KK][8]: cubic ln-T fits of ln viscosity [g/cm-s] (0..3) and ln conductivity
+                         [erg/cm-K-s] (4..7), for the engine's wall heat transfer (NULL: none) */
 } cko_cfg;
+
+/* engine parameter block (problem 4; same layout as ckmi_reactor_cfg.eng, include/ckmi.h) */
+enum {
+  CKO_ENG_CA0 = 0,   /* DEG0 crank angle at t = 0 [deg] */
+  CKO_ENG_RPM,       /* RPM */
+  CKO_ENG_CMPR,      /* CMPR compression ratio */
+  CKO_ENG_BORE,      /* BORE [cm] */
+  CKO_ENG_STROKE,    /* STRK [cm] */
+  CKO_ENG_LOLR,      /* connecting rod length / crank radius */
+  CKO_ENG_POLEN,     /* POLEN piston pin offset [cm] */
+  CKO_ENG_HTMODEL,   /* 0 adiabatic, 1 ICHX: Nu = a Re^b Pr^c */
+  CKO_ENG_HTA, CKO_ENG_HTB, CKO_ENG_HTC, CKO_ENG_TWALL,
+  CKO_ENG_C11, CKO_ENG_C12, CKO_ENG_C2, CKO_ENG_SWIRL, /* GVEL Woschni gas velocity */
+  CKO_ENG_CYBAR, CKO_ENG_PSBAR, /* cylinder-head / piston-head area over the bore area */
+  CKO_ENG_N = 20    /* 18, 19 reserved (0) */
+};
 
 typedef struct {
   double tau;       /* ignition delay [s], -1 if not detected */

@@ -56,7 +56,7 @@ class _Cfg(ct.Structure):
         ("gfac", ct.c_double), ("qloss", ct.c_double), ("htc", ct.c_double), ("areaq", ct.c_double),
         ("tamb", ct.c_double), ("pert_rxn", ct.c_int), ("pert_fac", ct.c_double), ("nprof2", ct.c_int),
         ("prof2_kind", ct.c_int), ("prof2_t", _P), ("prof2_v", _P), ("nprof3", ct.c_int), ("prof3_t", _P),
-        ("prof3_v", _P),
+        ("prof3_v", _P), ("eng", _P), ("tran", _P),
     ]
 
 
@@ -137,7 +137,8 @@ class Oracle:
     def make_cfg(problem=1, energy=1, t_end=1.0, atol=1e-12, rtol=1e-6, h0=0.0, hmax=0.0, nneg=False,
                  ign_mode=None, ign_val=0.0, ign_species=0, ign_stop=False, max_steps=0, profile=None,
                  prof_kind=0, gfac=1.0, qloss=0.0, htc=0.0, areaq=0.0, tamb=300.0, asteps=0, pert_rxn=-1,
-                 pert_fac=1.0, profile2=None, prof2_kind=0, avar=-1, avalue=0.0, profile3=None):
+                 pert_fac=1.0, profile2=None, prof2_kind=0, avar=-1, avalue=0.0, profile3=None, engine=None,
+                 tran=None):
         """asteps / avar / avalue (adaptive output points) do not change the integration and are
         accepted for signature parity with pychemkin_amd._native.make_cfg."""
         c = _Cfg()
@@ -167,6 +168,15 @@ class Oracle:
             keep = (keep or []) + [(x, v)]
         else:
             c.nprof = 0
+        if engine is not None:  # problem 4: the CKO_ENG_* parameter block (ckoracle.h)
+            e = np.zeros(20)
+            e[:len(engine)] = np.asarray(engine, np.float64)
+            c.eng = _ptr(e)
+            keep = (keep or []) + [e]
+        if tran is not None:  # [KK][8] viscosity / conductivity fits (engine heat transfer)
+            tf = np.ascontiguousarray(tran, np.float64)
+            c.tran = _ptr(tf)
+            keep = (keep or []) + [tf]
         return c, keep
 
     def reactor(self, T0, P0, V0, Y0, t_save: Optional[np.ndarray] = None, **cfg):

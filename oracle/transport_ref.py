@@ -98,6 +98,82 @@ def mixture_viscosity(T, X, wt, fits):
     return np.sum(X * eta / den, axis=1)
 
 
+def omega11(tstar, dstar):
+    """Omega(1,1)*: Neufeld et al. (1972) Lennard-Jones correlation + 0.19 delta*^2 / T* (Brokaw)."""
+    tstar = np.asarray(tstar, dtype=np.float64)
+    lj = (1.06036 * tstar ** -0.15610 + 0.19300 * np.exp(-0.47635 * tstar) + 1.03587 * np.exp(-1.52996 * tstar)
+          + 1.76474 * np.exp(-3.89411 * tstar))
+    return lj + 0.19 * dstar * dstar / tstar
+
+
+def _parker(tstar):
+    """Parker's temperature dependence of the rotational collision number, F(T*) (Zrot(T) = Zrot(298) F(298/eps) / F(T*))."""
+    r = 1.0 / np.asarray(tstar, dtype=np.float64)
+    return 1.0 + 0.5 * np.pi ** 1.5 * r ** 0.5 + (0.25 * np.pi ** 2 + 2.0) * r + np.pi ** 1.5 * r ** 1.5
+
+
+def species_conductivity_exact(T, wt, params, cv_R):
+    """lambda_k(T) [erg/(cm s K)], the Warnatz form of the Chemkin TRANFIT species conductivity:
+    lambda = eta / W (f_tr Cv_tr + f_rot Cv_rot + f_vib Cv_vib), rho D_kk / eta from the self-diffusion
+    coefficient (Omega(1,1)*), Zrot with Parker's correction; atoms: 15/4 R eta / W.
+    T [n], cv_R [n, KK] (cv / R of each species at T) -> [n, KK]."""
+    T = np.atleast_1d(np.asarray(T, dtype=np.float64))
+    geo = np.array([p[0] for p in params])
+    eps = np.array([p[1] for p in params])
+    sig = np.array([p[2] for p in params]) * ANGSTROM
+    mu = np.array([p[3] for p in params]) * DEBYE
+    zrot = np.array([p[5] for p in params])
+    dstar = 0.5 * mu * mu / (eps * BOLTZMANN * sig ** 3)
+    W = np.asarray(wt, dtype=np.float64)
+    m = W / AVOGADRO
+    R = BOLTZMANN * AVOGADRO
+    eta = species_viscosity_exact(T, wt, params)
+    tstar = T[:, None] / eps[None, :]
+    kT = BOLTZMANN * T[:, None]
+    # rho D_kk = (3/16) sqrt(2 pi (kT)^3 / (m / 2)) / (pi sigma^2 Omega11*) * m / kT
+    rhoD = 3.0 / 16.0 * np.sqrt(2.0 * np.pi * kT ** 3 / (0.5 * m[None, :])) / (
+        np.pi * sig[None, :] ** 2 * omega11(tstar, dstar[None, :])) * m[None, :] / kT
+    x = rhoD / eta
+    cvt = 1.5
+    cvr = np.where(geo == 1, 1.0, np.where(geo == 2, 1.5, 0.0))[None, :]
+    cvv = np.asarray(cv_R) - cvt - cvr
+    Z = zrot[None, :] * _parker(298.0 / eps)[None, :] / _parker(tstar)
+    A = 2.5 - x
+    Bc = Z + 2.0 / np.pi * (5.0 / 3.0 * cvr + x)
+    ftr = 2.5 * (1.0 - 2.0 / np.pi * cvr / cvt * A / Bc)
+    frot = x * (1.0 + 2.0 / np.pi * A / Bc)
+    lam = eta / W[None, :] * R * (ftr * cvt + frot * cvr + x * cvv)
+    atom = (geo == 0)[None, :]
+    return np.where(atom, 3.75 * R * eta / W[None, :], lam)
+
+
+def cv_R_nasa(thermo, T):
+    """cv / R of every species from the [KK][17] NASA-7 table at T [n] -> [n, KK]."""
+    th = np.asarray(thermo, dtype=np.float64)
+    T = np.atleast_1d(np.asarray(T, dtype=np.float64))
+    hi = T[:, None] > th[None, :, 1]
+    a = np.where(hi[:, :, None], th[None, :, 10:17], th[None, :, 3:10])
+    Tn = T[:, None]
+    cp = a[..., 0] + Tn * (a[..., 1] + Tn * (a[..., 2] + Tn * (a[..., 3] + Tn * a[..., 4])))
+    return cp - 1.0
+
+
+def conductivity_fits(wt, params, thermo, thigh):
+    """Cubic fits of ln lambda_k in ln T: [KK, 4] (same grid as viscosity_fits)."""
+    Tf = np.linspace(FIT_TLOW, thigh, FIT_NPTS)
+    V = np.vander(np.log(Tf), FIT_ORDER, increasing=True)
+    y = np.log(species_conductivity_exact(Tf, wt, params, cv_R_nasa(thermo, Tf)))
+    coef, *_ = np.linalg.lstsq(V, y, rcond=None)
+    return coef.T.copy()
+
+
+def mixture_conductivity(T, X, fits):
+    """0.5 (sum X_k lambda_k + 1 / sum X_k / lambda_k); T [n], X [n, KK] -> [n]."""
+    X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+    lam = species_viscosity(T, fits)  # same ln-T cubic evaluation
+    return 0.5 * (np.sum(X * lam, axis=1) + 1.0 / np.sum(X / lam, axis=1))
+
+
 def mole_fractions(Y, wt):
     Y = np.atleast_2d(np.asarray(Y, dtype=np.float64))
     x = Y / np.asarray(wt)[None, :]

@@ -52,7 +52,7 @@ class ReactorCfg(ct.Structure):
         ("areaq", ct.c_double), ("tamb", ct.c_double), ("asteps", ct.c_int32), ("avar", ct.c_int32),
         ("avalue", ct.c_double), ("nprof2", ct.c_int32), ("prof2_kind", ct.c_int32), ("prof2_t", ct.c_double * 64),
         ("prof2_v", ct.c_double * 64), ("nprof3", ct.c_int32), ("prof3_t", ct.c_double * 64),
-        ("prof3_v", ct.c_double * 64),
+        ("prof3_v", ct.c_double * 64), ("eng", ct.c_double * 20), ("tran", _P),
     ]
 
 
@@ -96,6 +96,7 @@ PROTOTYPES = {
     "ckmi_parsed_symbols": (ct.c_int, [_P, _P, _P, _P, _P]),
     "ckmi_parsed_equation": (ct.c_int, [_P, ct.c_int32, ct.c_char_p, ct.c_int32, ct.POINTER(ct.c_int32)]),
     "ckmi_transport_fit": (ct.c_int, [ct.c_int32, _P, _P, ct.c_double, ct.c_double, _P]),
+    "ckmi_conductivity_fit": (ct.c_int, [ct.c_int32, _P, _P, _P, ct.c_double, ct.c_double, _P]),
     "ckmi_transport_create": (ct.c_int, [_P, _P, ct.POINTER(_P)]),
     "ckmi_transport_destroy": (ct.c_int, [_P]),
     "ckmi_transport_fits": (ct.c_int, [_P, _P]),
@@ -210,12 +211,25 @@ def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: flo
              ign_stop: bool = False, max_steps: int = 0, profile=None, prof_kind: int = 0, gfac: float = 1.0,
              qloss: float = 0.0, htc: float = 0.0, areaq: float = 0.0, tamb: float = 300.0,
              asteps: int = 0, avar: int = -1, avalue: float = 0.0, profile2=None, prof2_kind: int = 0,
-             profile3=None) -> ReactorCfg:
+             profile3=None, engine=None, tran=None) -> ReactorCfg:
     """Typed form of the reactor keywords (see include/ckmi.h ckmi_reactor_cfg).
 
     profile: (x, v) VPRO/PPRO (prof_kind 0) or TPRO (prof_kind 1); profile2: (x, v) QPRO
-    (prof2_kind 1) or AEXT (prof2_kind 2); profile3: (x, v) AEXT beside a QPRO profile2."""
+    (prof2_kind 1) or AEXT (prof2_kind 2); profile3: (x, v) AEXT beside a QPRO profile2; engine: the
+    CKMI_ENG_* parameter block of problem 4 (<= 20 values); tran: device tensor [KK][8] of viscosity and
+    conductivity fits (the engine's ICHX heat transfer), kept alive by the returned struct."""
     c = ReactorCfg()
+    if engine is not None:
+        e = np.asarray(engine, np.float64)
+        if e.size > 20:
+            raise ValueError("engine block has at most 20 values")
+        for i, v in enumerate(e):
+            c.eng[i] = float(v)
+    if tran is not None:
+        if not isinstance(tran, torch.Tensor) or tran.dtype != torch.float64 or not tran.is_cuda:
+            raise ValueError("tran must be a float64 device tensor [KK][8]")
+        c.tran = tran.data_ptr()
+        c._tran_keep = tran
     c.avar, c.avalue = int(avar), float(avalue)
     c.nprof2, c.prof2_kind = 0, int(prof2_kind)
     if profile2 is not None:
@@ -396,8 +410,8 @@ class DeviceMechanism:
         max_adap > 0 with cfg.asteps > 0: adaptive solution points (t_adap, y_adap, n_adap)."""
         if not isinstance(problem, torch.Tensor):
             pv = np.asarray(problem)
-            if pv.size and not np.all((pv == 1) | (pv == 2) | (pv == 3)):
-                raise NativeError("problem must be 1 (CONP), 2 (CONV) or 3 (plug flow) for every reactor")
+            if pv.size and not np.all((pv >= 1) & (pv <= 4)):
+                raise NativeError("problem must be 1 (CONP), 2 (CONV), 3 (plug flow) or 4 (engine) for every reactor")
         T0 = self._dev(T0).reshape(-1)
         n = T0.numel()
         P0 = self._dev(P0).reshape(-1)
@@ -468,6 +482,21 @@ def transport_fit(wt: np.ndarray, params: np.ndarray, tlow: float, thigh: float)
     fits = np.zeros((KK, 4))
     _check(lib().ckmi_transport_fit(KK, wt.ctypes.data, params.ctypes.data, float(tlow), float(thigh),
                                     fits.ctypes.data), "ckmi_transport_fit")
+    return fits
+
+
+def conductivity_fit(wt: np.ndarray, params: np.ndarray, thermo: np.ndarray, tlow: float, thigh: float) -> np.ndarray:
+    """Thermal conductivity fits [KK][4] (ln lambda_k as a cubic in ln T) from TRANLIB parameters [KK][6]
+    and the NASA-7 table [KK][17]; host only."""
+    wt = np.ascontiguousarray(wt, dtype=np.float64)
+    params = np.ascontiguousarray(params, dtype=np.float64)
+    thermo = np.ascontiguousarray(thermo, dtype=np.float64)
+    KK = wt.shape[0]
+    if params.shape != (KK, 6) or thermo.shape != (KK, 17):
+        raise NativeError(f"need params [{KK}][6] and thermo [{KK}][17], got {params.shape}, {thermo.shape}")
+    fits = np.zeros((KK, 4))
+    _check(lib().ckmi_conductivity_fit(KK, wt.ctypes.data, params.ctypes.data, thermo.ctypes.data, float(tlow),
+                                       float(thigh), fits.ctypes.data), "ckmi_conductivity_fit")
     return fits
 
 

@@ -135,6 +135,24 @@ class Chemistry:
             raise ChemistryError("no transport data processed")
         return self._vfits.copy()
 
+    @property
+    def conductivity_fits(self) -> np.ndarray:
+        """[KK][4] coefficients of ln lambda_k [erg/(cm s K)] in powers of ln T (ckmi_conductivity_fit)."""
+        if self._tran_params is None:
+            raise ChemistryError("no transport data processed")
+        if getattr(self, "_cfits", None) is None or self._cfits_version != self._version:
+            self._cfits = _transport.conductivity_fits(self._mech.wt, self._tran_params, self._mech.to_tables()["thermo"])
+            self._cfits_version = self._version
+        return self._cfits.copy()
+
+    def SpeciesCond(self, temp: float = 0.0) -> np.ndarray:
+        """Species thermal conductivities [erg/(cm s K)] at temp (chemistry.py SpeciesCond, KINGetConductivity)."""
+        if temp <= 0.0:
+            raise ChemistryError("temperature must be > 0")
+        x = np.log(float(temp))
+        c = self.conductivity_fits
+        return np.exp(c[:, 0] + x * (c[:, 1] + x * (c[:, 2] + x * c[:, 3])))
+
     def device_transport(self, device_index: int = None):
         """The viscosity tables of this chemistry set on a GPU (created on first use)."""
         if self._vfits is None:

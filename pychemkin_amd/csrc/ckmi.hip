@@ -61,7 +61,10 @@ __device__ __forceinline__ void state_PV(const MechView& M, const RunCtx& R, dou
   const double T = bcast(yl, 0);
   const double Wb = 1.0 / wave_sum(isp ? yl * M.rwt()[lane - 1] : 0.0);
   double d;
-  if (PF && R.pfr) {
+  if (PF && R.pfr == 2) {
+    engine_volume(R.cfg->eng, t, V, d);
+    P = (R.rho0 * R.V0 / V) * RU * T / Wb;
+  } else if (PF && R.pfr == 1) {
     P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, t, T, Wb, d);
     V = R.G / (P * Wb / (RU * T));  // velocity
   } else if (R.conp) {
@@ -197,7 +200,8 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             break;
           }
           const int prob = io.problem[r];
-          if (PF ? (sel == SEL_PFR && prob != 3) : prob == 3) break;  // the other launch's reactor
+          // plug flow (3) and engines (4) run in the FP64-inverse launch
+          if (PF ? (sel == SEL_PFR && prob < 3) : prob >= 3) break;  // the other launch's reactor
           c.r = r;
           // TPRO runs start at the profile's initial temperature
           const double T0 = (cfg->prof_kind == 1 && cfg->energy == 2 && cfg->nprof > 0) ? cfg->prof_v[0] : io.T0[r];
@@ -206,7 +210,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           if (lane == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + lane - 1];
           const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
-          R.pfr = PF && prob == 3;
+          R.pfr = PF ? (prob == 3 ? 1 : (prob == 4 ? 2 : 0)) : 0;
           R.conp = (prob == 1 || prob == 3);
           R.energy = cfg->energy;
           R.npv = cfg->prof_kind == 0 ? cfg->nprof : 0;
@@ -214,8 +218,18 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           R.rho0 = P0 * Wbar0 / (RU * T0);
           R.V0 = (!R.conp && R.npv > 0) ? cfg->prof_v[0] : io.V0[r];
           R.P0 = (R.conp && R.npv > 0) ? cfg->prof_v[0] : P0;
+          if constexpr (PF) {
+            if (R.pfr == 2) {  // engine: V0 from the crank position at t = 0; gamma (G), T (Pm) of the charge
+              double dv;
+              engine_volume(cfg->eng, 0.0, R.V0, dv);
+              const double cpR = isp ? nasa7_img(V, lane - 1, T0, log(T0), 1.0 / T0).cpR : 0.0;
+              const double cpm = wave_sum(isp ? yl * cpR * V.rwt()[lane - 1] : 0.0);
+              R.G = cpm / (cpm - 1.0 / Wbar0);
+              R.Pm = T0;
+            }
+          }
           R.mass = R.rho0 * R.V0;
-          if (R.pfr) {  // plug flow: V0 is the inlet velocity u0 [cm/s]
+          if (PF && R.pfr == 1) {  // plug flow: V0 is the inlet velocity u0 [cm/s]
             R.G = R.P0 * Wbar0 / (RU * T0) * R.V0;
             R.Pm = R.P0 + R.G * R.V0;
           }
@@ -1804,6 +1818,8 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   if (cfg->nprof3 > 0 && !(cfg->nprof2 > 0 && cfg->prof2_kind == 1))
     return fail(CKMI_ERR_ARG, "the third profile (AEXT) needs a QPRO second profile");
   if (cfg->avar > m->KK || cfg->avar < -1) return fail(CKMI_ERR_ARG, "avar must be -1, 0 (T) or 1 + species index");
+  if (cfg->eng[CKMI_ENG_HTMODEL] == 1.0 && !cfg->tran)
+    return fail(CKMI_ERR_ARG, "the engine's ICHX heat transfer needs the transport fits (cfg->tran)");
   if (n == 0) return CKMI_OK;
   DevCfg dc;  // this call's configuration (staged per launch: no state shared between calls)
   {
@@ -1841,7 +1857,15 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   // follows it for them (it pulls and drops the other indices: ~0.1 ms per 65,536 reactors when
   // there are none); the problem array is device memory, so the host cannot tell in advance.
   const int no_pf = SEL_NO_PFR;
-  if (nvar > 64 || rpath == 1) rc = launch_big_reactors(m, n, dc, io, st);
+  if (nvar > 64 || rpath == 1) {
+    // the workgroup kernel has no engine model: checked on the host (one synchronous copy of problem[])
+    std::vector<int32_t> hp(n);
+    HIP_CHECK(hipMemcpyAsync(hp.data(), problem, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    if (std::find(hp.begin(), hp.end(), 4) != hp.end())
+      return fail(CKMI_ERR_UNSUPPORTED, "engine reactors (problem 4) need KK + 1 <= 64 (the wave-per-reactor kernel)");
+    rc = launch_big_reactors(m, n, dc, io, st);
+  }
   else if (m->has_plog) {
     rc = f64 ? launch_reactors<64, true, true>(m, n, dc, io, st) : launch_reactors<64, true>(m, n, dc, io, st, no_pf);
     if (!rc && !f64) rc = launch_reactors<64, true, true>(m, n, dc, io, st, SEL_PFR);

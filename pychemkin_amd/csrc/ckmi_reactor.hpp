@@ -47,8 +47,10 @@ constexpr int LDJ = WAVE + 1;  // leading dimension of the shared J scratch (odd
 
 struct RunCtx {
   int conp, energy;
-  int pfr;                   // problem 3: plug flow in x [cm] (conp = 1 as well)
-  double G, Pm;              // plug flow: mass flux rho0 u0, momentum constant P0 + G u0
+  int pfr;                   // 1: problem 3, plug flow in x [cm] (conp = 1 as well); 2: problem 4,
+                             // single-zone IC engine (V(t) from cfg->eng; conp = 0)
+  double G, Pm;              // plug flow: mass flux rho0 u0, momentum constant P0 + G u0;
+                             // engine: cp / cv (G) and temperature (Pm) of the initial charge (Woschni)
   int npv;     // VPRO / PPRO profile points (0 = constant V / P)
   int ntp;     // TPRO profile points (given-temperature runs, 0 = T from the state)
   int pslot;   // device slot of the reaction whose A is perturbed (-1 none), and ln(factor)
@@ -92,6 +94,58 @@ __device__ __forceinline__ double pfr_pressure(const ckmi_reactor_cfg* c, int np
   dPdx = 0.0;
   const double q = G * G * RU * T / Wbar;
   return 0.5 * (Pm + sqrt(Pm * Pm - 4.0 * q));
+}
+// Single-zone IC engine (problem 4, oracle/ckoracle.c engine_volume): slider-crank with piston-pin
+// offset e = -POLEN, the crank angle counted from the offset engine's top dead centre, clearance
+// volume from the actual stroke and CMPR.  dVdt = dV/dt [cm3/s].
+__device__ __forceinline__ void engine_volume(const double* e, double t, double& V, double& dVdt) {
+  constexpr double PI = 3.14159265358979323846;
+  const double B = e[CKMI_ENG_BORE], a = 0.5 * e[CKMI_ENG_STROKE], L = e[CKMI_ENG_LOLR] * a, ee = -e[CKMI_ENG_POLEN];
+  const double Ab = 0.25 * PI * B * B;
+  const double st = sqrt((L + a) * (L + a) - ee * ee), sb = sqrt((L - a) * (L - a) - ee * ee);
+  const double Vc = Ab * (st - sb) / (e[CKMI_ENG_CMPR] - 1.0);
+  const double omega = e[CKMI_ENG_RPM] * (2.0 * PI / 60.0);
+  const double th = (e[CKMI_ENG_CA0] + 6.0 * e[CKMI_ENG_RPM] * t) * (PI / 180.0) + asin(ee / (L + a));
+  const double sn = sin(th), cs = cos(th);
+  const double u = a * sn - ee, r = sqrt(L * L - u * u);
+  V = Vc + Ab * (st - (a * cs + r));
+  dVdt = Ab * (a * sn + u * a * cs / r) * omega;
+}
+// Wall heat loss coefficient h A [erg/(K s)] of the ICHX correlation with the Woschni gas velocity
+// (oracle/ckoracle.c engine_hA, same arithmetic): lane 1 + k holds species k (X_k, Y_k); mu by Wilke
+// over the species fits of cfg->tran, lambda = 0.5 (sum X lambda + 1 / sum X / lambda).  Wave-uniform
+// result; the KK^2 Wilke sum broadcasts (sqrt eta_j, W_j, X_j) lane by lane.
+__device__ __forceinline__ double engine_hA(const MechView& Mv, const RunCtx& R, double T, double lnT, double P,
+                                            double rho, double V, double Xk, double cpmass, bool isp, int s) {
+  constexpr double PI = 3.14159265358979323846;
+  const double* e = R.cfg->eng;
+  const double* f = R.cfg->tran + 8 * s;
+  const int KK = Mv.KK;
+  const double muk = isp ? exp(fma(lnT, fma(lnT, fma(lnT, f[3], f[2]), f[1]), f[0])) : 1.0;
+  const double lamk = isp ? exp(fma(lnT, fma(lnT, fma(lnT, f[7], f[6]), f[5]), f[4])) : 1.0;
+  const double Wk = isp ? Mv.wt()[s] : 1.0;
+  const double sk = sqrt(muk), qk = sqrt(sqrt(Wk));
+  double den = 0.0;
+  for (int j = 0; j < KK; ++j) {
+    const double sj = bcast(sk, 1 + j), qj = bcast(qk, 1 + j), Wj = bcast(Wk, 1 + j), Xj = bcast(Xk, 1 + j);
+    const double q = 1.0 + (sk / sj) * (qj / qk);
+    den += Xj * q * q / sqrt(8.0 * (1.0 + Wk / Wj));
+  }
+  const double mum = wave_sum(isp ? Xk * muk / den : 0.0);
+  const double l1 = wave_sum(isp ? Xk * lamk : 0.0), l2 = wave_sum(isp ? Xk / lamk : 0.0);
+  const double lamm = 0.5 * (l1 + 1.0 / l2);
+  const double B = e[CKMI_ENG_BORE], Ab = 0.25 * PI * B * B;
+  const double a = 0.5 * e[CKMI_ENG_STROKE], L = e[CKMI_ENG_LOLR] * a, ee = -e[CKMI_ENG_POLEN];
+  const double Vd = Ab * (sqrt((L + a) * (L + a) - ee * ee) - sqrt((L - a) * (L - a) - ee * ee));
+  const double Vc = Vd / (e[CKMI_ENG_CMPR] - 1.0);
+  const double Sp = 2.0 * e[CKMI_ENG_STROKE] * e[CKMI_ENG_RPM] / 60.0;
+  const double vsw = e[CKMI_ENG_SWIRL] * e[CKMI_ENG_RPM] * (2.0 * PI / 60.0) * 0.5 * B;
+  const double Pmot = R.P0 * pow(R.V0 / V, R.G);  // engine: G holds gamma of the initial charge
+  const double w = (e[CKMI_ENG_C11] + e[CKMI_ENG_C12] * vsw / Sp) * Sp +
+                   e[CKMI_ENG_C2] * Vd * R.Pm / (R.P0 * R.V0) * fmax(P - Pmot, 0.0);  // Pm: T_i
+  const double Re = rho * w * B / mum, Pr = cpmass * mum / lamm;
+  const double h = e[CKMI_ENG_HTA] * pow(Re, e[CKMI_ENG_HTB]) * pow(Pr, e[CKMI_ENG_HTC]) * lamm / B;
+  return h * ((e[CKMI_ENG_CYBAR] + e[CKMI_ENG_PSBAR]) * Ab + PI * B * (V - Vc) / Ab);
 }
 // VPRO / PPRO / TPRO slot
 __device__ __forceinline__ void profile_eval(const ckmi_reactor_cfg* c, int nprof, double t, double tsel, double base,
@@ -206,9 +260,14 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   const double sumYW = wave_sum(Yk * rw);
   const double Wbar = 1.0 / sumYW;
   const int conp = R.conp;
-  const bool pfr = PF && R.pfr;
+  const bool pfr = PF && R.pfr == 1;
+  const bool eng = PF && R.pfr == 2;
   double rho, P, V_, dVdt = 0.0, dPdt = 0.0;
-  if (pfr) {
+  if (eng) {
+    engine_volume(R.cfg->eng, t, V_, dVdt);
+    rho = R.rho0 * R.V0 / V_;
+    P = rho * RU * T / Wbar;
+  } else if (pfr) {
     double dPdx;
     P = pfr_pressure(R.cfg, R.npv, R.G, R.Pm, t, R.tsel, T, Wbar, dPdx);
     rho = P * Wbar / (RU * T);
@@ -386,8 +445,17 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     if (R.nq > 0) profile2_eval(R.cfg, R.nq, t, R.tsel, qloss, dummy);
     if (R.na > 0) pwl_eval(R.a_t, R.a_v, R.na, t, R.tsel, area, dummy);
     const double mcp = R.mass * cpm;
-    const double q1 = pfr ? 0.0 : R.htc * area * ERG_PER_CAL;  // plug flow: no wall heat loss on this path
-    if (!pfr) fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
+    double q1 = pfr ? 0.0 : R.htc * area * ERG_PER_CAL;  // plug flow: no wall heat loss on this path
+    if (eng) {  // engine wall heat transfer replaces QLOS / HTC
+      q1 = 0.0;
+      if (R.cfg->eng[CKMI_ENG_HTMODEL] == 1.0) {
+        const double cpmass = wave_sum(Yk * cpk);
+        q1 = engine_hA(V, R, T, lnT, P, rho, V_, Yk * rw * Wbar, cpmass, isp, s);
+        fT -= q1 * (T - R.cfg->eng[CKMI_ENG_TWALL]) / mcp;
+      }
+    } else if (!pfr) {
+      fT -= (qloss * ERG_PER_CAL + q1 * (T - R.tamb)) / mcp;
+    }
     if (lane == 0) fl = fT;
     if (with_j) {
       const double JkT = isp ? L.dwdT()[s] * Wk * rinv + (conp ? fY * invT : 0.0) : 0.0;

@@ -167,6 +167,60 @@ int ckmi_transport_fit(int32_t KK, const double* wt, const double* params, doubl
   return CKMI_OK;
 }
 
+int ckmi_conductivity_fit(int32_t KK, const double* wt, const double* params, const double* thermo, double tlow,
+                          double thigh, double* fits) {
+  // lambda_k = eta_k / W_k (f_tr Cv_tr + f_rot Cv_rot + f_vib Cv_vib) (Warnatz; TRANFIT), rho D_kk / eta_k
+  // from the self-diffusion coefficient with Omega11* (Neufeld) + 0.19 delta*^2 / T*, Zrot(T) by Parker's
+  // F(T*), Cv_vib = Cv - Cv_tr - Cv_rot from the NASA-7 cp; atoms 15/4 R eta / W; then a cubic in ln T
+  if (KK <= 0 || !wt || !params || !thermo || !fits) return fail(CKMI_ERR_ARG, "ckmi_conductivity_fit: bad argument");
+  if (!(tlow > 0.0) || !(thigh > tlow)) return fail(CKMI_ERR_ARG, "ckmi_conductivity_fit: need 0 < tlow < thigh");
+  const double R = KB * NA;
+  auto parker = [](double ts) {
+    const double r = 1.0 / ts;
+    return 1.0 + 0.5 * std::pow(M_PI, 1.5) * std::sqrt(r) + (0.25 * M_PI * M_PI + 2.0) * r + std::pow(M_PI, 1.5) * r * std::sqrt(r);
+  };
+  for (int k = 0; k < KK; ++k) {
+    const double* p = params + 6 * k;
+    const int geo = (int)p[0];
+    const double eps = p[1], sig = p[2] * ANGSTROM, mu = p[3] * DEBYE, zrot = p[5];
+    if (!(eps > 0.0) || !(sig > 0.0) || !(wt[k] > 0.0))
+      return fail(CKMI_ERR_ARG, "ckmi_conductivity_fit: species " + std::to_string(k) + " needs eps/k > 0, sigma > 0, W > 0");
+    const double dstar = 0.5 * mu * mu / (eps * KB * sig * sig * sig);
+    const double m = wt[k] / NA;
+    const double* th = thermo + 17 * k;
+    double V[FIT_NPTS][FIT_ORDER], y[FIT_NPTS];
+    for (int i = 0; i < FIT_NPTS; ++i) {
+      const double T = tlow + (thigh - tlow) * i / (FIT_NPTS - 1);
+      const double ts = T / eps;
+      const double eta = (5.0 / 16.0) * std::sqrt(M_PI * m * KB * T) / (M_PI * sig * sig * omega22(ts, dstar));
+      double lam;
+      if (geo == 0) {
+        lam = 3.75 * R * eta / wt[k];
+      } else {
+        const double om11 = 1.06036 * std::pow(ts, -0.15610) + 0.19300 * std::exp(-0.47635 * ts) +
+                            1.03587 * std::exp(-1.52996 * ts) + 1.76474 * std::exp(-3.89411 * ts) + 0.19 * dstar * dstar / ts;
+        const double kT = KB * T;
+        const double rhoD = 3.0 / 16.0 * std::sqrt(2.0 * M_PI * kT * kT * kT / (0.5 * m)) / (M_PI * sig * sig * om11) * m / kT;
+        const double x = rhoD / eta;
+        const double* a = T > th[1] ? th + 10 : th + 3;
+        const double cv = a[0] + T * (a[1] + T * (a[2] + T * (a[3] + T * a[4]))) - 1.0;  // cv / R
+        const double cvt = 1.5, cvr = geo == 1 ? 1.0 : 1.5, cvv = cv - cvt - cvr;
+        const double Z = zrot * parker(298.0 / eps) / parker(ts);
+        const double A = 2.5 - x, Bc = Z + 2.0 / M_PI * (5.0 / 3.0 * cvr + x);
+        const double ftr = 2.5 * (1.0 - 2.0 / M_PI * cvr / cvt * A / Bc);
+        const double frot = x * (1.0 + 2.0 / M_PI * A / Bc);
+        lam = eta / wt[k] * R * (ftr * cvt + frot * cvr + x * cvv);
+      }
+      const double lx = std::log(T);
+      V[i][0] = 1.0;
+      for (int j = 1; j < FIT_ORDER; ++j) V[i][j] = V[i][j - 1] * lx;
+      y[i] = std::log(lam);
+    }
+    lsq_qr(V, y, fits + FIT_ORDER * k);
+  }
+  return CKMI_OK;
+}
+
 int ckmi_transport_create(const ckmi_mech* m, const double* fits, ckmi_transport** out) {
   if (!m || !fits || !out) return fail(CKMI_ERR_ARG, "ckmi_transport_create: null argument");
   const int KK = m->KK;

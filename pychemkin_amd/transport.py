@@ -70,3 +70,10 @@ def viscosity_fits(wt: np.ndarray, params: np.ndarray) -> np.ndarray:
     from . import _native
 
     return _native.transport_fit(wt, params, FIT_TLOW, FIT_THIGH)
+
+
+def conductivity_fits(wt: np.ndarray, params: np.ndarray, thermo: np.ndarray) -> np.ndarray:
+    """[KK][4] ln-T cubic fits of the species thermal conductivities (host C++: ckmi_conductivity_fit)."""
+    from . import _native
+
+    return _native.conductivity_fit(wt, params, thermo, FIT_TLOW, FIT_THIGH)

@@ -15,8 +15,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r"""
 import os, sys, json, numpy as np
 sys.path.insert(0, %r)
-import torch, bench
+import ctypes, torch, bench
 from pychemkin_amd import _native
+# an older library of the same reactor ABI may lack later symbols: bind only what it exports
+_L = ctypes.CDLL(_native.LIB_PATH)
+for _k in [k for k in _native.PROTOTYPES if not hasattr(_L, k)]:
+    _native.PROTOTYPES.pop(_k)
 n = %d
 mech = bench.mechanism()
 dm = _native.DeviceMechanism(mech.to_tables(), device=0)

@@ -11,6 +11,7 @@ if ROOT not in sys.path:
 
 CHEM = os.path.join(ROOT, "data", "grimech30_chem.inp")
 THERM = os.path.join(ROOT, "data", "grimech30_thermo.dat")
+TRAN = os.path.join(ROOT, "data", "grimech30_transport.dat")
 P_ATM = 1.01325e6
 
 
@@ -58,6 +59,16 @@ def chem():
     c = ck.Chemistry(label="GRI 3.0")
     c.chemfile = CHEM
     c.thermfile = THERM
+    c.preprocess()
+    return c
+
+
+@pytest.fixture(scope="session")
+def chem_tran():
+    """GRI-3.0 with its transport data (viscosity / conductivity fits)."""
+    import pychemkin_amd as ck
+
+    c = ck.Chemistry(chem=CHEM, therm=THERM, tran=TRAN, label="GRI 3.0")
     c.preprocess()
     return c
 

@@ -16,13 +16,15 @@ KEEP = {
     "CONV": None,
     "reactionrates": None,
     "simple": None,
-    "speciesproperties": ["tolerance-var", "tolerance-frac", "tolerance-ROP", "state-temperature", "state-Cv"],
+    "speciesproperties": ["tolerance-var", "tolerance-frac", "tolerance-ROP", "state-temperature", "state-Cv",
+                          "state-conductivity"],
     "createmixture": ["tolerance-var", "tolerance-frac", "tolerance-ROP", "state-temperature", "state-density"],
     "sensitivity": None,
     "adiabaticflametemperature": None,
     "equilibriumcomposition": None,
     "mixturemixing": None,
     "plugflow": None,
+    "hcciengine": None,
 }
 
 if __name__ == "__main__":

@@ -1,0 +1,220 @@
+"""Single-zone IC engine (problem 4; SURVEY.md §8(f) rank 4: HCCI reuse of the batch-reactor ODE
+kernel), CPU side: kinematics, the oracle against the reference's hcciengine golden, the conductivity
+fits behind the wall heat transfer, and the drop-in HCCIengine's host logic.
+
+Golden case (hcciengine.py:48-176): GRI-3.0, fuel CH4 / C3H8 / C2H6 = 0.9 / 0.05 / 0.05, air, phi 0.8
+with 30 % EGR (the equilibrium products of the fresh charge at 447 K, 1.065 atm, threshold 1e-8),
+447 K and 1.065 atm at IVC = -142 CA, EVO 116 CA, 1000 RPM, bore 12.065, stroke 14.005, rod 26.0093,
+CR 16.5, pin offset -0.5 cm, ICHX 0.035 / 0.71 / 0 with a 400 K wall, Woschni 2.28 / 0.308 / 3.24 / 0,
+head areas 123.5 (cylinder) and 124.75 (piston) cm2, saved every 0.5 CA, ATOL 1e-12, RTOL 1e-10, NNEG.
+"""
+import numpy as np
+import pytest
+
+from conftest import P_ATM, TRAN, golden, within
+
+T_IVC, P_IVC = 447.0, 1.065 * P_ATM
+ENG = dict(ca0=-142.0, ca1=116.0, rpm=1000.0, cr=16.5, bore=12.065, stroke=14.005, rod=26.0093, polen=-0.5,
+           ht=(0.035, 0.71, 0.0), twall=400.0, gvel=(2.28, 0.308, 3.24, 0.0), cyl=123.5, pis=124.75)
+
+
+def engine_block(ht=True):
+    ab = np.pi * ENG["bore"] ** 2 / 4
+    e = np.zeros(20)
+    e[:7] = [ENG["ca0"], ENG["rpm"], ENG["cr"], ENG["bore"], ENG["stroke"], ENG["rod"] / (ENG["stroke"] / 2),
+             ENG["polen"]]
+    if ht:
+        e[7] = 1.0
+        e[8:11] = ENG["ht"]
+        e[11] = ENG["twall"]
+        e[12:16] = ENG["gvel"]
+        e[16], e[17] = ENG["cyl"] / ab, ENG["pis"] / ab
+    return e
+
+
+def golden_times():
+    ca = np.asarray(golden("hcciengine")["state-crank_angle"])
+    return ca, (ca - ENG["ca0"]) / (6.0 * ENG["rpm"])
+
+
+def charge_Y(mech):
+    """The golden's fresh charge with EGR (hcciengine.py:63-110), mass fractions."""
+    from oracle.equilibrium import TPEquilibrium
+    from oracle.oracle import Oracle
+
+    sp = mech.species
+    KK = mech.KK
+
+    def vec(pairs):
+        x = np.zeros(KK)
+        for s, v in pairs:
+            x[sp.index(s)] = v
+        return x
+
+    fuel = vec([("CH4", 0.9), ("C3H8", 0.05), ("C2H6", 0.05)])
+    oxid = vec([("O2", 0.21), ("N2", 0.79)])
+    A = mech.ncf.astype(float)
+    el = mech.elements
+    o2 = A[el.index("C")] @ fuel + A[el.index("H")] @ fuel / 4 - A[el.index("O")] @ fuel / 2
+    alpha = o2 / oxid[sp.index("O2")]
+
+    def x_by_phi(add, thr):  # mixture.py X_by_Equivalence_Ratio (products CO2, H2O, N2)
+        add = np.where(add < thr, 0.0, add)
+        x = 0.8 * fuel + alpha * oxid
+        x /= x.sum()
+        return x * (1 - add.sum()) + add if add.sum() > 0 else x
+
+    x0 = x_by_phi(np.zeros(KK), 1e-10)
+    Y0 = x0 * mech.wt
+    Y0 /= Y0.sum()
+    eq = TPEquilibrium(mech, Oracle(mech).thermo)
+    for Tq in (2500.0, 2000.0, 1500.0, 1200.0, 1000.0, 800.0, 650.0, 550.0, 480.0, T_IVC):  # continuation
+        xe = eq.solve(Tq, P_IVC / P_ATM, Y0)
+    egr = np.where(xe > 1e-8, 0.3 * xe, 0.0)  # get_EGR_mole_fraction(0.3, threshold=1e-8)
+    x1 = x_by_phi(egr, 1e-8)
+    Y1 = x1 * mech.wt
+    return Y1 / Y1.sum()
+
+
+def tran_fits(mech):
+    from oracle import transport_ref as tr
+    P = tr.parse_transport(open(TRAN).read())
+    params = [P[s] for s in mech.species]
+    th = mech.to_tables()["thermo"]
+    return np.hstack([tr.viscosity_fits(mech.wt, params, 3500.0), tr.conductivity_fits(mech.wt, params, th, 3500.0)])
+
+
+@pytest.fixture(scope="module")
+def hcci_oracle_run(oracle, mech):
+    ca, ts = golden_times()
+    Y0 = charge_Y(mech)
+    res, _, (t, ys, ps, vs) = oracle.reactor(T_IVC, P_IVC, 1.0, Y0, t_save=ts, problem=4, energy=1, t_end=ts[-1],
+                                             atol=1e-12, rtol=1e-10, nneg=True, ign_mode="TIFP",
+                                             engine=engine_block(), tran=tran_fits(mech))
+    return res, ys, ps, vs, Y0
+
+
+def test_engine_volume_matches_golden():
+    from pychemkin_amd.engines.HCCI import engine_volume
+
+    ca, ts = golden_times()
+    V = engine_volume(engine_block(), ts)
+    assert np.max(np.abs(V / np.asarray(golden("hcciengine")["state-volume"]) - 1)) < 1e-13
+    # zero offset: the textbook slider-crank
+    e = engine_block()
+    e[6] = 0.0
+    R = ENG["rod"] / (ENG["stroke"] / 2)
+    th = np.radians(ca)
+    Vd = np.pi * ENG["bore"] ** 2 / 4 * ENG["stroke"]
+    Vtb = Vd / (ENG["cr"] - 1) * (1 + (ENG["cr"] - 1) / 2 * (R + 1 - np.cos(th) - np.sqrt(R * R - np.sin(th) ** 2)))
+    assert np.allclose(engine_volume(e, ts), Vtb, rtol=1e-13)
+
+
+def test_oracle_engine_against_golden(hcci_oracle_run, mech):
+    res, ys, ps, vs, Y0 = hcci_oracle_run
+    g = golden("hcciengine")
+    assert res.status == 0
+    assert np.max(np.abs(vs / np.asarray(g["state-volume"]) - 1)) < 1e-13
+    rho = ps / (8.31447247e7 * ys[:, 0]) / np.sum(ys[:, 1:] / mech.wt, axis=1)
+    # mass / V: the charge (fuel, air, 30 % EGR at equilibrium) and its density are the golden's
+    assert np.max(np.abs(rho / np.asarray(g["state-density"]) - 1)) < 1e-7
+    Pg = np.asarray(g["state-pressure"])
+    p = ps * 1e-6
+    ok = within(p, Pg, *g["tolerance-var"])
+    # pressure: within the golden's tolerance through the first 32 CA of compression (measured: the first
+    # 54 points), then the wall heat loss of the published ICHX / Woschni form (about 1.2x the golden's)
+    # shows: -0.3 % at -82 CA, ignition (peak pressure) 3 CA late
+    assert ok[:40].all() and ok.sum() >= 50
+    assert abs(np.argmax(p) - np.argmax(Pg)) * 0.5 <= 3.5
+    assert abs(p.max() / Pg.max() - 1) < 0.15
+    # the golden's Cp column (CPBL [kJ/mol-K]) on the same early points
+    cp_R = np.array([np.sum(ys[i, 1:] / mech.wt * _cpR(mech, ys[i, 0])) for i in range(40)])
+    cp = cp_R * 8.31447247 / np.sum(ys[:40, 1:] / mech.wt, axis=1) * 1e-3
+    assert np.all(within(cp, np.asarray(g["state-Cp"])[:40], *g["tolerance-var"]))
+
+
+def _cpR(mech, T):
+    th = mech.to_tables()["thermo"]
+    a = np.where(T > th[:, 1:2], th[:, 10:15], th[:, 3:8])
+    return a[:, 0] + T * (a[:, 1] + T * (a[:, 2] + T * (a[:, 3] + T * a[:, 4])))
+
+
+def test_oracle_engine_heat_loss_bracket(oracle, mech):
+    """The golden lies between the adiabatic cylinder and the one with wall heat transfer (compression)."""
+    ca, ts = golden_times()
+    Y0 = charge_Y(mech)
+    tq = ts[:100]
+    kw = dict(problem=4, energy=1, t_end=tq[-1], atol=1e-12, rtol=1e-10, nneg=True)
+    _, _, (_, _, pa, _) = oracle.reactor(T_IVC, P_IVC, 1.0, Y0, t_save=tq, engine=engine_block(ht=False), **kw)
+    _, _, (_, _, ph, _) = oracle.reactor(T_IVC, P_IVC, 1.0, Y0, t_save=tq, engine=engine_block(),
+                                         tran=tran_fits(mech), **kw)
+    Pg = np.asarray(golden("hcciengine")["state-pressure"])[:100] * 1e6
+    assert np.all(ph[1:] < Pg[1:]) and np.all(Pg[1:] < pa[1:])
+
+
+def test_oracle_engine_adiabatic_compression_is_isentropic(oracle, mech):
+    """Frozen chemistry (GFAC 1e-30), no wall heat: the mixture entropy stays constant along the stroke."""
+    Y0 = charge_Y(mech)
+    ts = np.linspace(0.0, 0.02, 41)  # -142 .. -22 CA
+    _, _, (_, ys, ps, _) = oracle.reactor(T_IVC, P_IVC, 1.0, Y0, t_save=ts, problem=4, energy=1, t_end=ts[-1],
+                                          atol=1e-14, rtol=1e-12, gfac=1e-30, engine=engine_block(ht=False))
+    X = Y0 / mech.wt
+    X /= X.sum()
+    nz = X > 0
+    s = []
+    for i in range(len(ts)):
+        _, _, sR = oracle.thermo(ys[i, 0])
+        s.append(np.sum(X[nz] * (sR[nz] - np.log(X[nz] * ps[i] / P_ATM))))
+    s = np.asarray(s)
+    assert np.max(np.abs(s / s[0] - 1)) < 1e-9
+    assert ys[-1, 0] > T_IVC + 300.0
+
+
+def test_conductivity_fits_native_vs_numpy_and_golden(chem_tran, mech):
+    from oracle import transport_ref as tr
+    P = tr.parse_transport(open(TRAN).read())
+    ref = tr.conductivity_fits(mech.wt, [P[s] for s in mech.species], mech.to_tables()["thermo"], 3500.0)
+    assert np.max(np.abs(chem_tran.conductivity_fits - ref)) < 1e-9
+    g = golden("speciesproperties")  # species conductivity of N2 (speciesproperties.py:106-121)
+    k = chem_tran.get_specindex("N2")
+    lam = np.array([chem_tran.SpeciesCond(T)[k] for T in g["state-temperature"]]) * 1e-7  # J/(cm s K)
+    gl = np.asarray(g["state-conductivity"])
+    # Warnatz form + Neufeld Omega(1,1)*: 2.2e-3 at most (Chemkin's tabulated collision integrals are
+    # not restated); within the golden's tolerance (1e-6 J/(cm s K) + 1e-4) on 79 of 100 points
+    assert np.max(np.abs(lam / gl - 1)) < 2.5e-3
+    assert within(lam, gl, *g["tolerance-var"]).sum() >= 79
+
+
+def test_hcci_host_setup(chem_tran):
+    import pychemkin_amd as ck
+    from pychemkin_amd.engines import HCCIengine
+    from pychemkin_amd.reactormodel import ReactorError
+
+    m = ck.Mixture(chem_tran)
+    m.temperature, m.pressure = T_IVC, P_IVC
+    m.X = [("CH4", 1.0), ("O2", 2.0), ("N2", 7.52)]
+    with pytest.raises(ReactorError, match="multi-zone"):
+        HCCIengine(m, nzones=2)
+    e = HCCIengine(reactor_condition=m, nzones=1)
+    with pytest.raises(ReactorError, match="missing"):
+        e.validate_inputs()
+    e.bore, e.stroke, e.connecting_rod_length = ENG["bore"], ENG["stroke"], ENG["rod"]
+    e.compression_ratio, e.RPM = ENG["cr"], ENG["rpm"]
+    e.set_piston_pin_offset(offset=ENG["polen"])
+    e.starting_CA, e.ending_CA = ENG["ca0"], ENG["ca1"]
+    assert e.validate_inputs() == 0
+    with pytest.raises(ReactorError, match="not on the device path"):
+        e.set_wall_heat_transfer("hohenburg", [1, 2, 3, 4, 5], 400.0)
+    e.set_wall_heat_transfer("dimensionless", list(ENG["ht"]), ENG["twall"])
+    e.set_gas_velocity_correlation(list(ENG["gvel"]))
+    e.set_piston_head_area(area=ENG["pis"])
+    e.set_cylinder_head_area(area=ENG["cyl"])
+    assert np.allclose(e.engine_block(), engine_block(), rtol=1e-15)
+    e.CAstep_for_saving_solution = 0.5
+    ca, ts = golden_times()
+    from pychemkin_amd.batchreactor import save_times
+
+    tg = save_times(e.rundurationCA / e.degpersec, 0.5 / e.degpersec)
+    assert len(tg) == len(ca) and np.allclose(e.get_CA(tg), ca, rtol=0, atol=1e-9)
+    assert abs(e.get_displacement_volume() - np.pi * ENG["bore"] ** 2 / 4 * ENG["stroke"]) < 1e-12
+    assert e.get_number_of_zones() == 1

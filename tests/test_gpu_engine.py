@@ -1,0 +1,97 @@
+"""Single-zone IC engines on the GPU (problem 4 of ckmi_reactor_run, the wave-per-reactor kernel):
+batches of cylinders against the oracle, the drop-in HCCIengine through hcciengine.py line for line
+against the golden, and the workgroup kernel's refusal."""
+import numpy as np
+import pytest
+
+from conftest import P_ATM, ch4_air_Y, golden, within
+from test_engine import ENG, P_IVC, T_IVC, charge_Y, engine_block, golden_times, tran_fits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("ht", [False, True])
+def test_engine_batch_matches_oracle(tables, oracle, mech, ht):
+    import torch
+
+    from pychemkin_amd import _native
+
+    dm = _native.DeviceMechanism(tables)
+    cases = [(447.0, 1.065, 0.8), (500.0, 1.5, 0.5), (420.0, 2.0, 1.0), (470.0, 1.0, 0.35)]
+    T0 = np.array([c[0] for c in cases])
+    P0 = np.array([c[1] for c in cases]) * P_ATM
+    Y0 = np.stack([ch4_air_Y(mech, c[2])[0] for c in cases])
+    eng = engine_block(ht=ht)
+    tf = tran_fits(mech)
+    ca, ts = golden_times()
+    ts = ts[::8]
+    run = dict(energy=1, t_end=ts[-1], atol=1e-12, rtol=1e-9, nneg=True, ign_mode="TIFP")
+    tran = torch.tensor(tf, dtype=torch.float64, device=dm.device) if ht else None
+    res = {k: v.cpu().numpy() for k, v in
+           dm.reactor_run(_native.make_cfg(engine=eng, tran=tran, **run), np.full(len(cases), 4, np.int32),
+                          T0, P0, np.ones(len(cases)), Y0, t_save=ts).items()}
+    for i in range(len(cases)):
+        r, Ye, (_, ys, ps, vs) = oracle.reactor(T0[i], P0[i], 1.0, Y0[i], t_save=ts, problem=4, engine=eng,
+                                                tran=tf if ht else None, **run)
+        assert r.status == 0 and res["stats"][i, 6] == 0
+        assert abs(res["V"][i] / r.V - 1) < 1e-13
+        assert abs(res["T"][i] / r.T - 1) < 1e-5 and abs(res["P"][i] / r.P - 1) < 1e-5
+        if r.tau > 0:
+            assert abs(res["tau"][i] / r.tau - 1) < 1e-4
+        assert np.max(np.abs(res["y_save"][i][:, 0] / ys[:, 0] - 1)) < 1e-4
+
+
+def test_hcci_golden_through_drop_in(chem_tran, mech):
+    """hcciengine.py:63-236 through the drop-in HCCIengine (the charge composed as in test_engine)."""
+    import pychemkin_amd as ck
+    from pychemkin_amd.engines.HCCI import HCCIengine
+
+    fresh = ck.Mixture(chem_tran)
+    fresh.temperature, fresh.pressure = T_IVC, P_IVC
+    fresh.Y = charge_Y(mech)
+    e = HCCIengine(reactor_condition=fresh, nzones=1)
+    e.bore, e.stroke, e.connecting_rod_length = ENG["bore"], ENG["stroke"], ENG["rod"]
+    e.compression_ratio, e.RPM = ENG["cr"], ENG["rpm"]
+    e.set_piston_pin_offset(offset=ENG["polen"])
+    e.starting_CA, e.ending_CA = ENG["ca0"], ENG["ca1"]
+    e.set_wall_heat_transfer("dimensionless", list(ENG["ht"]), ENG["twall"])
+    e.set_gas_velocity_correlation(list(ENG["gvel"]))
+    e.set_piston_head_area(area=ENG["pis"])
+    e.set_cylinder_head_area(area=ENG["cyl"])
+    e.CAstep_for_saving_solution = 0.5
+    e.CAstep_for_printing_solution = 10.0
+    e.adaptive_solution_saving(mode=False, steps=20)
+    e.tolerances = (1.0e-12, 1.0e-10)
+    e.force_nonnegative = True
+    e.set_ignition_delay(method="T_inflection")
+    assert e.run() == 0
+    delayCA = e.get_ignition_delay()
+    HR10, HR50, HR90 = e.get_engine_heat_release_CAs()
+    assert e.starting_CA < HR10 < HR50 < HR90 < e.ending_CA
+    e.process_engine_solution()
+    n = e.getnumbersolutionpoints()
+    t = e.get_solution_variable_profile("time")
+    CA = np.array([e.get_CA(x) for x in t])
+    pres = e.get_solution_variable_profile("pressure") * 1e-6
+    vol = e.get_solution_variable_profile("volume")
+    den = np.array([e.get_solution_mixture_at_index(solution_index=i).RHO for i in range(n)])
+    g = golden("hcciengine")
+    assert n == 517 and np.allclose(CA, g["state-crank_angle"], rtol=0, atol=1e-9)
+    assert np.max(np.abs(vol / np.asarray(g["state-volume"]) - 1)) < 1e-13
+    assert np.max(np.abs(den / np.asarray(g["state-density"]) - 1)) < 1e-7
+    Pg = np.asarray(g["state-pressure"])
+    ok = within(pres, Pg, *g["tolerance-var"])
+    assert ok[:40].all() and ok.sum() >= 50  # as the oracle (test_engine.py)
+    assert abs(np.argmax(pres) - np.argmax(Pg)) * 0.5 <= 3.5
+    assert abs(delayCA - CA[np.argmax(Pg)]) < 5.0
+
+
+def test_engine_refused_above_63_species(big_mech):
+    from pychemkin_amd import _native
+
+    dm = _native.DeviceMechanism(big_mech.to_tables())
+    Y0 = np.zeros((1, big_mech.KK))
+    Y0[0, big_mech.species.index("N2")] = 1.0
+    with pytest.raises(_native.NativeError, match="problem 4"):
+        dm.reactor_run(_native.make_cfg(energy=1, t_end=1e-3, engine=engine_block(ht=False)), np.array([4], np.int32),
+                       np.array([450.0]), np.array([P_ATM]), np.ones(1), Y0)

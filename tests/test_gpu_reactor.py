@@ -257,7 +257,7 @@ def test_invalid_config_fails_loudly(dm, mech):
     with pytest.raises(_native.NativeError):
         dm.reactor_run(_native.make_cfg(t_end=-1.0), np.array([1], np.int32), [1200.0], [P_ATM], [1.0], Y0)
     with pytest.raises(_native.NativeError):
-        dm.reactor_run(_native.make_cfg(t_end=1.0), np.array([4], np.int32), [1200.0], [P_ATM], [1.0], Y0)
+        dm.reactor_run(_native.make_cfg(t_end=1.0), np.array([5], np.int32), [1200.0], [P_ATM], [1.0], Y0)
 
 
 def test_hp_equilibrium_golden_on_gpu(dm, mech, tables):
