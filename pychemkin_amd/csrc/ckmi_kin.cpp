@@ -47,6 +47,7 @@ struct ChemSet {
   double* dbuf = nullptr;               // device scratch for single-state calls
   size_t dbuf_n = 0;
   ckmi_transport* tran = nullptr;       // viscosity fits (KINPreProcess with itran = 1)
+  double* dtran = nullptr;              // device [KK][8] viscosity + conductivity fits (engine heat transfer)
 };
 std::vector<ChemSet*> g_sets;  // chemistry set id = index + 1
 int g_active = 0;
@@ -64,7 +65,9 @@ struct Profile {
 // the one configured 0-D reactor (KINAll0D_*), as in the reference's native library
 struct Reactor0D {
   int chemset = 0, problem = 0, energy = 0;
-  int reactortype = 1;  // 1 batch, 3 plug flow (problem 3 of ckmi_reactor_run: x [cm] is the variable)
+  int reactortype = 1;  // 1 batch, 3 plug flow (problem 3 of ckmi_reactor_run: x [cm] is the variable),
+                        // 4 HCCI engine (problem 4: V(t) from the crank, eng below)
+  double eng[20] = {};  // engine: the CKMI_ENG_* block (KINAll0D_SetupHCCIInputs + engine keywords)
   bool setup = false, inputs = false;
   double t_end = 0, T0 = 0, P0 = 0, V0 = 0, qloss = 0;
   double x0 = 0;        // plug flow: start position [cm] (output positions are x0 + the integration variable)
@@ -175,11 +178,12 @@ int species_index(const ChemSet* s, const std::string& name) {
 // and everything else rejected with a message.
 const char* const KW_DEVICE[] = {"ATOL", "RTOL", "HO", "STPT", "NNEG", "TIFP", "DTIGN", "TLIM", "KLIM", "IGN_STOP",
                                  "DTSV", "ADAP", "ASTEPS", "AVAR", "AVALUE", "GFAC", "QLOS", "HTC", "TAMB", "AREAQ",
-                                 "MAXIT", "NSTP", "DXMX"};
+                                 "MAXIT", "NSTP", "DXMX", "POLEN", "ICHX", "GVEL", "CYBAR", "PSBAR", "DEGSAVE"};
 // RTIME (residence time output), MOMEN (the momentum equation is always on unless PPRO is given) and
 // AREAF (the flow area comes with KINAll0D_SetupPFRInputs' diameter) are the plug-flow reactor's
+// DEGPRINT (engine text-output interval) is the engine's
 const char* const KW_NOEFFECT[] = {"DELT", "VOL", "AREA", "NADAP", "NO_SDOUTPUT_WRITE", "NO_XMLOUTPUT_WRITE",
-                                   "RTIME", "MOMEN", "AREAF"};
+                                   "RTIME", "MOMEN", "AREAF", "DEGPRINT"};
 int keyword_class(const std::string& k) {
   for (const char* x : KW_DEVICE)
     if (k == x) return 1;
@@ -236,7 +240,26 @@ int apply_keywords(const ChemSet* s, ckmi_reactor_cfg& c, double& dtsv, bool& ad
     else if (k == "TAMB") ok = num(c.tamb);
     else if (k == "AREAQ") ok = num(c.areaq);
     else if (k == "MAXIT" || k == "NSTP") { ok = num(x) && x >= 1.0; c.max_steps = (int)x; }
-    else return fail(CKMI_ERR_UNSUPPORTED, "keyword " + k + " is not supported on the device path");
+    else if (k == "DEGPRINT") ok = g_r.problem == 4 && num(x) && x > 0.0;
+    else if (k == "DEGSAVE") ok = g_r.problem == 4 && num(x) && x > 0.0 && ((dtsv = x / (6.0 * g_r.eng[CKMI_ENG_RPM])), true);
+    else if (k == "POLEN") ok = g_r.problem == 4 && num(c.eng[CKMI_ENG_POLEN]);
+    else if (k == "CYBAR") ok = g_r.problem == 4 && num(c.eng[CKMI_ENG_CYBAR]) && c.eng[CKMI_ENG_CYBAR] > 0.0;
+    else if (k == "PSBAR") ok = g_r.problem == 4 && num(c.eng[CKMI_ENG_PSBAR]) && c.eng[CKMI_ENG_PSBAR] > 0.0;
+    else if (k == "ICHX" || k == "GVEL") {  // "ICHX a b c Twall" (engine.py:898-924), "GVEL C11 C12 C2 swirl"
+      std::istringstream is(v);
+      double q[4];
+      int m = 0;
+      while (m < 4 && (is >> q[m])) ++m;
+      std::string extra;
+      ok = g_r.problem == 4 && m == 4 && !(is >> extra);
+      if (ok && k == "ICHX") {
+        c.eng[CKMI_ENG_HTMODEL] = 1.0;
+        std::copy(q, q + 3, c.eng + CKMI_ENG_HTA);
+        c.eng[CKMI_ENG_TWALL] = q[3];
+      } else if (ok) {
+        std::copy(q, q + 4, c.eng + CKMI_ENG_C11);
+      }
+    } else return fail(CKMI_ERR_UNSUPPORTED, "keyword " + k + " is not supported on the device path");
     if (!ok) return fail(CKMI_ERR_ARG, "bad value for keyword " + k + ": '" + v + "'");
   }
   if (adap && c.asteps == 0 && c.avar < 0) c.asteps = 20;  // ADAP default ASTEPS (batchreactor.py:373-460)
@@ -291,6 +314,16 @@ double pwl(const std::vector<double>& x, const std::vector<double>& y, double t)
   return y[j] + (y[j + 1] - y[j]) / (x[j + 1] - x[j]) * (t - x[j]);
 }
 
+// the kernel's engine_volume (ckmi_reactor.hpp) on the host, for the output volume and pressure
+double engine_volume_host(const double* e, double t) {
+  const double B = e[CKMI_ENG_BORE], a = 0.5 * e[CKMI_ENG_STROKE], L = e[CKMI_ENG_LOLR] * a, ee = -e[CKMI_ENG_POLEN];
+  const double Ab = 0.25 * M_PI * B * B;
+  const double st = std::sqrt((L + a) * (L + a) - ee * ee), sb = std::sqrt((L - a) * (L - a) - ee * ee);
+  const double th = (e[CKMI_ENG_CA0] + 6.0 * e[CKMI_ENG_RPM] * t) * (M_PI / 180.0) + std::asin(ee / (L + a));
+  const double u = a * std::sin(th) - ee;
+  return Ab * (st - sb) / (e[CKMI_ENG_CMPR] - 1.0) + Ab * (st - (a * std::cos(th) + std::sqrt(L * L - u * u)));
+}
+
 int run_reactor(ChemSet* s) {
   const int KK = s->KK, n = KK + 1;
   ckmi_reactor_cfg c;
@@ -303,11 +336,26 @@ int run_reactor(ChemSet* s) {
   c.gfac = 1.0;
   c.avar = -1;
   c.qloss = g_r.qloss;
-  double dtsv = g_r.t_end / 100.0;  // default DTSV (batchreactor.py:296)
+  const bool engine = g_r.problem == 4;
+  if (engine) {
+    std::copy(g_r.eng, g_r.eng + 20, c.eng);
+    c.eng[CKMI_ENG_C11] = 2.28, c.eng[CKMI_ENG_C12] = 0.308, c.eng[CKMI_ENG_C2] = 3.24;  // Woschni without GVEL
+  }
+  double dtsv = g_r.t_end / 100.0;  // default DTSV (batchreactor.py:296); engines: DEGSAVE / (6 RPM)
   bool adap = false;
   int rc = apply_keywords(s, c, dtsv, adap);
   if (!rc) rc = apply_profiles(c);
   if (rc) return rc;
+  if (engine) {
+    if (c.qloss != 0.0 || c.htc != 0.0 || c.nprof > 0 || c.nprof2 > 0)
+      return fail(CKMI_ERR_UNSUPPORTED, "QLOS / HTC / profiles do not apply to an engine cylinder (use ICHX)");
+    if (c.eng[CKMI_ENG_HTMODEL] == 1.0) {
+      if (!s->dtran) return fail(CKMI_ERR_ARG, "ICHX needs transport data (KINPreProcess with itran = 1)");
+      if (!(c.eng[CKMI_ENG_CYBAR] > 0.0) || !(c.eng[CKMI_ENG_PSBAR] > 0.0))
+        return fail(CKMI_ERR_ARG, "ICHX needs the head areas (CYBAR, PSBAR)");
+      c.tran = s->dtran;
+    }
+  }
   const bool pfr = g_r.problem == 3;
   std::vector<double> ts;
   if (pfr) {
@@ -416,7 +464,10 @@ int run_reactor(ChemSet* s) {
     double sw = 0.0;
     for (int k = 0; k < KK; ++k) sw += pt.second[1 + k] / s->wt[k];
     double P, V;
-    if (pfr) {  // momentum (ckmi.h problem 3) or PPRO; V = the velocity
+    if (engine) {
+      V = engine_volume_host(c.eng, t);  // c.eng: with the POLEN keyword
+      P = (rho0 * engine_volume_host(c.eng, 0.0) / V) * RU * T * sw;
+    } else if (pfr) {  // momentum (ckmi.h problem 3) or PPRO; V = the velocity
       const double Pin = pp ? pp->y.front() : g_r.P0;
       const double G = Pin / (RU * g_r.T0 * sw0) * g_r.V0, Pm = Pin + G * g_r.V0;
       P = pp ? pwl(pp->x, pp->y, t) : 0.5 * (Pm + std::sqrt(Pm * Pm - 4.0 * G * G * RU * T * sw));
@@ -490,6 +541,7 @@ int ckmi_kin_release(int32_t chemset) {
   if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
   if (s->dbuf) (void)hipFree(s->dbuf);
   ckmi_transport_destroy(s->tran);
+  if (s->dtran) (void)hipFree(s->dtran);
   ckmi_mech_destroy(s->mech);
   delete s;
   g_sets[chemset - 1] = nullptr;
@@ -691,15 +743,22 @@ int KINAll0D_Setup(int* chemset, int* reactortype, int* problem, int* energy, in
   std::lock_guard<std::recursive_mutex> lk(g_mu);
   (void)npsr, (void)ninlets, (void)nzones;
   if (!get_set(chemset)) return fail(CKMI_ERR_ARG, "unknown chemistry set");
-  if (!reactortype || (*reactortype != 1 && *reactortype != 3))
-    return fail(CKMI_ERR_UNSUPPORTED, "only closed batch reactors (type 1) and plug-flow reactors (type 3)");
+  if (!reactortype || (*reactortype != 1 && *reactortype != 3 && *reactortype != 4))
+    return fail(CKMI_ERR_UNSUPPORTED, "only closed batch reactors (type 1), plug-flow reactors (type 3) and "
+                                      "single-zone HCCI engines (type 4)");
   if (!solver || *solver != 1) return fail(CKMI_ERR_UNSUPPORTED, "only the transient solver (1)");
-  if (!problem || (*problem != 1 && *problem != 2)) return fail(CKMI_ERR_ARG, "problem must be 1 (CONP) or 2 (CONV)");
+  if (*reactortype == 4) {  // HCCI.py:84-139: problem ICEN (3), one zone
+    if (!problem || *problem != 3) return fail(CKMI_ERR_ARG, "an HCCI engine needs problem 3 (ICEN)");
+    if (nzones && *nzones != 1) return fail(CKMI_ERR_UNSUPPORTED, "multi-zone HCCI engines are not on this path");
+  } else if (!problem || (*problem != 1 && *problem != 2)) {
+    return fail(CKMI_ERR_ARG, "problem must be 1 (CONP) or 2 (CONV)");
+  }
   if (!energy || (*energy != 1 && *energy != 2)) return fail(CKMI_ERR_ARG, "energy must be 1 (ENRG) or 2 (TGIV)");
   g_r = Reactor0D();
   g_r.chemset = *chemset;
   g_r.reactortype = *reactortype;
-  g_r.problem = *reactortype == 3 ? 3 : *problem;  // PFR.py:75 sets CONP; x is the variable (problem 3)
+  // PFR.py:75 sets CONP; x is the variable (problem 3); HCCI: ckmi_reactor_run's engine problem 4
+  g_r.problem = *reactortype == 3 ? 3 : (*reactortype == 4 ? 4 : *problem);
   g_r.energy = *energy;
   g_r.setup = true;
   return CKMI_OK;
@@ -765,6 +824,83 @@ int KINAll0D_SetupPFRInputs(int* chemset, double* x0, double* xend, double* T, d
   g_r.prof.clear();
   g_r.inputs = true;
   g_r.done = false;
+  return CKMI_OK;
+}
+
+// KINAll0D_SetupHCCIInputs (chemkin_wrapper.py:657-670, HCCI.py:1105-1125): IVC and EVO crank angles
+// [deg], RPM, compression ratio, bore and stroke [cm], rod length / crank radius, T [K] and P [dyn/cm2]
+// at IVC, heat loss (must be 0: ICHX replaces it), mass fractions.  The cylinder runs as problem 4 of
+// ckmi_reactor_run; POLEN / ICHX / GVEL / CYBAR / PSBAR / DEGSAVE come as keywords.
+int KINAll0D_SetupHCCIInputs(int* chemset, double* ivc, double* evo, double* rpm, double* cmpr, double* bore,
+                             double* stroke, double* lolr, double* T, double* P, double* qloss, double* Y) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !g_r.setup || *chemset != g_r.chemset) return fail(CKMI_ERR_ARG, "KINAll0D_Setup first");
+  if (g_r.reactortype != 4) return fail(CKMI_ERR_ARG, "KINAll0D_SetupHCCIInputs needs reactor type 4 (HCCI)");
+  if (!ivc || !evo || !rpm || !cmpr || !bore || !stroke || !lolr || !T || !P || !Y || !(*evo > *ivc) ||
+      !(*rpm > 0.0) || !(*cmpr > 1.0) || !(*bore > 0.0) || !(*stroke > 0.0) || !(*lolr > 1.0) || !(*T > 0.0) ||
+      !(*P > 0.0))
+    return fail(CKMI_ERR_ARG, "HCCI inputs: EVO > IVC, RPM, bore, stroke, T, P > 0, CMPR > 1, rod / crank > 1");
+  if (qloss && *qloss != 0.0) return fail(CKMI_ERR_UNSUPPORTED, "engine heat loss comes from ICHX, not QLOS");
+  if (s->KK + 1 > 64) return fail(CKMI_ERR_UNSUPPORTED, "engine cylinders need at most 63 species");
+  std::fill(g_r.eng, g_r.eng + 20, 0.0);
+  g_r.eng[CKMI_ENG_CA0] = *ivc;
+  g_r.eng[CKMI_ENG_RPM] = *rpm;
+  g_r.eng[CKMI_ENG_CMPR] = *cmpr;
+  g_r.eng[CKMI_ENG_BORE] = *bore;
+  g_r.eng[CKMI_ENG_STROKE] = *stroke;
+  g_r.eng[CKMI_ENG_LOLR] = *lolr;
+  g_r.t_end = (*evo - *ivc) / (6.0 * *rpm);
+  g_r.T0 = *T;
+  g_r.P0 = *P;
+  g_r.V0 = 1.0;
+  g_r.qloss = 0.0;
+  g_r.Y0.assign(Y, Y + s->KK);
+  g_r.kw.clear();
+  g_r.prof.clear();
+  g_r.inputs = true;
+  g_r.done = false;
+  return CKMI_OK;
+}
+
+// KINAll0D_GetEngineHeatRelease (chemkin_wrapper.py:769-777, engine.py:953-988): crank angles of 10 / 50
+// / 90 % of the cumulative chemical heat release of the last engine run, -sum_k h_k(298.15 K) W_k
+// (n_k(t) - n_k(0)) on its solution points (linear interpolation of the crossing).  The heat-loss and
+// apparent-heat-release rates per CA are not produced (0).
+int KINAll0D_GetEngineHeatRelease(double* qloss_ca, double* ahrr, double* ahrrp, double* hr10, double* hr50,
+                                  double* hr90) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  if (!g_r.done || g_r.problem != 4) return fail(CKMI_ERR_ARG, "no completed engine run");
+  ChemSet* s = get_set(&g_r.chemset);
+  if (!s) return fail(CKMI_ERR_ARG, "unknown chemistry set");
+  std::vector<double> cpR, hRT, sR;
+  int rc = species_thermo(s, 298.15, cpR, hRT, sR);
+  if (rc) return rc;
+  const int KK = s->KK;
+  const size_t np = g_r.t.size();
+  std::vector<double> q(np, 0.0);
+  for (size_t i = 0; i < np; ++i)
+    for (int k = 0; k < KK; ++k)
+      q[i] -= (g_r.Y[i * KK + k] - g_r.Y[k]) * hRT[k] * RU * 298.15 / s->wt[k];
+  if (qloss_ca) *qloss_ca = 0.0;
+  if (ahrr) *ahrr = 0.0;
+  if (ahrrp) *ahrrp = 0.0;
+  double* out[3] = {hr10, hr50, hr90};
+  const double lev[3] = {0.1, 0.5, 0.9};
+  const double rate = 6.0 * g_r.eng[CKMI_ENG_RPM];
+  for (int j = 0; j < 3; ++j) {
+    if (!out[j]) continue;
+    double ca = g_r.eng[CKMI_ENG_CA0];
+    if (np > 1 && q.back() > 0.0)
+      for (size_t i = 1; i < np; ++i)
+        if (q[i] / q.back() >= lev[j]) {
+          const double f0 = q[i - 1] / q.back(), f1 = q[i] / q.back();
+          const double t = g_r.t[i - 1] + (lev[j] - f0) / (f1 - f0) * (g_r.t[i] - g_r.t[i - 1]);
+          ca = g_r.eng[CKMI_ENG_CA0] + t * rate;
+          break;
+        }
+    *out[j] = ca;
+  }
   return CKMI_OK;
 }
 
@@ -1001,6 +1137,17 @@ int KINPreProcess(int* isurf, int* itran, char* chem, char* surf, char* therm, c
     std::vector<double> fits((size_t)4 * KK);
     rc = ckmi_transport_fit(KK, s->wt.data(), params.data(), CKMI_VISC_FIT_TLOW, CKMI_VISC_FIT_THIGH, fits.data());
     if (!rc) rc = ckmi_transport_create(s->mech, fits.data(), &s->tran);
+    std::vector<double> cfits((size_t)4 * KK), f8((size_t)8 * KK);
+    if (!rc) rc = ckmi_conductivity_fit(KK, s->wt.data(), params.data(), s->thermo.data(), CKMI_VISC_FIT_TLOW,
+                                        CKMI_VISC_FIT_THIGH, cfits.data());
+    if (!rc) {
+      for (int k = 0; k < KK; ++k) {
+        std::copy(fits.begin() + 4 * k, fits.begin() + 4 * k + 4, f8.begin() + 8 * k);
+        std::copy(cfits.begin() + 4 * k, cfits.begin() + 4 * k + 4, f8.begin() + 8 * k + 4);
+      }
+      rc = hip_ok(hipMalloc((void**)&s->dtran, f8.size() * sizeof(double)), "hipMalloc");
+      if (!rc) rc = hip_ok(hipMemcpy(s->dtran, f8.data(), f8.size() * sizeof(double), hipMemcpyHostToDevice), "H2D");
+    }
     if (rc) {
       const std::string msg = ckmi_last_error();
       ckmi_kin_release(cs);
@@ -1324,13 +1471,9 @@ CKMI_OUT_OF_SCOPE(KINCalculateEqGasWithOption, "the equilibrium solver", int*, i
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupPSRReactorInputs, "the PSR model", int*, int*, double*, double*, double*, double*,
                   double*, double*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupPSRInletInputs, "the PSR model", int*, int*, int*, double*, double*, double*)
-CKMI_OUT_OF_SCOPE(KINAll0D_SetupHCCIInputs, "the HCCI engine model", int*, double*, double*, double*, double*,
-                  double*, double*, double*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupHCCIZoneInputs, "the HCCI engine model", int*, int*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_SetupSIInputs, "the SI engine model", int*, double*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_GetHeatRelease, "QRGEQ heat-release output", double*, double*)
-CKMI_OUT_OF_SCOPE(KINAll0D_GetEngineHeatRelease, "engine heat release", double*, double*, double*, double*,
-                  double*, double*)
 CKMI_OUT_OF_SCOPE(KINAll0D_GetExitMassFlowRate, "open-reactor output", double*)
 CKMI_OUT_OF_SCOPE(KINPremix_SetParameter, "the premixed flame model", char*, double*)
 CKMI_OUT_OF_SCOPE(KINPremix_CalculateFlame, "the premixed flame model", int*, int*, double*, double*, double*,

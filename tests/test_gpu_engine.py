@@ -95,3 +95,56 @@ def test_engine_refused_above_63_species(big_mech):
     with pytest.raises(_native.NativeError, match="problem 4"):
         dm.reactor_run(_native.make_cfg(energy=1, t_end=1e-3, engine=engine_block(ht=False)), np.array([4], np.int32),
                        np.array([450.0]), np.array([P_ATM]), np.ones(1), Y0)
+
+
+def test_hcci_golden_through_kin_calls(mech):
+    """HCCI.py:1058-1239 through the KIN ABI alone: KINPreProcess (itran = 1) -> KINAll0D_Setup (type 4,
+    ICEN) -> KINAll0D_SetupHCCIInputs -> the engine keywords (POLEN, ICHX, GVEL, CYBAR, PSBAR, DEGSAVE)
+    -> KINAll0D_Calculate -> KINAll0D_GetGasSolnResponse / KINAll0D_GetEngineHeatRelease."""
+    import ctypes as ct
+
+    from conftest import CHEM, THERM, TRAN
+    from pychemkin_amd import kin
+
+    L = kin.bind()
+    cs = ct.c_int(0)
+    z, one = ct.c_int(0), ct.c_int(1)
+    names = [CHEM, "", THERM, TRAN, "chem.asc", "surf.asc", "tran.asc", ""]
+    assert L.KINPreProcess(ct.byref(z), ct.byref(one), *[ct.c_char_p(x.encode()) for x in names], ct.byref(cs)) == 0, \
+        kin.last_error()
+    try:
+        i = lambda v: ct.byref(ct.c_int(v))  # noqa: E731
+        d = lambda v: ct.byref(ct.c_double(v))  # noqa: E731
+        assert L.KINAll0D_Setup(ct.byref(cs), i(4), i(3), i(1), i(1), i(1), np.zeros(1, np.int32), i(1)) == 0, \
+            kin.last_error()
+        Y0 = charge_Y(mech)
+        a = ENG["stroke"] / 2
+        assert L.KINAll0D_SetupHCCIInputs(ct.byref(cs), d(ENG["ca0"]), d(ENG["ca1"]), d(ENG["rpm"]), d(ENG["cr"]),
+                                          d(ENG["bore"]), d(ENG["stroke"]), d(ENG["rod"] / a), d(T_IVC), d(P_IVC),
+                                          d(0.0), Y0) == 0, kin.last_error()
+        ab = np.pi * ENG["bore"] ** 2 / 4
+        lines = [f"POLEN    {ENG['polen']}", "ICHX    0.035    0.71    0.0    400.0", "GVEL    2.28    0.308    3.24    0.0",
+                 f"CYBAR    {ENG['cyl'] / ab}", f"PSBAR    {ENG['pis'] / ab}", "DEGSAVE    0.5", "DEGPRINT    10.0",
+                 "ATOL    1e-12", "RTOL    1e-10", "NNEG", "TIFP"]
+        for line in lines:
+            assert L.KINAll0D_SetUserKeyword(line.encode()) == 0, line
+        assert L.KINAll0D_Calculate(ct.byref(cs)) == 0, kin.last_error()
+        nr, npts = ct.c_int(0), ct.c_int(0)
+        assert L.KINAll0D_GetSolnResponseSize(ct.byref(nr), ct.byref(npts)) == 0
+        n = npts.value
+        t, T, P, V = (np.zeros(n) for _ in range(4))
+        Y = np.zeros((mech.KK, n), order="F")
+        assert L.KINAll0D_GetGasSolnResponse(ct.byref(nr), ct.byref(npts), i(mech.KK), t, T, P, V, Y) == 0
+        g = golden("hcciengine")
+        assert n == 517 and np.allclose(ENG["ca0"] + t * 6.0 * ENG["rpm"], g["state-crank_angle"], rtol=0, atol=1e-9)
+        assert np.max(np.abs(V / np.asarray(g["state-volume"]) - 1)) < 1e-13
+        rho = P / (8.31447247e7 * T) / np.sum(Y.T / mech.wt, axis=1)
+        assert np.max(np.abs(rho / np.asarray(g["state-density"]) - 1)) < 1e-7
+        ok = within(P * 1e-6, np.asarray(g["state-pressure"]), *g["tolerance-var"])
+        assert ok[:40].all() and ok.sum() >= 50
+        hr = [ct.c_double(0.0) for _ in range(6)]
+        q = np.zeros(1)
+        assert L.KINAll0D_GetEngineHeatRelease(q, *[ct.byref(x) for x in hr[1:]]) == 0
+        assert ENG["ca0"] < hr[3].value < hr[4].value < hr[5].value < ENG["ca1"]
+    finally:
+        kin.release(cs.value)
