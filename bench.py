@@ -18,12 +18,15 @@ Secondary lines in the same JSON object (each sharded over the ranks, max-over-r
   lu / rop_161sp: configs[4] components (batched MFMA LU, 161-species ROP)
   rop_ext161  the specialised ROP kernel on the extended 161-species stand-in (PLOG, HIGH, FORD /
        RORD, fractional and wide reactions: every reaction form since round 3)
+  pfr  4,096 GRI-3.0 plug-flow tubes (problem 3, 1 cm at 1 cm/s), FP64-inverse wave kernel
+  hcci 15,625 single-zone HCCI cylinders (problem 4, the hcciengine golden's engine with its
+       ICHX / Woschni wall heat transfer, -142 .. 116 CA), FP64-inverse wave kernel
 Each carries a roofline object (algorithmic FLOPs from the solver statistics, pychemkin_amd/perf.py,
 over the kernel time measured with HIP events on the launch stream) and, on rank 0 at N = 1, a
 CPU baseline: the oracle C restatement (OpenMP) timed on a bounded sample of the same workload on
 this host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu,rop161,ropext]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu,rop161,ropext,pfr,hcci]
 
 Launch: under torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one
 rank.  Run directly with --gpus N > 1, bench.py is its own launcher: it starts N child processes
@@ -380,6 +383,74 @@ def secondary_sweep(name, dm, dev, mech, ops, sweep_fn, world, rank, args, kerne
     return line
 
 
+def model_sweep(mech, world, rank, total, T_lo, T_hi, P_lo, P_hi, phi_lo, phi_hi):
+    """A fixed-total (strong-scaling) T0 x phi x P grid of `total` reactors, strided over the ranks."""
+    m = int(round(total ** (1.0 / 3.0)))
+    T = T_lo + (T_hi - T_lo) * np.arange(m) / (m - 1)
+    phi = phi_lo + (phi_hi - phi_lo) * np.arange(m) / (m - 1)
+    P = P_lo + (P_hi - P_lo) * np.arange(m) / (m - 1)
+    TT, FF, PP = (a.ravel() for a in np.meshgrid(T, phi, P, indexing="ij"))
+    sel = slice(rank, None, world)
+    return TT[sel], PP[sel], ch4_air_Y(mech, FF[sel])
+
+
+def hcci_block():
+    """The hcciengine golden's cylinder (hcciengine.py:117-157): CKMI_ENG_* block (include/ckmi.h)."""
+    ab = np.pi * 12.065 ** 2 / 4
+    e = np.zeros(20)
+    e[:7] = [-142.0, 1000.0, 16.5, 12.065, 14.005, 26.0093 / 7.0025, -0.5]
+    e[7:12] = [1.0, 0.035, 0.71, 0.0, 400.0]
+    e[12:16] = [2.28, 0.308, 3.24, 0.0]
+    e[16:18] = [123.5 / ab, 124.75 / ab]
+    return e
+
+
+def model_line(kind, dm, dev, mech, ops, world, rank, args):
+    """Plug-flow tubes (problem 3) or HCCI cylinders (problem 4) on the FP64-inverse wave kernel, one
+    timed launch of a fixed total over the ranks.  flops count the batch-reactor RHS / Jacobian / LU
+    work only (the engine's transport terms and the tube's rho / G scaling are not counted)."""
+    from pychemkin_amd import transport as trn
+
+    total = 16 ** 3 if kind == "pfr" else 16 ** 3 * 4
+    if kind == "pfr":  # configs[2]-like tubes: 1 cm at 1 cm/s inlet velocity = 1 s of residence
+        T0, P0, Y0 = model_sweep(mech, world, rank, total, 1100.0, 1700.0, P_ATM, 100 * P_ATM, 0.5, 2.0)
+        cfg = _native.make_cfg(**RUN)
+        workload = (f"plug-flow tubes: GRI-3.0 CH4/air, {total} tubes in total (16 T0 1100-1700 K x 16 phi x 16 P "
+                    "1-100 atm), 1 cm at 1 cm/s, momentum equation on, TIFP")
+    else:
+        T0, P0, Y0 = model_sweep(mech, world, rank, total, 420.0, 520.0, 1.0 * P_ATM, 2.0 * P_ATM, 0.3, 1.0)
+        text = open(os.path.join(ROOT, "data", "grimech30_transport.dat")).read()
+        params = trn.species_params(trn.parse_transport_text(text), mech.species)
+        th = mech.to_tables()["thermo"]
+        fits = np.hstack([trn.viscosity_fits(mech.wt, params), trn.conductivity_fits(mech.wt, params, th)])
+        tran = torch.tensor(fits, dtype=torch.float64, device=dev)
+        # NNEG as the reference's HCCI example sets it (hcciengine.py:173): without it 3-4 of the 15,625
+        # cylinders stall in the expansion stroke on the GPU (DESIGN.md §4)
+        run = dict(RUN, t_end=258.0 / 6000.0, nneg=True)
+        cfg = _native.make_cfg(engine=hcci_block(), tran=tran, **run)
+        workload = (f"HCCI cylinders: GRI-3.0 CH4/air, {round(total ** (1 / 3)) ** 3} in total (T_IVC 420-520 K x "
+                    "phi 0.3-1 x P_IVC 1-2 atm), the hcciengine golden's engine, ICHX/Woschni wall heat, -142..116 CA, NNEG")
+    code = 3 if kind == "pfr" else 4
+    sh = Shard(dm, dev, T0, P0, Y0, np.full(len(T0), code, np.int32))
+    sh.step(cfg, 0, min(sh.n, 256))
+    tmax, kern_ms, res = timed(world, lambda: sh.step(cfg), 1)
+    stats = res["stats"].cpu().numpy()
+    tau = res["tau"].cpu().numpy()
+    tot = torch.tensor([sh.n], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot)
+    tot = int(tot.item())
+    unit = "tubes/s" if kind == "pfr" else "cylinders/s"
+    del sh, res
+    return {"metric": f"{'plug-flow reactor' if kind == 'pfr' else 'engine cycle'} integrations/sec ({workload})",
+            "value": tot / tmax, "unit": unit, "total": tot, "per_gpu": len(T0), "seconds": tmax, "scaling": "strong",
+            "failed": int((stats[:, 6] != 0).sum()), "not_ignited": int((tau <= 0).sum()),
+            "solver": solver_summary(stats),
+            "roofline": reactor_roofline(ops, stats, float(np.mean(kern_ms)) / 1e3, "reactor_kernel<54, false, true>",
+                                         None, len(T0)),
+            "cpu_baseline": None}
+
+
 def _free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
         so.bind(("127.0.0.1", 0))
@@ -450,8 +521,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reactors", type=int, default=0, help="override the headline reactors per GPU (0 = full 65,536)")
     ap.add_argument("--sub-reactors", type=int, default=0, help="cap the c4 / c5 shards (0 = full sweeps)")
-    ap.add_argument("--lines", default="c3,c4,c5,rop,lu,rop161,ropext",
-                    help="comma list of: c3 (headline, always run), c4, c5, rop, lu, rop161")
+    ap.add_argument("--lines", default="c3,c4,c5,rop,lu,rop161,ropext,pfr,hcci",
+                    help="comma list of: c3 (headline, always run), c4, c5, rop, lu, rop161, ropext, pfr, hcci")
     ap.add_argument("--rop-states", type=int, default=10_000_000)
     ap.add_argument("--lu-systems", type=int, default=16384)
     ap.add_argument("--big-states", type=int, default=1_000_000)
@@ -555,6 +626,9 @@ def main():
                            label=f"data/gri30_tracer161_ext (PLOG, HIGH, FORD/RORD, fractional, wide), KK = {em.KK}, "
                                  f"II = {em.II}")
 
+    pfr = model_line("pfr", dm, dev, mech, ops, world, rank, args) if "pfr" in lines else None
+    hcci = model_line("hcci", dm, dev, mech, ops, world, rank, args) if "hcci" in lines else None
+
     if rank == 0:
         line = {
             "metric": "reactor integrations/sec (GRI-3.0 const-P ignition)",
@@ -586,6 +660,8 @@ def main():
             "lu": lu,
             "rop_161sp": rop_big,
             "rop_ext161": rop_ext,
+            "pfr": pfr,
+            "hcci": hcci,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -387,7 +387,8 @@ static double engine_displacement(const double* e) {
  * speed, v_swirl = swirl ratio x crank angular speed x B / 2, P_motored = P_i (V_i / V)^gamma_i (gamma_i of
  * the initial charge); wall area = (CYBAR + PSBAR) A_bore + pi B (V - Vc) / A_bore (CYBAR taken as the
  * clearance surface, the liner as swept above it).  mu: Wilke mixture of the species fits; lambda:
- * 0.5 (sum X lambda + 1 / sum X / lambda) (cfg->tran).  The published form of Chemkin's engine heat
+ * 0.5 (sum X lambda + 1 / sum X / lambda) (cfg->tran), both of the mole fractions of max(Y, 0): negative
+ * mass fractions inside the tolerance (runs without NNEG) must not enter the transport sums.  The published form of Chemkin's engine heat
  * transfer (engine.py:766-924 sets its keywords; the correlation runs in the closed library): the
  * hcciengine golden's pressure is met only in part (tests/test_engine.py). */
 static double engine_hA(const rctx* c, double T, double P, double rho, double V, const double* Y, double cpmass) {
@@ -398,7 +399,7 @@ static double engine_hA(const rctx* c, double T, double P, double rho, double V,
   const double lnT = log(T);
   double X[NMAX], mu[NMAX], lam[NMAX], sx = 0.0;
   for (int k = 0; k < KK; ++k) {
-    X[k] = Y[k] / m->wt[k];
+    X[k] = fmax(Y[k], 0.0) / m->wt[k];  /* transport of the non-negative part of the composition */
     sx += X[k];
     const double* f = tf + 8 * k;
     mu[k] = exp(f[0] + lnT * (f[1] + lnT * (f[2] + lnT * f[3])));

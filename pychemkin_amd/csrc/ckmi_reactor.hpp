@@ -450,7 +450,9 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       q1 = 0.0;
       if (R.cfg->eng[CKMI_ENG_HTMODEL] == 1.0) {
         const double cpmass = wave_sum(Yk * cpk);
-        q1 = engine_hA(V, R, T, lnT, P, rho, V_, Yk * rw * Wbar, cpmass, isp, s);
+        // transport of the non-negative part of the composition (oracle engine_hA)
+        const double xp = fmax(Yk, 0.0) * rw;
+        q1 = engine_hA(V, R, T, lnT, P, rho, V_, xp / wave_sum(xp), cpmass, isp, s);
         fT -= q1 * (T - R.cfg->eng[CKMI_ENG_TWALL]) / mcp;
       }
     } else if (!pfr) {
