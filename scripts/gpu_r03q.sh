@@ -3,6 +3,9 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_engine.py -q --timeout 250 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu_engine_r03q.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_gpu_engine_r03q.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python3 scripts/hcci_diag.py --nneg > gpurun_out/hcci_diag_c.json 2> gpurun_out/hcci_diag_c.err
 rc=$?; cut -c1-300 gpurun_out/hcci_diag_c.json
 if [ $rc -ne 0 ]; then exit $rc; fi
