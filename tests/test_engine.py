@@ -218,3 +218,15 @@ def test_hcci_host_setup(chem_tran):
     assert len(tg) == len(ca) and np.allclose(e.get_CA(tg), ca, rtol=0, atol=1e-9)
     assert abs(e.get_displacement_volume() - np.pi * ENG["bore"] ** 2 / 4 * ENG["stroke"]) < 1e-12
     assert e.get_number_of_zones() == 1
+
+
+def test_engine_keywords_in_the_one_keyword_policy():
+    """The KIN path's engine keywords (HCCI.py / engine.py write them) are device keywords; DEGPRINT has no
+    effect; the multi-zone / other correlations stay rejected."""
+    from pychemkin_amd import kin
+
+    for k in ("POLEN", "ICHX", "GVEL", "CYBAR", "PSBAR", "DEGSAVE"):
+        assert kin.keyword_class(k) == 1, k
+    assert kin.keyword_class("DEGPRINT") == 2
+    for k in ("ICHW", "ICHH", "HIMP", "MLMT"):
+        assert kin.keyword_class(k) == 0, k
