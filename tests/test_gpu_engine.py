@@ -153,8 +153,8 @@ def test_hcci_golden_through_kin_calls(mech):
 def test_cold_lean_cylinders_with_nneg(tables, oracle, mech):
     """Non-igniting cold / lean cylinders of the bench sweep (T_IVC 420-437 K), ICHX heat transfer, with NNEG
     as the reference's HCCI example sets it: every one completes and ends at the oracle's state.  (Without
-    NNEG, at the bench's rtol 1e-8 / atol 1e-10, 3-4 of 15,625 such cylinders stall in the expansion
-    stroke on the GPU while the oracle completes them: an open issue)"""
+    NNEG, at the bench's rtol 1e-8 / atol 1e-10, 3-4 of 15,625 such cylinders run away through negative
+    trace concentrations in the expansion stroke -- the oracle too at slightly different rtol)"""
     import torch
 
     import bench
