@@ -37,6 +37,10 @@
 extern "C" {
 #endif
 
+/* ABI version returned by ckmi_version(): bumped whenever a struct layout or a table stride changes.
+ * 1: round-1/2 layout (CKMI_SLOTS 4, ckmi_reactor_cfg up to prof3_v); 2: CKMI_SLOTS 8, cfg.eng[20], cfg.tran. */
+#define CKMI_ABI_VERSION 2
+
 #define CKMI_SLOTS 8 /* distinct species per reaction side in the flat tables ([II][CKMI_SLOTS] arrays) */
 
 /* reaction types */
@@ -322,6 +326,16 @@ int ckmi_transport_fit(int32_t KK, const double* wt, const double* params, doubl
 int ckmi_conductivity_fit(int32_t KK, const double* wt, const double* params, const double* thermo, double tlow,
                           double thigh, double* fits);
 int ckmi_transport_create(const ckmi_mech* mech, const double* fits, ckmi_transport** out);
+/* Thermal conductivity: replaces KINGetConductivity (chemkin_wrapper.py:413-418, mixture.py:1885-1909,
+ * chemistry.py:1361-1396) and KINGetMixtureConductivity (:449-455, mixture.py:1979-2013).
+ *   ckmi_transport_set_conductivity  uploads ckmi_conductivity_fit's [KK][4] fits beside the viscosity tables
+ *   ckmi_species_conductivity        T [n] -> lambda [KK][n] erg/(cm s K)                  (device pointers)
+ *   ckmi_mixture_conductivity        T [n], Y [KK][n] mass fractions -> lambda [n], mixture-averaged
+ *                                    (sum X lambda + 1 / sum X / lambda) / 2                 (device pointers) */
+int ckmi_transport_set_conductivity(ckmi_transport* tr, const double* cfits);
+int ckmi_species_conductivity(const ckmi_transport* tr, int32_t n, const double* T, double* cond, void* stream);
+int ckmi_mixture_conductivity(const ckmi_transport* tr, int32_t n, const double* T, const double* Y, double* cond,
+                              void* stream);
 int ckmi_transport_destroy(ckmi_transport* tr);
 int ckmi_transport_fits(const ckmi_transport* tr, double* fits);
 int ckmi_species_viscosity(const ckmi_transport* tr, int32_t n, const double* T, double* visc, void* stream);

@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # _lib/libckmi_prof.so, used by scripts/phase_profile.py); it is never a CPU path.
 LIB_PATH = os.environ.get("CKMI_LIB") or os.path.join(_HERE, "_lib", "libckmi.so")
 
-SLOTS = 4
+ABI_VERSION = 2  # CKMI_ABI_VERSION (include/ckmi.h): the layouts of MechDesc / ReactorCfg below
 NSTAT = 8
 STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "nni")
 RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures"}
@@ -102,6 +102,9 @@ PROTOTYPES = {
     "ckmi_transport_fits": (ct.c_int, [_P, _P]),
     "ckmi_species_viscosity": (ct.c_int, [_P, ct.c_int32, _P, _P, _P]),
     "ckmi_mixture_viscosity": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P]),
+    "ckmi_transport_set_conductivity": (ct.c_int, [_P, _P]),
+    "ckmi_species_conductivity": (ct.c_int, [_P, ct.c_int32, _P, _P, _P]),
+    "ckmi_mixture_conductivity": (ct.c_int, [_P, ct.c_int32, _P, _P, _P, _P]),
 }
 LU_NMAX = 192
 
@@ -117,6 +120,9 @@ def lib() -> ct.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        if L.ckmi_version() != ABI_VERSION:
+            raise NativeError(f"{LIB_PATH} has ABI version {L.ckmi_version()}, this binding needs {ABI_VERSION}; "
+                              "rebuild with __graft_entry__.build()")
         _lib = L
     return _lib
 
@@ -501,9 +507,10 @@ def conductivity_fit(wt: np.ndarray, params: np.ndarray, thermo: np.ndarray, tlo
 
 
 class DeviceTransport:
-    """Viscosity fits and Wilke tables of one DeviceMechanism, on its GPU (wraps ckmi_transport)."""
+    """Viscosity (and optionally conductivity) fits and Wilke tables of one DeviceMechanism, on its GPU
+    (wraps ckmi_transport)."""
 
-    def __init__(self, dm: "DeviceMechanism", fits: np.ndarray):
+    def __init__(self, dm: "DeviceMechanism", fits: np.ndarray, cond_fits: Optional[np.ndarray] = None):
         self.dm = dm
         self.KK = dm.KK
         fits = np.ascontiguousarray(fits, dtype=np.float64)
@@ -513,6 +520,14 @@ class DeviceTransport:
         with torch.cuda.device(dm.device):
             _check(lib().ckmi_transport_create(dm.handle, fits.ctypes.data, ct.byref(h)), "ckmi_transport_create")
         self._h = h
+        self.has_conductivity = False
+        if cond_fits is not None:
+            cf = np.ascontiguousarray(cond_fits, dtype=np.float64)
+            if cf.shape != (self.KK, 4):
+                raise NativeError(f"conductivity fits must be [{self.KK}][4], got {cf.shape}")
+            with torch.cuda.device(dm.device):
+                _check(lib().ckmi_transport_set_conductivity(self._h, cf.ctypes.data), "ckmi_transport_set_conductivity")
+            self.has_conductivity = True
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -549,6 +564,27 @@ class DeviceTransport:
         with torch.cuda.device(self.dm.device):
             _check(lib().ckmi_mixture_viscosity(self._h, n, _ptr(T), _ptr(Y), _ptr(out), _stream_ptr(self.dm.device)),
                    "ckmi_mixture_viscosity")
+        return out
+
+    def species_conductivity(self, T) -> torch.Tensor:
+        """T[n] -> lambda[KK][n] [erg/(cm s K)] (device tensor; KINGetConductivity x n)."""
+        T = self.dm._dev(T).reshape(-1)
+        n = T.numel()
+        out = torch.empty((self.KK, n), dtype=torch.float64, device=self.dm.device)
+        with torch.cuda.device(self.dm.device):
+            _check(lib().ckmi_species_conductivity(self._h, n, _ptr(T), _ptr(out), _stream_ptr(self.dm.device)),
+                   "ckmi_species_conductivity")
+        return out
+
+    def mixture_conductivity(self, T, Y_soa) -> torch.Tensor:
+        """T[n], Y[KK][n] mass fractions -> lambda[n] [erg/(cm s K)] (mixture-averaged; device tensor)."""
+        T = self.dm._dev(T).reshape(-1)
+        n = T.numel()
+        Y = self.dm._dev(Y_soa).reshape(self.KK, n)
+        out = torch.empty(n, dtype=torch.float64, device=self.dm.device)
+        with torch.cuda.device(self.dm.device):
+            _check(lib().ckmi_mixture_conductivity(self._h, n, _ptr(T), _ptr(Y), _ptr(out),
+                                                   _stream_ptr(self.dm.device)), "ckmi_mixture_conductivity")
         return out
 
 

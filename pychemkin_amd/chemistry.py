@@ -146,12 +146,25 @@ class Chemistry:
         return self._cfits.copy()
 
     def SpeciesCond(self, temp: float = 0.0) -> np.ndarray:
-        """Species thermal conductivities [erg/(cm s K)] at temp (chemistry.py SpeciesCond, KINGetConductivity)."""
+        """Species thermal conductivities [erg/(cm s K)] at temp, on the GPU (chemistry.py:1361-1396,
+        KINGetConductivity -> ckmi_species_conductivity)."""
+        import torch
+
         if temp <= 0.0:
             raise ChemistryError("temperature must be > 0")
-        x = np.log(float(temp))
-        c = self.conductivity_fits
-        return np.exp(c[:, 0] + x * (c[:, 1] + x * (c[:, 2] + x * c[:, 3])))
+        dt = self.device_transport()
+        T = torch.tensor([float(temp)], dtype=torch.float64, device=dt.dm.device)
+        return dt.species_conductivity(T)[:, 0].cpu().numpy()
+
+    def SpeciesVisc(self, temp: float = 0.0) -> np.ndarray:
+        """Species viscosities [g/(cm s)] at temp, on the GPU (chemistry.py:1316-1359, KINGetViscosity)."""
+        import torch
+
+        if temp <= 0.0:
+            raise ChemistryError("temperature must be > 0")
+        dt = self.device_transport()
+        T = torch.tensor([float(temp)], dtype=torch.float64, device=dt.dm.device)
+        return dt.species_viscosity(T)[:, 0].cpu().numpy()
 
     def device_transport(self, device_index: int = None):
         """The viscosity tables of this chemistry set on a GPU (created on first use)."""

@@ -1395,7 +1395,7 @@ int ckmi_debug_phase_buffer(void* buf) {
   return CKMI_OK;
 }
 #endif
-int ckmi_version(void) { return 1; }
+int ckmi_version(void) { return CKMI_ABI_VERSION; }
 
 int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   if (!d || !out) return fail(CKMI_ERR_ARG, "null argument");

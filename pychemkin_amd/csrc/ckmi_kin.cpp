@@ -1140,6 +1140,7 @@ int KINPreProcess(int* isurf, int* itran, char* chem, char* surf, char* therm, c
     std::vector<double> cfits((size_t)4 * KK), f8((size_t)8 * KK);
     if (!rc) rc = ckmi_conductivity_fit(KK, s->wt.data(), params.data(), s->thermo.data(), CKMI_VISC_FIT_TLOW,
                                         CKMI_VISC_FIT_THIGH, cfits.data());
+    if (!rc) rc = ckmi_transport_set_conductivity(s->tran, cfits.data());
     if (!rc) {
       for (int k = 0; k < KK; ++k) {
         std::copy(fits.begin() + 4 * k, fits.begin() + 4 * k + 4, f8.begin() + 8 * k);
@@ -1206,6 +1207,45 @@ int KINGetMixtureViscosity(int* chemset, double* T, double* Y, double* visc) {
   rc = ckmi_mixture_viscosity(s->tran, 1, s->dbuf, s->dbuf + 1, s->dbuf + 1 + KK, nullptr);
   if (rc) return fail(rc, ckmi_last_error());
   return hip_ok(hipMemcpy(visc, s->dbuf + 1 + KK, sizeof(double), hipMemcpyDeviceToHost), "D2H");
+}
+
+// KINGetConductivity (chemkin_wrapper.py:413-418, mixture.py:1885-1909, chemistry.py:1361-1396):
+// species thermal conductivities [erg/(cm s K)] at T from the fits made by KINPreProcess (itran = 1)
+int KINGetConductivity(int* chemset, double* T, double* cond) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !cond || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  if (!s->tran) return fail(CKMI_ERR_ARG, "no transport data processed (KINPreProcess with itran = 1)");
+  const int KK = s->KK;
+  int rc = ensure_scratch(s, 1 + (size_t)KK);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, T, sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  rc = ckmi_species_conductivity(s->tran, 1, s->dbuf, s->dbuf + 1, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  return hip_ok(hipMemcpy(cond, s->dbuf + 1, KK * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+}
+
+// KINGetMixtureConductivity (chemkin_wrapper.py:449-455, mixture.py:1979-2013): mixture-averaged
+// conductivity [erg/(cm s K)], (sum X lambda + 1 / sum X / lambda) / 2.  The composition argument is
+// read as MASS fractions, as mixture.py:2002 passes self.Y (the same convention as
+// KINGetMixtureViscosity, which the CONV golden decides).
+int KINGetMixtureConductivity(int* chemset, double* T, double* Y, double* cond) {
+  std::lock_guard<std::recursive_mutex> lk(g_mu);
+  ChemSet* s = get_set(chemset);
+  if (!s || !T || !Y || !cond || !(*T > 0.0)) return fail(CKMI_ERR_ARG, "bad argument");
+  if (!s->tran) return fail(CKMI_ERR_ARG, "no transport data processed (KINPreProcess with itran = 1)");
+  const int KK = s->KK;
+  int rc = ensure_scratch(s, 2 + (size_t)KK);
+  if (rc) return rc;
+  (void)hipSetDevice(s->device);
+  std::vector<double> in(1 + KK);
+  in[0] = *T;
+  std::copy(Y, Y + KK, in.begin() + 1);
+  if ((rc = hip_ok(hipMemcpy(s->dbuf, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice), "H2D"))) return rc;
+  rc = ckmi_mixture_conductivity(s->tran, 1, s->dbuf, s->dbuf + 1, s->dbuf + 1 + KK, nullptr);
+  if (rc) return fail(rc, ckmi_last_error());
+  return hip_ok(hipMemcpy(cond, s->dbuf + 1 + KK, sizeof(double), hipMemcpyDeviceToHost), "D2H");
 }
 
 // KINGetGasReactionString (chemkin_wrapper.py:365-371, chemistry.py:1759-1781): 1-based reaction index
@@ -1457,9 +1497,7 @@ int KINAll0D_CalculateInput(int* lout, int* chemset, char* lines, int* nlines, i
 // PFR, engines, flames) and return CKMI_ERR_UNSUPPORTED with a message.
 #define CKMI_OUT_OF_SCOPE(name, what, ...) \
   int name(__VA_ARGS__) { return fail(CKMI_ERR_UNSUPPORTED, #name ": " what " is not on this path"); }
-CKMI_OUT_OF_SCOPE(KINGetConductivity, "transport", int*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetDiffusionCoeffs, "transport", int*, double*, double*, double*)
-CKMI_OUT_OF_SCOPE(KINGetMixtureConductivity, "transport", int*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetMixtureDiffusionCoeffs, "transport", int*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetOrdinaryDiffusionCoeffs, "transport", int*, double*, double*, double*, double*)
 CKMI_OUT_OF_SCOPE(KINGetThermalDiffusionCoeffs, "transport", int*, double*, double*, double*, double*, double*)

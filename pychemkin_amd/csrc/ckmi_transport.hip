@@ -1,4 +1,5 @@
-// ckmi_transport.hip -- pure-species and mixture viscosity on gfx950.
+// ckmi_transport.hip -- pure-species and mixture viscosity and thermal conductivity on gfx950
+// (SURVEY.md §8(f) rank 4).
 //
 // The reference reads a Chemkin transport file at preprocess (chemistry.py:636-687, itran = 1) and
 // its closed library evaluates viscosities on demand: KINGetViscosity (species, mixture.py:1860-1883)
@@ -20,6 +21,8 @@
 // 1 / s_j live in a per-thread LDS column ([KK][block] doubles, conflict-free), so the KK^2 Wilke
 // double loop reads its lane's vectors from LDS and the (k, j) table entries from the scalar cache.
 // Bound: FP64 VALU (KK^2 x 6 FLOP per state); HBM traffic is (KK + 2) x 8 B per state.
+// Conductivity (KINGetConductivity / KINGetMixtureConductivity, mixture.py:1885-1909,1979-2013):
+// lambda_k from the ln-T cubic of ckmi_conductivity_fit, mixed by lambda = (sum X lambda + 1 / sum X / lambda) / 2.
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -37,8 +40,10 @@ struct ckmi_transport {
   double* fits = nullptr;  // device [KK][4]
   double* A = nullptr;     // device [KK][KK]
   double* B = nullptr;     // device [KK][KK]
+  double* cfits = nullptr; // device [KK][4] conductivity fits (ckmi_transport_set_conductivity), else NULL
   const double* wt = nullptr;  // the mechanism's device weights
   std::vector<double> fits_host;
+  std::vector<double> cfits_host;
 };
 
 namespace {
@@ -137,6 +142,30 @@ __global__ void mixture_viscosity_kernel(int KK, int n, const double* __restrict
     mix += xk * (sk * sk) / den;
   }
   if (live) visc[i] = mix;
+}
+
+// one state per lane: X_k = (Y_k / W_k) / sum_j Y_j / W_j, lambda_k = exp(poly_k(ln T)),
+// lambda = (sum_k X_k lambda_k + 1 / sum_k X_k / lambda_k) / 2 (Chemkin's mixture-averaged rule, the
+// form the engine's wall heat transfer evaluates in ckmi_reactor.hpp).  Species with X_k = 0 add
+// nothing to either sum.  KK x (2 FLOP + exp) per state: FP64 VALU / transcendental bound.
+__global__ void mixture_conductivity_kernel(int KK, int n, const double* __restrict__ cfits,
+                                            const double* __restrict__ wt, const double* __restrict__ T,
+                                            const double* __restrict__ Y, double* __restrict__ cond) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = log(T[i]);
+  double sx = 0.0, sxl = 0.0, sxr = 0.0;
+  for (int k = 0; k < KK; ++k) {
+    const double xk = Y[(size_t)k * n + i] / wt[k];
+    if (xk == 0.0) continue;
+    const double* a = cfits + 4 * k;
+    const double lk = exp(fma(x, fma(x, fma(x, a[3], a[2]), a[1]), a[0]));
+    sx += xk;
+    sxl = fma(xk, lk, sxl);
+    sxr += xk / lk;
+  }
+  // with x_k unnormalised: sum X lambda = sxl / sx, 1 / sum X / lambda = sx / sxr
+  cond[i] = sx > 0.0 ? 0.5 * (sxl / sx + sx / sxr) : 0.0;
 }
 
 }  // namespace
@@ -258,8 +287,49 @@ int ckmi_transport_create(const ckmi_mech* m, const double* fits, ckmi_transport
   return CKMI_OK;
 }
 
+int ckmi_transport_set_conductivity(ckmi_transport* t, const double* cfits) {
+  if (!t || !cfits) return fail(CKMI_ERR_ARG, "ckmi_transport_set_conductivity: null argument");
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  if (prev != t->device) (void)hipSetDevice(t->device);
+  int rc = CKMI_OK;
+  if (!t->cfits && hipMalloc(&t->cfits, sizeof(double) * FIT_ORDER * t->KK) != hipSuccess)
+    rc = fail(CKMI_ERR_HIP, "ckmi_transport_set_conductivity: device allocation failed");
+  else if (hipMemcpy(t->cfits, cfits, sizeof(double) * FIT_ORDER * t->KK, hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(CKMI_ERR_HIP, "ckmi_transport_set_conductivity: upload failed");
+  else
+    t->cfits_host.assign(cfits, cfits + (size_t)FIT_ORDER * t->KK);
+  if (prev >= 0 && prev != t->device) (void)hipSetDevice(prev);
+  return rc;
+}
+
+int ckmi_species_conductivity(const ckmi_transport* t, int32_t n, const double* T, double* cond, void* stream) {
+  if (!t || n < 0 || !T || !cond) return fail(CKMI_ERR_ARG, "ckmi_species_conductivity: bad argument");
+  if (!t->cfits) return fail(CKMI_ERR_ARG, "ckmi_species_conductivity: no conductivity fits (ckmi_transport_set_conductivity)");
+  if (n == 0) return CKMI_OK;
+  const int bs = 256;
+  // the same ln-T cubic evaluation as the species viscosities, on the conductivity fits
+  hipLaunchKernelGGL(species_viscosity_kernel, dim3((n + bs - 1) / bs), dim3(bs), 0, (hipStream_t)stream, t->KK, n,
+                     t->cfits, T, cond);
+  if (hipGetLastError() != hipSuccess) return fail(CKMI_ERR_HIP, "species conductivity launch failed");
+  return CKMI_OK;
+}
+
+int ckmi_mixture_conductivity(const ckmi_transport* t, int32_t n, const double* T, const double* Y, double* cond,
+                              void* stream) {
+  if (!t || n < 0 || !T || !Y || !cond) return fail(CKMI_ERR_ARG, "ckmi_mixture_conductivity: bad argument");
+  if (!t->cfits) return fail(CKMI_ERR_ARG, "ckmi_mixture_conductivity: no conductivity fits (ckmi_transport_set_conductivity)");
+  if (n == 0) return CKMI_OK;
+  const int bs = 256;
+  hipLaunchKernelGGL(mixture_conductivity_kernel, dim3((n + bs - 1) / bs), dim3(bs), 0, (hipStream_t)stream, t->KK, n,
+                     t->cfits, t->wt, T, Y, cond);
+  if (hipGetLastError() != hipSuccess) return fail(CKMI_ERR_HIP, "mixture_conductivity_kernel launch failed");
+  return CKMI_OK;
+}
+
 int ckmi_transport_destroy(ckmi_transport* t) {
   if (!t) return CKMI_OK;
+  (void)hipFree(t->cfits);
   (void)hipFree(t->fits);
   (void)hipFree(t->A);
   (void)hipFree(t->B);

@@ -51,7 +51,8 @@ def device_transport(chem, device_index: int = None):
     key = (id(chem), int(device_index))
     dt = _tcache.get(key)
     if dt is None or dt.version != chem._version:
-        dt = _native.DeviceTransport(dm, chem._vfits)
+        cf = chem.conductivity_fits if chem._tran_params is not None else None
+        dt = _native.DeviceTransport(dm, chem._vfits, cf)
         dt.version = chem._version
         _tcache[key] = dt
     return dt

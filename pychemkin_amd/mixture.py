@@ -147,11 +147,12 @@ class Mixture:
     # ------------------------------------------------------------------ algebra
     @staticmethod
     def normalize(frac) -> Tuple[int, np.ndarray]:
-        """(0, frac / sum(frac)) (reference mixture.py:486-523)."""
-        f = np.asarray(frac, dtype=np.float64)
+        """(0, frac / sum(frac)) with negative entries set to 0 first (reference mixture.py:486-523);
+        (1, the clipped copy) when nothing positive is left (the reference exits there)."""
+        f = np.maximum(np.asarray(frac, dtype=np.float64), 0.0)
         s = f.sum()
         if s <= 0.0:
-            return 1, f.copy()
+            return 1, f
         return 0, f / s
 
     @property
@@ -189,6 +190,36 @@ class Mixture:
             raise MixtureError("invalid pressure and/or temperature")
         W = Mixture.mean_molar_mass(frac, wt, mode)
         return p * W / (R_GAS * t)
+
+    @staticmethod
+    def mass_fraction_to_concentration(chemID: int, p: float, t: float, massfrac, wt) -> np.ndarray:
+        """Molar concentrations [mol/cm3] of a mass-fraction composition at (p, t) (mixture.py:821-877):
+        c_k = rho Y_k / W_k of the normalised (negatives removed) fractions; the input back when the
+        density is not positive."""
+        massfrac = np.asarray(massfrac, dtype=np.float64)
+        wt = np.asarray(wt, dtype=np.float64)
+        if len(massfrac) != len(wt):
+            raise MixtureError(f"mass fraction and molar mass arrays must have the same size = {len(massfrac)}")
+        den = Mixture.density(chemID, p, t, frac=massfrac, wt=wt, mode="mass")
+        if not den > 0.0:
+            return massfrac
+        err, c = Mixture.normalize(massfrac)
+        return c * den / wt if err == 0 else c
+
+    @staticmethod
+    def mole_fraction_to_concentration(chemID: int, p: float, t: float, molefrac, wt) -> np.ndarray:
+        """Molar concentrations [mol/cm3] of a mole-fraction composition at (p, t) (mixture.py:879-935):
+        c_k = X_k rho / W-bar = X_k P / (R T)."""
+        molefrac = np.asarray(molefrac, dtype=np.float64)
+        wt = np.asarray(wt, dtype=np.float64)
+        if len(molefrac) != len(wt):
+            raise MixtureError(f"mole fraction and molar mass arrays must have the same size = {len(molefrac)}")
+        mwt = Mixture.mean_molar_mass(molefrac, wt, "mole")
+        den = Mixture.density(chemID, p, t, frac=molefrac, wt=wt, mode="mole")
+        if not mwt * den > 0.0:
+            return molefrac
+        err, c = Mixture.normalize(molefrac)
+        return c * (den / mwt) if err == 0 else c
 
     @property
     def RHO(self) -> float:
@@ -315,6 +346,29 @@ class Mixture:
         T = torch.tensor([self._temp], dtype=torch.float64, device=dt.dm.device)
         Y = torch.as_tensor(self.Y.reshape(self._KK, 1).copy(), dtype=torch.float64, device=dt.dm.device)
         return float(dt.mixture_viscosity(T, Y)[0].item())
+
+    def species_Cond(self) -> np.ndarray:
+        """Species thermal conductivities [erg/(cm s K)] at the mixture temperature, on the GPU
+        (KINGetConductivity, mixture.py:1885-1909)."""
+        import torch
+
+        self._need_transport()
+        dt = self._chem.device_transport()
+        T = torch.tensor([self._temp], dtype=torch.float64, device=dt.dm.device)
+        return dt.species_conductivity(T)[:, 0].cpu().numpy()
+
+    def mixture_conductivity(self) -> float:
+        """Mixture-averaged thermal conductivity [erg/(cm s K)] (KINGetMixtureConductivity with the mass
+        fractions, mixture.py:1979-2013): (sum X lambda + 1 / sum X / lambda) / 2 on the GPU."""
+        import torch
+
+        self._need_transport()
+        if not (self._Xset or self._Yset):
+            raise MixtureError("mixture composition is not provided")
+        dt = self._chem.device_transport()
+        T = torch.tensor([self._temp], dtype=torch.float64, device=dt.dm.device)
+        Y = torch.as_tensor(self.Y.reshape(self._KK, 1).copy(), dtype=torch.float64, device=dt.dm.device)
+        return float(dt.mixture_conductivity(T, Y)[0].item())
 
     def massROP(self) -> np.ndarray:
         """Species mass rates of production [g/cm3-s]."""

@@ -30,6 +30,29 @@ def test_air_density_and_conversions(chem):
     assert abs(air.WTM - (0.21 * chem.WT[3] + 0.79 * chem.WT[47])) < 1e-12
 
 
+def test_fraction_to_concentration(chem):
+    """mixture.py:821-935: c_k = rho Y_k / W_k = X_k P / (R T); negative entries removed, then normalised."""
+    from pychemkin_amd.constants import R_GAS
+
+    air = ck.Mixture(chem)
+    air.pressure, air.temperature = 2 * P_ATM, 900.0
+    air.X = ck.Air.X()
+    cx = ck.Mixture.mole_fraction_to_concentration(chem.chemID, 2 * P_ATM, 900.0, air.X, chem.WT)
+    cy = ck.Mixture.mass_fraction_to_concentration(chem.chemID, 2 * P_ATM, 900.0, air.Y, chem.WT)
+    assert np.allclose(cx, air.X * 2 * P_ATM / (R_GAS * 900.0), rtol=1e-14, atol=0)
+    assert np.allclose(cy, cx, rtol=1e-14, atol=0)
+    assert np.allclose(air.concentration, cx, rtol=1e-14, atol=0)
+    y = air.Y.copy()
+    y[0] = -1e-3  # clipped, as Mixture.normalize does (mixture.py:506-511)
+    assert np.allclose(ck.Mixture.mass_fraction_to_concentration(chem.chemID, 2 * P_ATM, 900.0, y, chem.WT), cy,
+                       rtol=1e-14, atol=0)
+    assert ck.Mixture.normalize([-1.0, 1.0, 3.0])[1].tolist() == [0.0, 0.25, 0.75]
+    from pychemkin_amd.mixture import MixtureError
+
+    with pytest.raises(MixtureError):
+        ck.Mixture.mole_fraction_to_concentration(chem.chemID, P_ATM, 300.0, air.X[:5], chem.WT)
+
+
 def test_equivalence_ratio_matches_conv_baseline(chem):
     fuel = ck.Mixture(chem)
     fuel.X = [("CH4", 1.0)]

@@ -177,7 +177,9 @@ def test_conductivity_fits_native_vs_numpy_and_golden(chem_tran, mech):
     assert np.max(np.abs(chem_tran.conductivity_fits - ref)) < 1e-9
     g = golden("speciesproperties")  # species conductivity of N2 (speciesproperties.py:106-121)
     k = chem_tran.get_specindex("N2")
-    lam = np.array([chem_tran.SpeciesCond(T)[k] for T in g["state-temperature"]]) * 1e-7  # J/(cm s K)
+    c = chem_tran.conductivity_fits[k]  # the fit evaluated here; the device evaluation is test_gpu_transport's
+    x = np.log(np.asarray(g["state-temperature"]))
+    lam = np.exp(c[0] + x * (c[1] + x * (c[2] + x * c[3]))) * 1e-7  # J/(cm s K)
     gl = np.asarray(g["state-conductivity"])
     # Warnatz form + Neufeld Omega(1,1)*: 2.2e-3 at most (Chemkin's tabulated collision integrals are
     # not restated); within the golden's tolerance (1e-6 J/(cm s K) + 1e-4) on 79 of 100 points

@@ -160,3 +160,81 @@ def test_kin_preprocess_with_transport_file(mech, chem_tr, tr, oracle):
         assert b"transport" in L.ckmi_kin_last_error()
     finally:
         kin.release(cs.value)
+
+
+def test_species_and_mixture_conductivity_match_restatement(chem_tr, mech, tr):
+    """ckmi_species_conductivity / ckmi_mixture_conductivity against the numpy restatement (1e-12)."""
+    dt = chem_tr.device_transport()
+    assert dt.has_conductivity
+    cf = chem_tr.conductivity_fits
+    rng = np.random.default_rng(11)
+    n = 5000
+    T, Y = _states(rng, mech.KK, n)
+    lam = dt.species_conductivity(T).cpu().numpy()
+    ref = tr.species_viscosity(T, cf).T  # the same ln-T cubic, on the conductivity fits
+    assert np.max(np.abs(lam / ref - 1)) < 1e-13
+    mix = dt.mixture_conductivity(T, Y.T.copy()).cpu().numpy()
+    mref = tr.mixture_conductivity(T, tr.mole_fractions(Y, mech.wt), cf)
+    assert np.all(np.isfinite(mix))
+    assert np.max(np.abs(mix / mref - 1)) < 1e-12
+    k = mech.species.index("N2")
+    Yp = np.zeros((3, mech.KK))
+    Yp[:, k] = 1.0
+    Tp = np.array([300.0, 1000.0, 2500.0])
+    assert np.allclose(dt.mixture_conductivity(Tp, Yp.T.copy()).cpu().numpy(), tr.species_viscosity(Tp, cf)[:, k],
+                       rtol=1e-13, atol=0)
+
+
+def test_conductivity_golden_through_drop_in(chem_tr, mech, tr):
+    """speciesproperties.py:106-121: SpeciesCond of N2, 300-2280 K, on the GPU (Chemistry and Mixture)."""
+    import pychemkin_amd as ck
+
+    g = golden("speciesproperties")
+    k = chem_tr.get_specindex("N2")
+    Ts = np.asarray(g["state-temperature"])
+    lam = np.array([chem_tr.SpeciesCond(T)[k] for T in Ts]) * 1e-7  # J/(cm s K), as the test divides
+    assert np.max(np.abs(lam / (tr.species_viscosity(Ts, chem_tr.conductivity_fits)[:, k] * 1e-7) - 1)) < 1e-13
+    gl = np.asarray(g["state-conductivity"])
+    # measured: 79 of 100 within the golden's tolerance, <= 2.2e-3 (DESIGN.md §4, Conductivity)
+    assert within(lam, gl, *g["tolerance-var"]).sum() == 79
+    assert np.max(np.abs(lam / gl - 1)) < 2.5e-3
+    m = ck.Mixture(chem_tr)
+    m.temperature, m.pressure = 1500.0, P_ATM
+    m.X = [("N2", 0.79), ("O2", 0.21)]
+    sc = m.species_Cond()
+    assert np.max(np.abs(sc / tr.species_viscosity([1500.0], chem_tr.conductivity_fits)[0] - 1)) < 1e-13
+    ref = tr.mixture_conductivity([1500.0], m.X[None, :], chem_tr.conductivity_fits)[0]
+    assert abs(m.mixture_conductivity() / ref - 1) < 1e-12
+
+
+def test_kin_conductivity(mech, chem_tr, tr):
+    """KINGetConductivity / KINGetMixtureConductivity (chemkin_wrapper.py:413-418,449-455) with mass fractions."""
+    from pychemkin_amd import kin
+
+    L = kin.bind()
+    cs = ct.c_int(0)
+    one = ct.c_int(1)
+    zero = ct.c_int(0)
+    names = [CHEM, "", THERM, TRAN, "chem.asc", "surf.asc", "tran.asc", ""]
+    rc = L.KINPreProcess(ct.byref(zero), ct.byref(one), *[ct.c_char_p(x.encode()) for x in names], ct.byref(cs))
+    assert rc == 0, kin.last_error()
+    try:
+        cf = chem_tr.conductivity_fits
+        lam = np.zeros(mech.KK)
+        assert L.KINGetConductivity(ct.byref(cs), ct.byref(ct.c_double(1200.0)), lam) == 0
+        assert np.max(np.abs(lam / tr.species_viscosity([1200.0], cf)[0] - 1)) < 1e-13
+        Y = ch4_air_Y(mech, 0.8)[0]
+        v = ct.c_double(0.0)
+        assert L.KINGetMixtureConductivity(ct.byref(cs), ct.byref(ct.c_double(900.0)), np.ascontiguousarray(Y),
+                                           ct.byref(v)) == 0
+        ref = tr.mixture_conductivity([900.0], tr.mole_fractions(Y, mech.wt), cf)[0]
+        assert abs(v.value / ref - 1) < 1e-12
+    finally:
+        kin.release(cs.value)
+    rc = L.KINPreProcess(ct.byref(zero), ct.byref(zero), *[ct.c_char_p(x.encode()) for x in names], ct.byref(cs))
+    assert rc == 0
+    try:
+        assert L.KINGetConductivity(ct.byref(cs), ct.byref(ct.c_double(1500.0)), np.zeros(mech.KK)) != 0
+        assert b"transport" in L.ckmi_kin_last_error()
+    finally:
+        kin.release(cs.value)

@@ -29,7 +29,7 @@ def test_ctypes_prototypes_cover_header():
 
     assert sorted(_native.PROTOTYPES) == header_functions()
     L = _native.lib()  # loads without a GPU; no compute call is made here
-    assert L.ckmi_version() == 1
+    assert L.ckmi_version() == _native.ABI_VERSION == 2
 
 
 def test_gfx950_code_object_present():
@@ -52,3 +52,54 @@ def test_oracle_is_not_linked_into_product():
                 txt = open(os.path.join(root, f)).read()
                 assert not re.search(r"^\s*(import oracle|from oracle|#include\s*[<\"].*ckoracle)", txt, re.M), f
                 assert "libckoracle" not in txt, f
+
+
+def _header_struct_fields(name):
+    """Field names of `typedef struct { ... } name;` in include/ckmi.h, in order."""
+    import re
+
+    text = open(os.path.join(ROOT, "include", "ckmi.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    m = re.search(r"typedef struct \{([^}]*)\}\s*" + name + r";", text)
+    assert m, name
+    fields = []
+    for decl in m.group(1).split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        for part in decl.split(","):
+            fields.append(re.sub(r"\[.*?\]", "", part).replace("*", " ").split()[-1])
+    return fields
+
+
+def _integration_snippet_structs():
+    """The ctypes structures of INTEGRATION.md §3's binding, executed without loading the library."""
+    import ctypes
+    import re
+
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    ns = {"ctypes": ctypes}
+    exec("from ctypes import POINTER, c_double, c_int, c_int32, c_void_p", ns)
+    for cls in ("CkmiMechDesc", "CkmiReactorCfg", "CkmiReactorExt"):
+        m = re.search(r"^class " + cls + r"\(ctypes\.Structure\):.*?(?=^\S)", text, flags=re.S | re.M)
+        assert m, f"{cls} missing from INTEGRATION.md"
+        exec(m.group(0), ns)
+    return ns
+
+
+def test_integration_snippet_matches_header_and_binding():
+    """INTEGRATION.md's published binding cannot drift from include/ckmi.h or _native (round-3 verdict)."""
+    import ctypes
+
+    from pychemkin_amd import _native
+
+    ns = _integration_snippet_structs()
+    for snip, ours, cname in ((ns["CkmiMechDesc"], _native.MechDesc, "ckmi_mech_desc"),
+                              (ns["CkmiReactorCfg"], _native.ReactorCfg, "ckmi_reactor_cfg"),
+                              (ns["CkmiReactorExt"], _native.ReactorExt, "ckmi_reactor_ext")):
+        names = [f[0] for f in snip._fields_]
+        assert names == [f[0] for f in ours._fields_], cname
+        assert names == _header_struct_fields(cname), cname
+        assert ctypes.sizeof(snip) == ctypes.sizeof(ours), cname
+        for (n, a), (_, b) in zip(snip._fields_, ours._fields_):
+            assert ctypes.sizeof(a) == ctypes.sizeof(b), (cname, n)
