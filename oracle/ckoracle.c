@@ -1176,7 +1176,7 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   }
   if ((cfg->problem == 1 || cfg->problem == 3) && cfg->nprof > 0 && cfg->prof_kind == 0) ctx.P0 = cfg->prof_v[0];
   if (cfg->problem == 3) { /* plug flow: V0 is the inlet velocity u0 [cm/s] */
-    ctx.G = ctx.P0 * Wbar0 / (RU * T0) * V0;
+    ctx.G = rho0 * V0; /* mdot / A: the inlet density (inlet pressure) x u0, with or without PPRO */
     ctx.Pm = ctx.P0 + ctx.G * V0;
   }
   b->ctx = &ctx;
@@ -1228,6 +1228,13 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   }
   int status = 0, nst = 0, stopped = 0;
   const int max_steps = cfg->max_steps > 0 ? cfg->max_steps : 200000;
+  const double guard_y = cfg->atol * 1e3 > 1e-3 ? cfg->atol * 1e3 : 1e-3;
+  double guard_tlo = 1e300, guard_thi = 0.0;
+  for (int k = 0; k < KK; ++k) {
+    if (m->thermo[17 * k] < guard_tlo) guard_tlo = m->thermo[17 * k];
+    if (m->thermo[17 * k + 2] > guard_thi) guard_thi = m->thermo[17 * k + 2];
+  }
+  guard_tlo *= 0.5;
   double tstop_final = tend;
   while (b->tn < tend * (1.0 - 1e-15)) {
     /* clamp the next step to the next critical time */
@@ -1246,6 +1253,12 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
     const double told = b->tn;
     int r = bdf_step(b, &nst);
     if (r != 0) { status = r; break; }
+    /* runaway guard (include/ckmi.h CKMI_RUN_RUNAWAY; both device kernels test the same) */
+    {
+      int bad = cfg->energy == 1 && !(b->zn[0][0] >= guard_tlo && b->zn[0][0] <= guard_thi);
+      for (int k = 0; k < KK && !bad; ++k) bad = -b->zn[0][1 + k] > guard_y;
+      if (bad) { status = 4; break; }
+    }
     const double tn = b->tn;
     /* solution saving by interpolation */
     while (isave < nsave && t_save[isave] <= tn) {

@@ -24,7 +24,7 @@ LIB_PATH = os.environ.get("CKMI_LIB") or os.path.join(_HERE, "_lib", "libckmi.so
 ABI_VERSION = 2  # CKMI_ABI_VERSION (include/ckmi.h): the layouts of MechDesc / ReactorCfg below
 NSTAT = 8
 STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "nni")
-RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures"}
+RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures", 4: "runaway"}
 
 
 class NativeError(RuntimeError):

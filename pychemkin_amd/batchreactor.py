@@ -283,6 +283,10 @@ class BatchReactors(ReactorModel):
         for kw in self._keyword_list:
             if kin.keyword_class(kw.keyphrase) == 0:
                 raise ReactorError(f"keyword {kw.keyphrase} is not supported on the device path")
+            # the engine keywords of the KIN path: the drop-in takes them from the engine's properties
+            # (set_piston_pin_offset, set_wall_heat_transfer, ...), so a raw keyword would go unread
+            if kw.keyphrase in ("POLEN", "ICHX", "GVEL", "CYBAR", "PSBAR", "DEGSAVE"):
+                raise ReactorError(f"keyword {kw.keyphrase}: set it through the engine's properties (engines/engine.py)")
         for key in self._profiles_index:
             if key not in ("VPRO", "PPRO", "TPRO", "QPRO", "AEXT"):
                 raise ReactorError(f"{key} profiles are not supported on the device path")
@@ -327,10 +331,10 @@ class BatchReactors(ReactorModel):
             prof = (p.x, p.y)
         return _native.make_cfg(
             energy=self._energytype, t_end=self._endtime, atol=self._absolute_tolerance, rtol=self._relative_tolerance,
-            h0=float(self.getkeyword("HO", 0.0)), hmax=float(self.getkeyword("STPT", 0.0)),
+            h0=float(self.getkeyword("HO", 0.0)), hmax=float(self.getkeyword("STPT", self.getkeyword("DXMX", 0.0))),
             nneg=bool(self.getkeyword("NNEG", False)), ign_mode=ign_mode, ign_val=ign_val, ign_species=ign_sp,
             ign_stop=bool(self.getkeyword("IGN_STOP", False)), profile=prof, prof_kind=prof_kind,
-            gfac=self._gasratemultiplier, max_steps=int(self.getkeyword("MAXIT", self.getkeyword("NSTP", 0)) or 0),
+            gfac=float(self.getkeyword("GFAC", self._gasratemultiplier)), max_steps=int(self.getkeyword("MAXIT", self.getkeyword("NSTP", 0)) or 0),
             **heat, **adap)
 
     # ------------------------------------------------------------------ run

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           }
           R.mass = R.rho0 * R.V0;
           if (PF && R.pfr == 1) {  // plug flow: V0 is the inlet velocity u0 [cm/s]
-            R.G = R.P0 * Wbar0 / (RU * T0) * R.V0;
+            R.G = R.rho0 * R.V0;  // mdot / A: the inlet density (inlet pressure) x u0, with or without PPRO
             R.Pm = R.P0 + R.G * R.V0;
           }
           R.gfac = cfg->gfac;
@@ -717,6 +717,16 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             c.status = c.rc;
             st = ST_FINISH;
             break;
+          }
+          {  // runaway guard: a mass fraction far below 0, or T off the thermo range (energy runs)
+            const double z0 = b.zn[0];
+            double v = isp ? -z0 : -1.0;
+            if (lane == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
+            if (wave_max(v) > dcfg->guard_y) {
+              c.status = CKMI_RUN_RUNAWAY;
+              st = ST_FINISH;
+              break;
+            }
           }
           const double tn = S.tn;
           while (c.isave < io.nsave && io.t_save[c.isave] <= tn) {
@@ -1414,6 +1424,15 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   m->device = dev;
   m->KK = KK;
   m->II = II;
+  {  // runaway guard range from the NASA-7 fits
+    double tlo = 1e300, thi = 0.0;
+    for (int k = 0; k < KK; ++k) {
+      tlo = std::min(tlo, d->thermo[17 * k + 0]);
+      thi = std::max(thi, d->thermo[17 * k + 2]);
+    }
+    m->tguard_lo = 0.5 * tlo;
+    m->tguard_hi = thi;
+  }
   // ---- order reactions: elementary, then third-body, then falloff
   std::vector<int> ordr;
   // strips stay type-uniform: chemically activated reactions run in the falloff strips
@@ -1836,6 +1855,9 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
     tc.erase(std::unique(tc.begin(), tc.end()), tc.end());
     dc.ncrit = (int)tc.size();
     std::copy(tc.begin(), tc.end(), dc.tcrit);
+    dc.guard_y = std::max(1e-3, 1e3 * cfg->atol);
+    dc.guard_tlo = m->tguard_lo;
+    dc.guard_thi = m->tguard_hi;
   }
   ReactorIO io{problem, T0, P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save,
                ext ? ext->afac_rxn : nullptr, ext ? ext->afac : nullptr, ext ? ext->max_adap : 0,

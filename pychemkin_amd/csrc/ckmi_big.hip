@@ -1118,7 +1118,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           R.P0 = (R.conp && R.npv > 0) ? cfg->prof_v[0] : P0;
           R.mass = R.rho0 * R.V0;
           if (R.pfr) {  // plug flow: V0 is the inlet velocity u0 [cm/s]
-            R.G = R.P0 * Wbar0 / (RU * T0) * R.V0;
+            R.G = R.rho0 * R.V0;  // mdot / A (inlet density x u0), with or without PPRO
             R.Pm = R.P0 + R.G * R.V0;
           }
           R.gfac = cfg->gfac;
@@ -1598,6 +1598,16 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             c.status = c.rc;
             st = ST_FINISH;
             break;
+          }
+          {  // runaway guard (ckmi.hip reactor_kernel): one workgroup max per step
+            const double z0 = b.zn[0];
+            double v = isp ? -z0 : -1.0;
+            if (tid == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
+            if (bmax(B, v, wid, lane) > dcfg->guard_y) {
+              c.status = CKMI_RUN_RUNAWAY;
+              st = ST_FINISH;
+              break;
+            }
           }
           const double tn = S.tn;
           while (c.isave < io.nsave && io.t_save[c.isave] <= tn) {

@@ -73,6 +73,7 @@ struct ckmi_mech {
   bool has_plog = false;     // PLOG / chemically activated / general reactions: extended kernel variants
   bool has_general = false;  // FORD / RORD / non-integral coefficients (rxn_general)
   std::vector<int> slot_of;  // original reaction -> device slot
+  double tguard_lo = 0.0, tguard_hi = 1e300;  // runaway guard: min_k T_low,k / 2, max_k T_high,k
   ckmi::JitRop* jit = nullptr;
 };
 

@@ -278,7 +278,9 @@ int apply_profiles(ckmi_reactor_cfg& c) {
       if (p.key == "TPRO" && g_r.energy != 2) return fail(CKMI_ERR_ARG, "TPRO needs a fixed-temperature reactor");
       c.nprof = np;
       c.prof_kind = p.key == "TPRO" ? 1 : 0;
-      std::copy(p.x.begin(), p.x.end(), c.prof_t);
+      // plug flow integrates in x - x0 (KINAll0D_SetupPFRInputs); profile abscissae are absolute positions
+      const double shift = g_r.problem == 3 ? g_r.x0 : 0.0;
+      for (int i = 0; i < np; ++i) c.prof_t[i] = p.x[i] - shift;
       std::copy(p.y.begin(), p.y.end(), c.prof_v);
     } else if (p.key == "QPRO" || p.key == "AEXT") {
       // QPRO takes the second slot; AEXT the second alone, or the third beside a QPRO
@@ -346,13 +348,19 @@ int run_reactor(ChemSet* s) {
   int rc = apply_keywords(s, c, dtsv, adap);
   if (!rc) rc = apply_profiles(c);
   if (rc) return rc;
+  if (g_r.problem == 3) {  // MOMEN OFF means a given pressure: the PPRO profile supplies it
+    for (const auto& kv : g_r.kw)
+      if (kv.first == "MOMEN" && upper(trim(kv.second)) == "OFF" && !(c.nprof > 0 && c.prof_kind == 0))
+        return fail(CKMI_ERR_ARG, "MOMEN OFF needs a PPRO pressure profile (the momentum equation gives the pressure otherwise)");
+  }
   if (engine) {
     if (c.qloss != 0.0 || c.htc != 0.0 || c.nprof > 0 || c.nprof2 > 0)
       return fail(CKMI_ERR_UNSUPPORTED, "QLOS / HTC / profiles do not apply to an engine cylinder (use ICHX)");
     if (c.eng[CKMI_ENG_HTMODEL] == 1.0) {
       if (!s->dtran) return fail(CKMI_ERR_ARG, "ICHX needs transport data (KINPreProcess with itran = 1)");
-      if (!(c.eng[CKMI_ENG_CYBAR] > 0.0) || !(c.eng[CKMI_ENG_PSBAR] > 0.0))
-        return fail(CKMI_ERR_ARG, "ICHX needs the head areas (CYBAR, PSBAR)");
+      // CYBAR / PSBAR default to 1.0 (ChemkinKeywordTips.yaml:429-436)
+      if (!(c.eng[CKMI_ENG_CYBAR] > 0.0)) c.eng[CKMI_ENG_CYBAR] = 1.0;
+      if (!(c.eng[CKMI_ENG_PSBAR] > 0.0)) c.eng[CKMI_ENG_PSBAR] = 1.0;
       c.tran = s->dtran;
     }
   }

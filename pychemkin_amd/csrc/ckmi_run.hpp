@@ -57,7 +57,14 @@ struct DevCfg {
   ckmi_reactor_cfg c;
   int ncrit;
   double tcrit[192];  // breakpoints of the three profiles (64 each)
+  // runaway guard (CKMI_RUN_RUNAWAY): -Y_k above guard_y, or T outside [guard_tlo, guard_thi]
+  double guard_y, guard_tlo, guard_thi;
 };
+// true when an accepted state has left the physical domain (tested once per step by both kernels;
+// oracle/ckoracle.c runaway() is the same test)
+__device__ __forceinline__ bool runaway_value_bad(const DevCfg* d, double T) {
+  return !(T >= d->guard_tlo && T <= d->guard_thi);
+}
 __device__ __forceinline__ int n_crit(const DevCfg* d) { return d->ncrit + 1; }
 __device__ __forceinline__ double crit_time(const DevCfg* d, double tend, int idx) {
   return idx < d->ncrit ? d->tcrit[idx] : tend;

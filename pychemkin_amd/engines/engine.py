@@ -203,17 +203,15 @@ class Engine(BatchReactors):
         return self.enginestroke * self.borearea
 
     def list_engine_parameters(self):
-        print("      === engine parameters ===")
-        print(f"bore diameter         = {self.borediam} [cm]")
-        print(f"stroke                = {self.enginestroke} [cm]")
-        print(f"connecting rod length = {self.connectrodlength} [cm]")
-        print(f"cylinder head area    = {self.cylinderheadarea} [cm2]")
-        print(f"piston head area      = {self.pistonheadarea} [cm2]")
-        print(f"piston offset         = {self.pistonoffset} [cm]")
-        print(f"compression ratio     = {self.compressratio} [-]")
-        print(f"engine speed          = {self.enginespeed} [RPM]")
-        print(f"IVC crank angle       = {self.IVCCA} [degree]")
-        print(f"EVO crank angle       = {self.EVOCA} [degree]")
+        """Print the cylinder geometry and operating point, one quantity per line."""
+        rows = (("bore", self.borediam, "cm"), ("stroke", self.enginestroke, "cm"),
+                ("rod length", self.connectrodlength, "cm"), ("head area", self.cylinderheadarea, "cm2"),
+                ("piston area", self.pistonheadarea, "cm2"), ("pin offset", self.pistonoffset, "cm"),
+                ("CMPR", self.compressratio, "-"), ("speed", self.enginespeed, "rpm"),
+                ("IVC", self.IVCCA, "deg CA"), ("EVO", self.EVOCA, "deg CA"))
+        print("engine:")
+        for name, value, unit in rows:
+            print(f"  {name:<12s} {value:>14.6g}  {unit}")
 
     @property
     def CAstep_for_saving_solution(self) -> float:
@@ -272,15 +270,14 @@ class Engine(BatchReactors):
         e[0:7] = [self.IVCCA, self.enginespeed, self.compressratio, self.borediam, self.enginestroke,
                   self.connectrodlength / self.crankradius, self.pistonoffset]
         if self._wallheattransfer:
-            if self.cylinderheadarea <= 0.0 or self.pistonheadarea <= 0.0:
-                raise ReactorError("wall heat transfer needs the cylinder head and piston head areas")
             gv = self.gasvelocity or [2.28, 0.308, 3.24, 0.0]  # Woschni's constants when GVEL is absent
             e[7] = 1.0
             e[8:11] = self.heattransferparameters
             e[11] = self.cylinderwalltemperature
             e[12:16] = gv
-            e[16] = self.cylinderheadarea / self.borearea
-            e[17] = self.pistonheadarea / self.borearea
+            # CYBAR / PSBAR default to 1 (the head areas equal the bore area, ChemkinKeywordTips.yaml:429-436)
+            e[16] = self.cylinderheadarea / self.borearea if self.cylinderheadarea > 0.0 else 1.0
+            e[17] = self.pistonheadarea / self.borearea if self.pistonheadarea > 0.0 else 1.0
         return e
 
     def save_times(self) -> np.ndarray:

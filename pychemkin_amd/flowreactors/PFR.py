@@ -156,6 +156,8 @@ class PlugFlowReactor(BatchReactors):
         mix = self.reactormixture
         u0 = float(mix.velocity)
         cfg = self.reactor_cfg()  # PPRO (in x: the momentum equation is then off) or TPRO(x) as for CONP
+        for i in range(cfg.nprof):  # the kernel integrates in x - x0; profile abscissae are absolute positions
+            cfg.prof_t[i] -= self._startposition
         dm = self._chem.device_mechanism()
         xs = self._save_grid(span, u0)
         res = dm.reactor_run(cfg, np.array([PFR_PROBLEM], np.int32), np.array([mix.temperature]),
@@ -192,12 +194,12 @@ class PlugFlowReactor(BatchReactors):
         mix0 = self.reactormixture
         Wbar = 1.0 / (Y / mix0.WT).sum(axis=1)
         pp = self.getprofile("PPRO")
-        Pin = pp.y[0] if pp is not None else mix0.pressure
-        G = Pin * mix0.WTM / (R_GAS * mix0.temperature) * self._u0
+        # mass flux mdot / A = the inlet density (at the inlet pressure) x u0, with or without PPRO
+        G = mix0.pressure * mix0.WTM / (R_GAS * mix0.temperature) * self._u0
         if pp is not None:
-            P = np.interp(x, pp.x, pp.y)
+            P = np.interp(x + self._startposition, pp.x, pp.y)  # x from the start position; pp.x absolute
         else:
-            Pm = Pin + G * self._u0
+            Pm = mix0.pressure + G * self._u0
             P = 0.5 * (Pm + np.sqrt(Pm * Pm - 4.0 * G * G * R_GAS * T / Wbar))
         u = G / (P * Wbar / (R_GAS * T))
         return P, u

@@ -122,6 +122,17 @@ def test_one_keyword_policy_with_the_kin_abi(chem):
     assert r.reactor_cfg().max_steps == 5000
     for k, c in (("ATOL", 1), ("rtol", 1), ("DTSV", 1), ("DELT", 2), ("NADAP", 2), ("ATLO", 0), ("ASEN", 0)):
         assert kin.keyword_class(k) == c, k
+    # device keywords set as raw keywords are read, not dropped (round-3 advice)
+    r.setkeyword("GFAC", 2.0)
+    r.setkeyword("DXMX", 1e-5)
+    cfg = r.reactor_cfg()
+    assert cfg.gfac == 2.0 and cfg.hmax == 1e-5
+    r.removekeyword("GFAC")
+    r.removekeyword("DXMX")
+    r.setkeyword("POLEN", 0.5)  # an engine keyword on a batch reactor: rejected, not silently unread
+    with pytest.raises(ReactorError, match="POLEN"):
+        r.reactor_cfg()
+    r.removekeyword("POLEN")
     r.setprofile(ck.reactormodel.Profile("HTCPRO", [0.0, 1.0], [1.0, 2.0]))
     with pytest.raises(ReactorError, match="HTCPRO"):
         r.reactor_cfg()

@@ -172,3 +172,36 @@ def test_cold_lean_cylinders_with_nneg(tables, oracle, mech):
         r, _ = oracle.reactor(T0[i], P0[i], 1.0, Y0[i], problem=4, engine=bench.hcci_block(), tran=tf, **run)
         assert r.status == 0 and res["stats"][j, 6] == 0
         assert abs(res["T"][j] / r.T - 1) < 1e-5 and abs(res["P"][j] / r.P - 1) < 1e-5
+
+
+def test_cold_lean_cylinders_without_nneg_fail_fast(tables, oracle, mech):
+    """The same five cylinders without NNEG (round-3 verdict): those that run away end at once with
+    CKMI_RUN_RUNAWAY (status 4) instead of burning up to 200,000 steps, on the GPU and in the oracle; the
+    rest complete.  Every cylinder stops within 2,000 steps (the oracle finishes the healthy ones in ~530)."""
+    import torch
+
+    import bench
+    from pychemkin_amd import _native
+
+    dm = _native.DeviceMechanism(tables)
+    T0, P0, Y0 = bench.model_sweep(mech, 1, 0, 16 ** 3 * 4, 420.0, 520.0, P_ATM, 2 * P_ATM, 0.3, 1.0)
+    idx = [378, 389, 1738, 1815, 2903]
+    tf = tran_fits(mech)
+    run = dict(bench.RUN, t_end=258.0 / 6000.0)
+    res = {k: v.cpu().numpy() for k, v in dm.reactor_run(
+        _native.make_cfg(engine=bench.hcci_block(), tran=torch.tensor(tf, dtype=torch.float64, device=dm.device), **run),
+        np.full(len(idx), 4, np.int32), T0[idx], P0[idx], np.ones(len(idx)), Y0[idx]).items()}
+    st = res["stats"]
+    assert set(st[:, 6].tolist()) <= {0, 4}, st[:, 6]
+    assert st[:, 0].max() < 2000, st[:, 0]
+    for j, i in enumerate(idx):
+        if st[j, 6] == 4:  # ended in the physical domain's neighbourhood, not at 10,000 K
+            assert res["T"][j] < 1000.0 and res["Y"][j].min() > -0.01
+        else:
+            r, _ = oracle.reactor(T0[i], P0[i], 1.0, Y0[i], problem=4, engine=bench.hcci_block(), tran=tf, **run)
+            if r.status == 0:
+                assert abs(res["T"][j] / r.T - 1) < 1e-4
+    # the oracle's own runaway (cylinder 389 at rtol 1.062e-8, DESIGN.md §4) ends with the same status
+    r, Y = oracle.reactor(T0[389], P0[389], 1.0, Y0[389], problem=4, engine=bench.hcci_block(), tran=tf,
+                          **dict(run, rtol=1.062e-8))
+    assert r.status == 4 and r.nst < 1000 and Y.min() > -0.01
