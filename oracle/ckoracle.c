@@ -396,7 +396,10 @@ static double engine_hA(const rctx* c, double T, double P, double rho, double V,
   const cko_mech* m = c->m;
   const int KK = m->KK;
   const double* tf = c->cfg->tran;
-  const double lnT = log(T);
+  /* gas properties at the film temperature (T + Twall) / 2: the hcciengine golden's own heat loss, backed
+     out of its P / rho / V columns, is a constant multiple of this form (relative spread 4e-4 over
+     -134..-90 CA) and not of the bulk-temperature form (7e-3, drifting with T); scripts/hcci_golden_heat.py */
+  const double lnT = log(0.5 * (T + e[CKO_ENG_TWALL]));
   double X[NMAX], mu[NMAX], lam[NMAX], sx = 0.0;
   for (int k = 0; k < KK; ++k) {
     X[k] = fmax(Y[k], 0.0) / m->wt[k];  /* transport of the non-negative part of the composition */

@@ -112,7 +112,8 @@ __device__ __forceinline__ void engine_volume(const double* e, double t, double&
   dVdt = Ab * (a * sn + u * a * cs / r) * omega;
 }
 // Wall heat loss coefficient h A [erg/(K s)] of the ICHX correlation with the Woschni gas velocity
-// (oracle/ckoracle.c engine_hA, same arithmetic): lane 1 + k holds species k (X_k, Y_k); mu by Wilke
+// (oracle/ckoracle.c engine_hA, same arithmetic; lnT is the log of the film temperature at which mu and
+// lambda are evaluated): lane 1 + k holds species k (X_k, Y_k); mu by Wilke
 // over the species fits of cfg->tran, lambda = 0.5 (sum X lambda + 1 / sum X / lambda).  Wave-uniform
 // result; the KK^2 Wilke sum broadcasts (sqrt eta_j, W_j, X_j) lane by lane.
 __device__ __forceinline__ double engine_hA(const MechView& Mv, const RunCtx& R, double T, double lnT, double P,
@@ -452,7 +453,9 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
         const double cpmass = wave_sum(Yk * cpk);
         // transport of the non-negative part of the composition (oracle engine_hA)
         const double xp = fmax(Yk, 0.0) * rw;
-        q1 = engine_hA(V, R, T, lnT, P, rho, V_, xp / wave_sum(xp), cpmass, isp, s);
+        // transport properties at the film temperature (T + Twall) / 2 (oracle engine_hA)
+        q1 = engine_hA(V, R, T, log(0.5 * (T + R.cfg->eng[CKMI_ENG_TWALL])), P, rho, V_, xp / wave_sum(xp), cpmass,
+                       isp, s);
         fT -= q1 * (T - R.cfg->eng[CKMI_ENG_TWALL]) / mcp;
       }
     } else if (!pfr) {

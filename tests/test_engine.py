@@ -121,16 +121,70 @@ def test_oracle_engine_against_golden(hcci_oracle_run, mech):
     Pg = np.asarray(g["state-pressure"])
     p = ps * 1e-6
     ok = within(p, Pg, *g["tolerance-var"])
-    # pressure: within the golden's tolerance through the first 32 CA of compression (measured: the first
-    # 54 points), then the wall heat loss of the published ICHX / Woschni form (about 1.2x the golden's)
-    # shows: -0.3 % at -82 CA, ignition (peak pressure) 3 CA late
-    assert ok[:40].all() and ok.sum() >= 50
-    assert abs(np.argmax(p) - np.argmax(Pg)) * 0.5 <= 3.5
+    # pressure (measured, film-temperature properties): within the golden's tolerance on exactly the first
+    # 58 points and one more (-142 ... -113.5 CA), then the residual of the heat-transfer coefficient shows
+    # (the golden's h is 0.888 x this form, uniformly: test_golden_heat_loss_is_a_uniform_multiple); the
+    # pressure peak comes 2 CA late (11.5 vs 9.5 CA)
+    assert ok[:58].all() and ok.sum() == 59
+    assert abs(np.argmax(p) - np.argmax(Pg)) * 0.5 == 2.0
     assert abs(p.max() / Pg.max() - 1) < 0.15
-    # the golden's Cp column (CPBL [kJ/mol-K]) on the same early points
-    cp_R = np.array([np.sum(ys[i, 1:] / mech.wt * _cpR(mech, ys[i, 0])) for i in range(40)])
-    cp = cp_R * 8.31447247 / np.sum(ys[:40, 1:] / mech.wt, axis=1) * 1e-3
-    assert np.all(within(cp, np.asarray(g["state-Cp"])[:40], *g["tolerance-var"]))
+    # the golden's Cp column (CPBL [kJ/mol-K]) on all 517 points: the first 181 (to -52 CA) and 186 in all
+    cp_R = np.array([np.sum(ys[i, 1:] / mech.wt * _cpR(mech, ys[i, 0])) for i in range(len(ys))])
+    cp = cp_R * 8.31447247 / np.sum(ys[:, 1:] / mech.wt, axis=1) * 1e-3
+    okc = within(cp, np.asarray(g["state-Cp"]), *g["tolerance-var"])
+    assert okc[:181].all() and okc.sum() == 186
+
+
+def test_golden_heat_loss_is_a_uniform_multiple(mech):
+    """The hcciengine golden's own wall heat loss, backed out of its P / rho / V / Cp columns before the
+    low-temperature chemistry (-134 ... -90 CA; frozen charge, so T = P Wbar / (rho R) and the golden's Cp
+    column reproduces to 1e-15 at that T), is a constant multiple of the ICHX / Woschni h A (T - Twall)
+    with mu and lambda at the film temperature (T + Twall) / 2: the same factor on the head and the liner
+    area, relative spread < 1e-3; with bulk-temperature properties the ratio drifts with T (spread 7e-3).
+    The factor itself, 0.888, is the unexplained residual; scripts/hcci_golden_heat.py."""
+    from oracle import transport_ref as trf
+    from oracle.oracle import Oracle
+    from pychemkin_amd.constants import R_GAS
+
+    orc = Oracle(mech)
+    Y = charge_Y(mech)
+    Wbar = 1.0 / np.sum(Y / mech.wt)
+    X = Y / mech.wt * Wbar
+    g = golden("hcciengine")
+    ca = np.asarray(g["state-crank_angle"])
+    P, rho, V = (np.asarray(g[k]) for k in ("state-pressure", "state-density", "state-volume"))
+    P = P * 1e6
+    T = P * Wbar / (rho * R_GAS)
+    cp_mol = R_GAS * np.array([orc.thermo(t)[0] for t in T]) @ X
+    sel = (ca >= -134) & (ca <= -90)
+    assert np.max(np.abs(cp_mol[sel] * 1e-10 / np.asarray(g["state-Cp"])[sel] - 1)) < 1e-13
+    e = engine_block()
+    t = (ca - ca[0]) / (6 * ENG["rpm"])
+    Q = -(rho[0] * V[0] * (cp_mol - R_GAS) / Wbar * np.gradient(T, t) + P * np.gradient(V, t))
+    params = trf.parse_transport(open(TRAN).read())
+    pl = [params[s] for s in mech.species]
+    vf, cf = trf.viscosity_fits(mech.wt, pl, 3500.0), trf.conductivity_fits(mech.wt, pl, mech.to_tables()["thermo"], 3500.0)
+    B, Tw = ENG["bore"], ENG["twall"]
+    Ab = np.pi * B * B / 4
+    a, L, ee = ENG["stroke"] / 2, ENG["rod"], -ENG["polen"]
+    Vc = Ab * (np.sqrt((L + a) ** 2 - ee ** 2) - np.sqrt((L - a) ** 2 - ee ** 2)) / (ENG["cr"] - 1)
+    w = ENG["gvel"][0] * 2 * ENG["stroke"] * ENG["rpm"] / 60  # P = P_motored before ignition
+    head, liner = np.full_like(T, (e[16] + e[17]) * Ab), np.pi * B * (V - Vc) / Ab
+
+    def h_of(Tp):
+        mu = trf.mixture_viscosity(Tp, np.tile(X, (len(Tp), 1)), mech.wt, vf)
+        lam = trf.mixture_conductivity(Tp, np.tile(X, (len(Tp), 1)), cf)
+        return ENG["ht"][0] * (rho * w * B / mu) ** ENG["ht"][1] * lam / B
+
+    for Tp, spread in ((0.5 * (T + Tw), 1e-3), (T, 5e-3)):
+        Aeff = (Q / (h_of(Tp) * (T - Tw)))[sel]
+        r = Aeff / (head + liner)[sel]
+        if spread < 2e-3:
+            assert r.std() / r.mean() < spread and abs(r.mean() - 0.888) < 2e-3
+            coef = np.linalg.lstsq(np.stack([head[sel], liner[sel]], 1), Aeff, rcond=None)[0]
+            assert np.all(np.abs(coef - 0.888) < 5e-3)  # head and liner alike: not an area form
+        else:
+            assert r.std() / r.mean() > spread
 
 
 def _cpR(mech, T):
@@ -235,15 +289,16 @@ def test_engine_keywords_in_the_one_keyword_policy():
 
 
 def test_oracle_runaway_guard(mech, oracle):
-    """CKMI_RUN_RUNAWAY in the oracle: cylinder 389 of the bench's cold-lean sweep without NNEG at rtol
-    1.062e-8 ran away to 8,277 K over 200,000 steps (round 3); the guard ends it within ~530 steps at a
-    mass fraction of -1e-3, while the same cylinder at rtol 1e-8 completes with status 0."""
+    """CKMI_RUN_RUNAWAY in the oracle: without NNEG, one of 200 rtol-perturbed runs of the bench's five
+    cold-lean cylinders (378 at rtol 1.02e-8; round 3: 389 at 1.062e-8, 8,277 K after 200,000 steps) runs
+    away through negative trace concentrations; the guard ends it within ~640 steps at a mass fraction of
+    -1e-3, while the same cylinder at rtol 1e-8 completes with status 0."""
     import bench
 
     T0, P0, Y0 = bench.model_sweep(mech, 1, 0, 16 ** 3 * 4, 420.0, 520.0, P_ATM, 2 * P_ATM, 0.3, 1.0)
     tf = tran_fits(mech)
     run = dict(bench.RUN, t_end=258.0 / 6000.0, problem=4, engine=bench.hcci_block(), tran=tf)
-    r, Y = oracle.reactor(T0[389], P0[389], 1.0, Y0[389], **dict(run, rtol=1.062e-8))
+    r, Y = oracle.reactor(T0[378], P0[378], 1.0, Y0[378], **dict(run, rtol=1.02e-8))
     assert r.status == 4 and r.nst < 1000 and -0.01 < Y.min() < -1e-3 and r.T < 1000.0
-    r, Y = oracle.reactor(T0[389], P0[389], 1.0, Y0[389], **run)
+    r, Y = oracle.reactor(T0[378], P0[378], 1.0, Y0[378], **run)
     assert r.status == 0 and Y.min() > -1e-3
