@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -250,6 +251,9 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           c.nadap = 0;
           c.avar_last = bcast(yl, cfg->avar > 0 ? cfg->avar : 0);
           c.T0 = T0;
+          c.yguard = dcfg->guard_y;
+          c.tguard_lo = dcfg->guard_tlo;
+          c.tguard_hi = dcfg->guard_thi;
           S.rtol = cfg->rtol;
           S.atol = cfg->atol;
           S.nneg = cfg->nneg;
@@ -390,6 +394,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             st = ST_FINISH;
             break;
           }
+
           c.tc = crit_time(dcfg, c.tend, c.icrit);
           if (S.tn + S.hprime > c.tc) {
             const double hp = c.tc - S.tn;
@@ -708,7 +713,13 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             }
           }
           S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-          c.rc = 0;
+          {  // runaway guard on the accepted state: a mass fraction far below 0, or T off the thermo range
+             // (energy runs); it ends the reactor through ST_STEP_END's failure exit
+            const double z0 = b.zn[0];
+            double v = isp ? -z0 : -1.0;
+            if (lane == 0 && R.energy == 1 && !(z0 >= c.tguard_lo && z0 <= c.tguard_hi)) v = 1e300;
+            c.rc = wave_max(v) > c.yguard ? CKMI_RUN_RUNAWAY : 0;
+          }
           st = ST_STEP_END;
           break;
         }
@@ -717,16 +728,6 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             c.status = c.rc;
             st = ST_FINISH;
             break;
-          }
-          {  // runaway guard: a mass fraction far below 0, or T off the thermo range (energy runs)
-            const double z0 = b.zn[0];
-            double v = isp ? -z0 : -1.0;
-            if (lane == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
-            if (wave_max(v) > dcfg->guard_y) {
-              c.status = CKMI_RUN_RUNAWAY;
-              st = ST_FINISH;
-              break;
-            }
           }
           const double tn = S.tn;
           while (c.isave < io.nsave && io.t_save[c.isave] <= tn) {
@@ -1078,6 +1079,144 @@ int upload(ckmi_mech* m, const std::vector<T>& v, const T** out) {
   return CKMI_OK;
 }
 
+// ---------------------------------------------------------------- LDS lane assignment
+// The reaction strips scatter each lane's rate into the wave's wdot[] with one LDS atomic per unit
+// slot (reactor_rhs, rop_kernel) and gather C[] / g/RT[] through the same slots.  Which reaction sits
+// on which lane of its (type, slot-class) block, and in which order a reaction's unit slots are
+// listed, are free choices (products and sums over the slots commute); they decide the LDS bank
+// conflicts: ds_add_f64 is serviced in 16-lane groups on banks (a/4) mod 32, so two lanes of a group
+// adding to one species (or to species k and k + 16) serialise; ds_read_b64 in 32-lane groups on
+// banks (a/4) mod 64, where distinct species k and k + 32 collide.  Common species (H, O, OH, H2O)
+// make the mechanism's file order 4x conflict-bound (GRI-3.0: 456 LDS cycles of atomics per RHS
+// against 108 conflict-free, model below).  A deterministic annealing over lane swaps within a block
+// and slot orders within a reaction minimises the modelled cycles; the device code is unchanged.
+namespace lanes {
+struct Rx {
+  int ns[2];        // unit slots per side (a species with coefficient c occupies c slots)
+  uint8_t sp[2][4]; // the slots' species
+};
+// modelled LDS cycles of one strip (64 lanes): atomics (16-lane groups, max bank multiplicity) +
+// two gathers per slot (32-lane groups, max distinct addresses per bank)
+static int strip_cost(const std::vector<Rx>& rx, const std::vector<int>& lane_rx, int s0) {
+  bool s23 = false;
+  for (int l = 0; l < WAVE; ++l) {
+    const int r = lane_rx[s0 + l];
+    if (r >= 0 && (rx[r].ns[0] > 2 || rx[r].ns[1] > 2)) s23 = true;
+  }
+  int cost = 0;
+  for (int side = 0; side < 2; ++side)
+    for (int u = 0; u < (s23 ? 4 : 2); ++u) {
+      for (int g0 = 0; g0 < WAVE; g0 += 16) {  // atomics
+        int mult[32] = {0}, mx = 0;
+        for (int l = g0; l < g0 + 16; ++l) {
+          const int r = lane_rx[s0 + l];
+          if (r < 0 || u >= rx[r].ns[side]) continue;
+          mx = std::max(mx, ++mult[(2 * rx[r].sp[side][u]) & 31]);
+        }
+        cost += mx;
+      }
+      for (int g0 = 0; g0 < WAVE; g0 += 32) {  // gathers (C and g/RT: counted twice)
+        int seen[64];
+        int nseen = 0, mult[64] = {0}, mx = 0;
+        for (int l = g0; l < g0 + 32; ++l) {
+          const int r = lane_rx[s0 + l];
+          if (r < 0 || u >= rx[r].ns[side]) continue;
+          const int k = rx[r].sp[side][u];
+          bool dup = false;
+          for (int q = 0; q < nseen; ++q) dup |= seen[q] == k;
+          if (dup) continue;
+          seen[nseen++] = k;
+          mx = std::max(mx, ++mult[(2 * k) & 63]);
+        }
+        cost += 2 * mx;
+      }
+    }
+  return cost;
+}
+}  // namespace lanes
+
+// slots: device slot -> original reaction (-1 pad), reordered in place within (rtype, slot class)
+// blocks; perm[i]: the unit-slot order of original reaction i (reactant slots 0..3, product 4..7)
+void assign_lanes(const ckmi_mech_desc* d, std::vector<int>& slots, const std::vector<int>& blk,
+                  std::vector<std::array<uint8_t, 8>>& perm) {
+  using lanes::Rx;
+  const int II = d->II, n = (int)slots.size();
+  std::vector<Rx> rx(II);
+  perm.assign(II, {0, 1, 2, 3, 0, 1, 2, 3});
+  for (int i = 0; i < II; ++i) {
+    Rx& r = rx[i];
+    for (int side = 0; side < 2; ++side) {
+      const int ns = side == 0 ? d->nr[i] : d->np[i];
+      const int32_t* sp = (side == 0 ? d->rsp : d->psp) + CKMI_SLOTS * i;
+      const double* nu = (side == 0 ? d->rnu : d->pnu) + CKMI_SLOTS * i;
+      int c = 0;
+      for (int u = 0; u < ns && !rxn_general(d, i); ++u)
+        for (int k = 0; k < (int)nu[u] && c < 4; ++k) r.sp[side][c++] = (uint8_t)sp[u];
+      r.ns[side] = rxn_general(d, i) ? 0 : c;
+    }
+  }
+  const int nstrip = n / WAVE;
+  std::vector<int> cost(nstrip);
+  for (int s = 0; s < nstrip; ++s) cost[s] = lanes::strip_cost(rx, slots, s * WAVE);
+  uint64_t st = 0x9e3779b97f4a7c15ull;  // deterministic: the same image on every run and device
+  auto rnd = [&]() {
+    st ^= st << 13, st ^= st >> 7, st ^= st << 17;
+    return st;
+  };
+  double temp = 2.0;
+  const int iters = 400 * n;
+  for (int it = 0; it < iters; ++it, temp = std::max(0.05, temp * (1.0 - 6.0 / iters))) {
+    const int a = (int)(rnd() % n);
+    if (slots[a] < 0) continue;
+    int b = -1;
+    Rx save_a = rx[slots[a]];
+    if (rnd() & 1) {  // swap two lanes of one block
+      b = (int)(rnd() % n);
+      if (b == a || slots[b] < 0 || blk[slots[b]] != blk[slots[a]]) continue;
+      std::swap(slots[a], slots[b]);
+    } else {  // swap two unit slots of one side of one reaction
+      Rx& r = rx[slots[a]];
+      const int side = (int)(rnd() & 1);
+      if (r.ns[side] < 2) continue;
+      const int u = (int)(rnd() % r.ns[side]), v = (int)(rnd() % r.ns[side]);
+      if (u == v || r.sp[side][u] == r.sp[side][v]) continue;
+      std::swap(r.sp[side][u], r.sp[side][v]);
+    }
+    const int sa = a / WAVE, sb = b >= 0 ? b / WAVE : sa;
+    const int ca = lanes::strip_cost(rx, slots, sa * WAVE), cb = sb != sa ? lanes::strip_cost(rx, slots, sb * WAVE) : 0;
+    const int delta = ca + cb - cost[sa] - (sb != sa ? cost[sb] : 0);
+    const double x = (double)(rnd() >> 11) * (1.0 / 9007199254740992.0);
+    if (delta <= 0 || x < std::exp(-delta / temp)) {
+      cost[sa] = ca;
+      if (sb != sa) cost[sb] = cb;
+    } else if (b >= 0) {
+      std::swap(slots[a], slots[b]);
+    } else {
+      rx[slots[a]] = save_a;
+    }
+  }
+  // the slot orders as permutations of the file's unit-slot expansion
+  for (int i = 0; i < II; ++i) {
+    Rx ref;
+    for (int side = 0; side < 2; ++side) {
+      const int ns = side == 0 ? d->nr[i] : d->np[i];
+      const int32_t* sp = (side == 0 ? d->rsp : d->psp) + CKMI_SLOTS * i;
+      const double* nu = (side == 0 ? d->rnu : d->pnu) + CKMI_SLOTS * i;
+      int c = 0;
+      for (int u = 0; u < ns && !rxn_general(d, i); ++u)
+        for (int k = 0; k < (int)nu[u] && c < 4; ++k) ref.sp[side][c++] = (uint8_t)sp[u];
+      bool used[4] = {false, false, false, false};
+      for (int u = 0; u < rx[i].ns[side]; ++u)
+        for (int v = 0; v < rx[i].ns[side]; ++v)
+          if (!used[v] && ref.sp[side][v] == rx[i].sp[side][u]) {
+            used[v] = true;
+            perm[i][4 * side + u] = (uint8_t)v;
+            break;
+          }
+    }
+  }
+}
+
 // Pack the compact mechanism image (ckmi_image.hpp) from the device-slot tables.
 int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& slots, const std::vector<int>& flags,
                 const std::vector<int>& nrp, const std::vector<int4>& rsp, const std::vector<int4>& psp,
@@ -1086,7 +1225,8 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
                 const std::vector<double>& beta0, const std::vector<double>& Ea0, const std::vector<double>& fp,
                 const std::vector<double>& rlnA, const std::vector<double>& rbeta, const std::vector<double>& rEa,
                 const std::vector<int>& tb, const std::vector<int>& gptr, const std::vector<int>& gsp,
-                const std::vector<double>& geff, const std::vector<double>& wt, const std::vector<double>& rwt) {
+                const std::vector<double>& geff, const std::vector<double>& wt, const std::vector<double>& rwt,
+                const std::vector<std::array<uint8_t, 8>>& perm) {
   const int KK = m->KK, IIp = m->IIpad, G = m->G;
   const int KKp = (KK + 1 + WAVE - 1) / WAVE * WAVE;  // room for the dummy species slot
   const int sp_one = KKp - 1;                          // = SP_ONE (63) whenever KK <= 63
@@ -1103,20 +1243,24 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     const bool gen = (flags[s] & RX_GEN) != 0;  // real coefficients: no unit slots, aux stream
     // unit-coefficient slots: a species with coefficient c occupies c slots
     int ns_r = 0, ns_p = 0;
+    int ur[4] = {0, 0, 0, 0}, up[4] = {0, 0, 0, 0};  // unit slots in file order, then in assign_lanes' order
     for (int u = 0; u < nr && !gen; ++u) {
       const int c = (int)rnu[u * IIp + s];
       nu |= (uint32_t)std::min(c, 15) << (4 * u);
       for (int k = 0; k < c; ++k, ++ns_r)
-        if (ns_r < 4) a |= (uint32_t)r4[u] << (8 * ns_r);
+        if (ns_r < 4) ur[ns_r] = r4[u];
     }
     for (int u = 0; u < np && !gen; ++u) {
       const int c = (int)pnu[u * IIp + s];
       nu |= (uint32_t)std::min(c, 15) << (16 + 4 * u);
       for (int k = 0; k < c; ++k, ++ns_p)
-        if (ns_p < 4) b |= (uint32_t)p4[u] << (8 * ns_p);
+        if (ns_p < 4) up[ns_p] = p4[u];
     }
     if (ns_r > 4 || ns_p > 4)
       return fail(CKMI_ERR_UNSUPPORTED, "more than 4 molecules (sum of coefficients) on a reaction side");
+    const uint8_t* pm = slots[s] >= 0 ? perm[slots[s]].data() : nullptr;
+    for (int u = 0; u < ns_r; ++u) a |= (uint32_t)ur[pm ? pm[u] : u] << (8 * u);
+    for (int u = 0; u < ns_p; ++u) b |= (uint32_t)up[pm ? pm[4 + u] : u] << (8 * u);
     for (int u = ns_r; u < 4; ++u) a |= (uint32_t)sp_one << (8 * u);
     for (int u = ns_p; u < 4; ++u) b |= (uint32_t)sp_one << (8 * u);
     urs[s] = a;
@@ -1445,11 +1589,15 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
     for (int u = 0; u < d->np[i]; ++u) up += d->pnu[CKMI_SLOTS * i + u];
     return (ur > 2.0 || up > 2.0) ? 1 : 0;
   };
+  std::vector<int> blk(II, -1);  // (rtype, slot class) block of each reaction: lanes swap within one
   for (int t : {CKMI_RXN_ELEMENTARY, CKMI_RXN_LT, CKMI_RXN_THIRDBODY, CKMI_RXN_FALLOFF, CKMI_RXN_CHEMACT, CKMI_RXN_PLOG,
                 CKMI_RXN_CHEB})
     for (int cls = 0; cls < 3; ++cls)
       for (int i = 0; i < II; ++i)
-        if (d->rtype[i] == t && slot_class(i) == cls) ordr.push_back(i);
+        if (d->rtype[i] == t && slot_class(i) == cls) {
+          ordr.push_back(i);
+          blk[i] = 8 * t + cls;
+        }
   for (int i = 0; i < II; ++i) {
     if (d->rtype[i] < 0 || d->rtype[i] > CKMI_RXN_LT) {
       delete m;
@@ -1492,6 +1640,12 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   }
   const int IIpad = std::max(WAVE, (int)((slots.size() + WAVE - 1) / WAVE * WAVE));
   while ((int)slots.size() < IIpad) slots.push_back(-1);
+  std::vector<std::array<uint8_t, 8>> perm;
+  {
+    const char* e = std::getenv("CKMI_LANES");  // A/B knob: CKMI_LANES=0 keeps the file order
+    if (e && e[0] == '0') perm.assign(II, {0, 1, 2, 3, 0, 1, 2, 3});
+    else assign_lanes(d, slots, blk, perm);
+  }
   m->IIpad = IIpad;
   m->slot_of.assign(II, -1);
   // ---- third-body groups (distinct efficiency lists)
@@ -1648,7 +1802,7 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
   rc |= upload(m, gsp, &D.gsp);
   rc |= upload(m, geff, &D.geff);
   rc |= build_image(m, d, slots, flags, nrp, rsp, psp, rnu, pnu, lnA, beta, Ea, lnA0, beta0, Ea0, fp, rlnA, rbeta, rEa,
-                    tb, gptr, gsp, geff, wt, rwt);
+                    tb, gptr, gsp, geff, wt, rwt, perm);
   if (rc) {
     ckmi_mech_destroy(m);
     return rc;
@@ -1888,6 +2042,11 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
       return fail(CKMI_ERR_UNSUPPORTED, "engine reactors (problem 4) need KK + 1 <= 64 (the wave-per-reactor kernel)");
     rc = launch_big_reactors(m, n, dc, io, st);
   }
+#ifdef CKMI_PROBE_C3
+  // ISA probe build (scripts/isa_probe.sh): only the configs[2] kernel is instantiated, so that its
+  // register / scratch figures come out of a one-variant compile; never linked into libckmi.so
+  else rc = launch_reactors<54>(m, n, dc, io, st, no_pf);
+#else
   else if (m->has_plog) {
     rc = f64 ? launch_reactors<64, true, true>(m, n, dc, io, st) : launch_reactors<64, true>(m, n, dc, io, st, no_pf);
     if (!rc && !f64) rc = launch_reactors<64, true, true>(m, n, dc, io, st, SEL_PFR);
@@ -1901,6 +2060,7 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
     rc = f64 ? launch_reactors<64, false, true>(m, n, dc, io, st) : launch_reactors<64>(m, n, dc, io, st, no_pf);
     if (!rc && !f64) rc = launch_reactors<64, false, true>(m, n, dc, io, st, SEL_PFR);
   }
+#endif
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;

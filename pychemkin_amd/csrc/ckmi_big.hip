@@ -1589,7 +1589,13 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             }
           }
           S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-          c.rc = 0;
+          {  // runaway guard on the accepted state (ckmi.hip reactor_kernel): one workgroup max per step,
+             // the reactor ends through ST_STEP_END's failure exit
+            const double z0 = b.zn[0];
+            double v = isp ? -z0 : -1.0;
+            if (tid == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
+            c.rc = bmax(B, v, wid, lane) > dcfg->guard_y ? CKMI_RUN_RUNAWAY : 0;
+          }
           st = ST_STEP_END;
           break;
         }
@@ -1598,16 +1604,6 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             c.status = c.rc;
             st = ST_FINISH;
             break;
-          }
-          {  // runaway guard (ckmi.hip reactor_kernel): one workgroup max per step
-            const double z0 = b.zn[0];
-            double v = isp ? -z0 : -1.0;
-            if (tid == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
-            if (bmax(B, v, wid, lane) > dcfg->guard_y) {
-              c.status = CKMI_RUN_RUNAWAY;
-              st = ST_FINISH;
-              break;
-            }
           }
           const double tn = S.tn;
           while (c.isave < io.nsave && io.t_save[c.isave] <= tn) {

@@ -18,8 +18,8 @@
 //   nu        u32 [IIp]   (unused by the device kernels; kept for layout stability)
 //   info      u32 [IIp]   type:2 rev:1 hasrev:1 ftype:3 nr:3 np:3 | aux index << 16
 //   tb        i32 [IIp]   >= 0 third-body group, <= -2 single collider species -(tb+2), -1 none
-//   aux       double [naux][12]  lnA0 b0 E0/R, falloff parameters (TROE: a, 1/T***, 1/T*, T**;
-//                                SRI: a, b, 1/c, d, e), REV lnA b E/R, pad
+//   aux       double [naux][13]  lnA0 b0 E0/R, falloff parameters (TROE: a, 1/T***, 1/T*, T**;
+//                                SRI: a, b, 1/c, d, e), REV lnA b E/R, pad (AUXW)
 //   gptr i32 [G+1], gsp i32 [ng], geff double [ng]   third-body efficiency lists (eff - 1)
 //   geffd double [G][KKp]   the same lists dense (eff - 1, 0 for unlisted species)
 //   e2t   double [64]       2^(j/64), the table of fexp
@@ -29,7 +29,10 @@
 
 namespace ckmi {
 
-constexpr int AUXW = 12;
+// aux record width in doubles: odd, so that the records of consecutive lanes (a falloff strip reads
+// ax[0..10] of its own record) start on distinct bank pairs of ds_read_b64 (26-dword stride: conflict-
+// free across a 32-lane group; 12 doubles = 24 dwords was 4-way)
+constexpr int AUXW = 13;
 constexpr int SP_ONE = 63;  // dummy species slot of the reactor kernel's images (KK <= 63)
 constexpr int KK_IMAGE_MAX = 255;  // species bytes: the dummy slot KKp - 1 must fit in 8 bits
 
@@ -354,7 +357,7 @@ __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t i
 constexpr uint32_t RX_GEN = 0x4000u;
 constexpr int GEN_SLOTS = 8;                                  // species per side of a general reaction
 constexpr int GEN_P = 2 + 3 * GEN_SLOTS;                        // first product slot of the aux stream
-constexpr int GEN_RECORDS = (2 + 6 * GEN_SLOTS + 11) / 12;      // 2 + 48 doubles in AUXW records
+constexpr int GEN_RECORDS = (2 + 6 * GEN_SLOTS + AUXW - 1) / AUXW;  // 2 + 48 doubles in AUXW records
 
 // C^o for a reaction order o, the rule of oracle/ckoracle.c conc_pow: exact products for
 // o = 0..3; for 0 < o < 1 C^o above CONC_FLOOR and the chord CONC_FLOOR^(o-1) C below it (negative

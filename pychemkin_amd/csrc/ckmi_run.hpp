@@ -94,6 +94,7 @@ struct Ctl {
   int is_count, max_steps, nadap;
   double avar_last;
   double delp, saved_t, told, dsm, tc, tend, hmax, T0;
+  double yguard, tguard_lo, tguard_hi;  // runaway guard (DevCfg), copied per reactor
   double st_h0, st_tout, st_h, is_hg, is_hub, is_hlb, is_t0;
 };
 

@@ -21,6 +21,7 @@ from pychemkin_amd import _native
 _L = ctypes.CDLL(_native.LIB_PATH)
 for _k in [k for k in _native.PROTOTYPES if not hasattr(_L, k)]:
     _native.PROTOTYPES.pop(_k)
+_native.ABI_VERSION = _L.ckmi_version()  # an A/B may time an older build of the same reactor entry points
 n = %d
 mech = bench.mechanism()
 dm = _native.DeviceMechanism(mech.to_tables(), device=0)
