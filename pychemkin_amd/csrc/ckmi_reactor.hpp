@@ -579,8 +579,19 @@ struct NewtonMatrixGJ64 {
       const int p = uni(mask ? (int)__ffsll((unsigned long long)mask) - 1 : 0);
       const bool me = lane == p;
       if (me) {
+#ifndef CKMI_GJ_B128
+        // 64-bit stores by inline asm: any register pair is a valid source, so the allocator never
+        // re-packs the row into 4-VGPR tuples for ds_write_b128 (2 v_mov per processed column and
+        // step: ~3,000 VALU issues per factorisation at N = 54).  LDS operations of one wave complete
+        // in issue order, so the other lanes' ds_read_b128 after wave_lds_sync see these stores.
+        const uint32_t rb = (uint32_t)(uintptr_t)row;
+#pragma unroll
+        for (int j = 0; j < N; ++j)
+          asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rb), "v"(a[j]), "i"(8 * j) : "memory");
+#else
 #pragma unroll
         for (int j = 0; j < N; j += 2) row[j / 2] = make_double2(a[j], a[j + 1]);
+#endif
       }
       wave_lds_sync();  // other lanes' reads must follow the pivot lane's writes
       const double piv = bcast(a[k], p);

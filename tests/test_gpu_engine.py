@@ -81,9 +81,14 @@ def test_hcci_golden_through_drop_in(chem_tran, mech):
     assert np.max(np.abs(den / np.asarray(g["state-density"]) - 1)) < 1e-7
     Pg = np.asarray(g["state-pressure"])
     ok = within(pres, Pg, *g["tolerance-var"])
-    assert ok[:40].all() and ok.sum() >= 50  # as the oracle (test_engine.py)
-    assert abs(np.argmax(pres) - np.argmax(Pg)) * 0.5 <= 3.5
-    assert abs(delayCA - CA[np.argmax(Pg)]) < 5.0
+    # measured, as the oracle (test_engine.py): the first 58 points and 59 in all; the peak 2 CA late
+    assert ok[:58].all() and ok.sum() == 59
+    assert abs(np.argmax(pres) - np.argmax(Pg)) * 0.5 == 2.0
+    assert abs(delayCA - CA[np.argmax(Pg)]) < 3.0
+    # the golden's Cp column (CPBL kJ/(mol K)) on all 517 points: the first 181 and 186 in all (oracle alike)
+    cp = np.array([e.get_solution_mixture_at_index(solution_index=i).CPBL() for i in range(n)]) * 1e-10
+    okc = within(cp, np.asarray(g["state-Cp"]), *g["tolerance-var"])
+    assert okc[:181].all() and okc.sum() == 186
 
 
 def test_engine_refused_above_63_species(big_mech):
@@ -141,7 +146,7 @@ def test_hcci_golden_through_kin_calls(mech):
         rho = P / (8.31447247e7 * T) / np.sum(Y.T / mech.wt, axis=1)
         assert np.max(np.abs(rho / np.asarray(g["state-density"]) - 1)) < 1e-7
         ok = within(P * 1e-6, np.asarray(g["state-pressure"]), *g["tolerance-var"])
-        assert ok[:40].all() and ok.sum() >= 50
+        assert ok[:58].all() and ok.sum() == 59  # as the drop-in and the oracle
         hr = [ct.c_double(0.0) for _ in range(6)]
         q = np.zeros(1)
         assert L.KINAll0D_GetEngineHeatRelease(q, *[ct.byref(x) for x in hr[1:]]) == 0
