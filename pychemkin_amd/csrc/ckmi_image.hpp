@@ -22,7 +22,7 @@
 //                                SRI: a, b, 1/c, d, e), REV lnA b E/R, pad (AUXW)
 //   gptr i32 [G+1], gsp i32 [ng], geff double [ng]   third-body efficiency lists (eff - 1)
 //   geffd double [G][KKp]   the same lists dense (eff - 1, 0 for unlisted species)
-//   e2t   double [64]       2^(j/64), the table of fexp
+//   e2t   double [32]       2^(j/32), the table of fexp (E2T_N)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -139,23 +139,35 @@ __device__ __forceinline__ double powi(double c, int nu) {
   return r;
 }
 
-// exp(x) by Tang's table method: x = (64 m + j) ln2/64 + r, |r| <= ln2/128, e^x = 2^m 2^(j/64) e^r
-// with a degree-6 polynomial for e^r - 1 and the 64-entry table in LDS.  <= 1 ulp from the
-// correctly rounded value (checked against glibc over [-740, 709], 2e7 points); ~17 VALU
-// instructions + 1 LDS read instead of ~40 for the library exp.  NaN propagates; |x| > 1000
-// saturates to 0 / inf.
+// exp(x) by Tang's table method: x = (32 m + j) ln2/32 + r, |r| <= ln2/64, e^x = 2^m 2^(j/32) e^r
+// with a degree-6 polynomial for e^r - 1 (truncation 3e-18 relative at |r| = ln2/64, far below the
+// rounding of the result) and the 32-entry table in LDS: 32 doubles are 64 dwords, one per LDS bank,
+// so a wave's random-index gathers never conflict (a 64-entry table put entries j and j + 32 on one
+// bank pair: ~2-way on most gathers).  ~17 VALU instructions + 1 LDS read instead of ~40 for the
+// library exp.  NaN propagates; |x| > 1000 saturates to 0 / inf.
+#ifndef CKMI_E2T_64
+constexpr int E2T_N = 32;
+constexpr int E2T_SHIFT = 5;
+constexpr double E2T_INV_L = 46.166241308446828;          // 32 / ln 2
+constexpr double E2T_L_HI = 0x1.62e42fefa39efp-6;         // (ln 2)_hi / 32
+constexpr double E2T_L_LO = 0x1.abc9e3b39803fp-61;        // (ln 2)_lo / 32
+#else  // A/B only: the round-3 64-entry table
+constexpr int E2T_N = 64;
+constexpr int E2T_SHIFT = 6;
+constexpr double E2T_INV_L = 92.332482616893656;
+constexpr double E2T_L_HI = 0x1.62e42fefa39efp-7;
+constexpr double E2T_L_LO = 0x1.abc9e3b39803fp-62;
+#endif
 __device__ __forceinline__ double fexp(double x, const double* e2t) {
-  constexpr double INV_L = 92.332482616893656;           // 64 / ln 2
-  constexpr double L_HI = 0x1.62e42fefa39efp-7;           // (ln 2)_hi / 64
-  constexpr double L_LO = 0x1.abc9e3b39803fp-62;          // (ln 2)_lo / 64
+  constexpr double INV_L = E2T_INV_L, L_HI = E2T_L_HI, L_LO = E2T_L_LO;
   x = x < -1000.0 ? -1000.0 : (x > 1000.0 ? 1000.0 : x);
   const double kd = __builtin_rint(x * INV_L);
   const double r = fma(kd, -L_LO, fma(kd, -L_HI, x));
   const int k = (int)kd;
   const double p = fma(r * r,
                        fma(r, fma(r, fma(r, fma(r, 1.0 / 720.0, 1.0 / 120.0), 1.0 / 24.0), 1.0 / 6.0), 0.5), r);
-  const double t = e2t[k & 63];
-  return ldexp(fma(t, p, t), k >> 6);
+  const double t = e2t[k & (E2T_N - 1)];
+  return ldexp(fma(t, p, t), k >> E2T_SHIFT);
 }
 
 // ------------------------------------------------------------------ NASA-7 (lane = species)

@@ -134,3 +134,40 @@ def test_big_mechanism_tube(big_mech):
     assert r.status == 0 and res["stats"][0, 6] == 0
     assert abs(res["tau"][0] / r.tau - 1) < 1e-4 and abs(res["T"][0] / r.T - 1) < 1e-5
     assert abs(res["V"][0] / r.V - 1) < 1e-5
+
+
+def test_start_position_with_pressure_profile(chem):
+    """Round-3 advice: a tube that starts at x0 > 0 reads its PPRO profile at absolute positions, and its mass
+    flux is the inlet's (mdot / A) whatever PPRO(x0) is.  A tube from x0 = 1 cm with P(x) equals a tube from 0
+    with the profile shifted by -x0; both end at the pressure the profile gives at the absolute end."""
+    import pychemkin_amd as ck
+    from pychemkin_amd.flowreactors.PFR import PlugFlowReactor_FixedTemperature
+
+    def tube(x0, px, pv):
+        feed = ck.Stream(chem)
+        feed.temperature = T_IN
+        feed.pressure = P_IN
+        feed.X = FEED
+        feed.velocity = U_IN
+        t = PlugFlowReactor_FixedTemperature(feed)
+        t.diameter = DIAM
+        t.length = 3.0 + x0
+        if x0 > 0.0:
+            t.set_start_position(x0)
+        t.set_pressure_profile(px, pv)
+        t.timestep_for_saving_solution = 0.01
+        assert t.run() == 0
+        return t
+
+    px = np.array([0.0, 1.0, 2.0, 4.0])
+    pv = P_IN * np.array([1.0, 0.9, 0.8, 0.7])
+    a = tube(1.0, px, pv)
+    b = tube(0.0, px - 1.0, pv)
+    assert abs(a._final["P"] / (P_IN * 0.7) - 1) < 1e-12  # P(4 cm) of the absolute profile
+    assert abs(a._final["P"] / b._final["P"] - 1) < 1e-12
+    assert abs(a._final["T"] / b._final["T"] - 1) < 1e-12
+    assert np.max(np.abs(a._final["Y"] - b._final["Y"])) < 1e-12
+    # the outlet velocity is mdot / (rho A): the inlet's mass flux at the outlet density
+    rho_out = a._final["P"] / (ck.constants.R_GAS * a._final["T"]) / np.sum(a._final["Y"] / chem.WT)
+    rho_in = P_IN / (ck.constants.R_GAS * T_IN) / np.sum(a.reactormixture.Y / chem.WT)
+    assert abs(a._final["V"] / (rho_in * U_IN / rho_out) - 1) < 1e-10
