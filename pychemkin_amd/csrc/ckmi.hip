@@ -411,13 +411,12 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           c.saved_t = S.tn;
           c.ncf = c.nef = 0;
           c.nflag = NF_FIRST;
-          if (uni(S.nst) > 0 && uni(S.hprime) != uni(S.h)) {
-            const int qp = uni(S.qprime), q = uni(S.q);
-            if (qp != q) {
-              bdf_adjust_order(b, S, qp - q);
-              S.q = qp;
-              S.L = qp + 1;
-              S.qwait = qp + 1;
+          if (S.nst > 0 && S.hprime != S.h) {
+            if (S.qprime != S.q) {
+              bdf_adjust_order(b, S, S.qprime - S.q);
+              S.q = S.qprime;
+              S.L = S.q + 1;
+              S.qwait = S.L;
             }
             bdf_rescale(b, S);
           }
@@ -427,11 +426,8 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
         case ST_STEP_ATTEMPT: {
           bdf_predict(b, S);
           bdf_set(b, S);
-          {
-            const int nflag = uni(c.nflag), nst = uni(S.nst);
-            c.convfail = (nflag == NF_FIRST || nflag == NF_ERR_FAIL) ? CF_NONE : CF_OTHER;
-            c.call_setup = (nflag != NF_FIRST) || nst == 0 || nst >= uni(S.nstlp) + MSBP || fabs(uni(S.gamrat) - 1.0) > DGMAX;
-          }
+          c.convfail = (c.nflag == NF_FIRST || c.nflag == NF_ERR_FAIL) ? CF_NONE : CF_OTHER;
+          c.call_setup = (c.nflag != NF_FIRST) || S.nst == 0 || S.nst >= S.nstlp + MSBP || fabs(S.gamrat - 1.0) > DGMAX;
           st = ST_NLS_ATTEMPT;
           break;
         }
@@ -443,16 +439,16 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
         case ST_NLS_F: {
           b.ftemp = fe;
           S.nfe++;
-          if (!uni(c.call_setup)) {
+          if (!c.call_setup) {
             b.acor = 0.0;
             c.delp = 0.0;
             c.mm = 0;
             st = ST_NEWTON_ITER;
             break;
           }
-          const double dgamma = uni(fabs(S.gamma / S.gammap - 1.0));
-          const int nst = uni(S.nst), cf = uni(c.convfail);
-          const int jbad = nst == 0 || nst >= uni(S.nstlj) + MSBJ || (cf == CF_BAD_J && dgamma < DGMAX) || cf == CF_OTHER;
+          const double dgamma = fabs(S.gamma / S.gammap - 1.0);
+          const int jbad = S.nst == 0 || S.nst >= S.nstlj + MSBJ || (c.convfail == CF_BAD_J && dgamma < DGMAX) ||
+                           c.convfail == CF_OTHER;
           if (jbad) {
             // exclusive use of the workgroup's J scratch until it is copied out
             for (;;) {
@@ -520,23 +516,16 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           ph[PH_SOLVE] += __builtin_amdgcn_s_memtime() - t0;
 #endif
           S.nni++;
-          const double gamrat = uni(S.gamrat);
-          if (gamrat != 1.0) x *= 2.0 / (1.0 + gamrat);
+          if (S.gamrat != 1.0) x *= 2.0 / (1.0 + S.gamrat);
           if (!act) x = 0.0;
           const double del = wrms_lane(x, b.ewt, n);
           b.acor += x;
           b.y = b.zn[0] + b.acor;
-          const int mm = uni(c.mm);
-          const double delp = uni(c.delp);
-          double crate = uni(S.crate);
-          if (mm > 0) {
-            crate = fmax(CRDOWN * crate, del / delp);
-            S.crate = crate;
-          }
-          const double dcon = uni(del * fmin(1.0, crate) / S.tq[4]);
+          if (c.mm > 0) S.crate = fmax(CRDOWN * S.crate, del / c.delp);
+          const double dcon = del * fmin(1.0, S.crate) / S.tq[4];
           if (dcon <= 1.0) {
             bool negfail = false, negfix = false;
-            if (uni(S.nneg)) {
+            if (S.nneg) {
               const bool neg = act && lane >= 1 && b.y < 0.0;
               const double xn = neg ? b.y * b.ewt : 0.0;
               const double ss = wave_sum(xn * xn);
@@ -557,13 +546,13 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
               st = ST_NLS_FAIL;
               break;
             }
-            S.acnrm = (mm == 0 && !negfix) ? del : wrms_lane(b.acor, b.ewt, n);
+            S.acnrm = (c.mm == 0 && !negfix) ? del : wrms_lane(b.acor, b.ewt, n);
             S.jcur = 0;
             st = ST_ERRTEST;
             break;
           }
-          c.mm = mm + 1;
-          if (mm + 1 == MAXCOR || (mm + 1 >= 2 && del > RDIV * delp)) {
+          c.mm++;
+          if (c.mm == MAXCOR || (c.mm >= 2 && del > RDIV * c.delp)) {
             c.failed = 1;
             st = ST_NLS_FAIL;
             break;
@@ -605,32 +594,30 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           break;
         }
         case ST_ERRTEST: {
-          const double dsm = uni(S.acnrm * S.tq[2]);
-          c.dsm = dsm;
-          if (dsm <= 1.0) {
+          c.dsm = S.acnrm * S.tq[2];
+          if (c.dsm <= 1.0) {
             st = ST_STEP_COMPLETE;
             break;
           }
-          const int nef = uni(c.nef) + 1;
-          c.nef = nef;
+          c.nef++;
           S.nef_tot++;
           c.nflag = NF_ERR_FAIL;
           bdf_restore(b, S, c.saved_t);
-          if (fabs(S.h) <= S.hmin * ONEPSM || nef == MXNEF) {
+          if (fabs(S.h) <= S.hmin * ONEPSM || c.nef == MXNEF) {
             c.rc = CKMI_RUN_ERRTEST;
             st = ST_STEP_END;
             break;
           }
           S.etamax = 1.0;
           st = ST_STEP_ATTEMPT;
-          if (nef <= MXNEF1) {
-            S.eta = 1.0 / (eta_root(BIAS2 * dsm, uni(S.L)) + ADDON);
+          if (c.nef <= MXNEF1) {
+            S.eta = 1.0 / (eta_root(BIAS2 * c.dsm, S.L) + ADDON);
             S.eta = fmax(ETAMIN, fmax(S.eta, S.hmin / fabs(S.h)));
-            if (nef >= SMALL_NEF) S.eta = fmin(S.eta, ETAMXF);
+            if (c.nef >= SMALL_NEF) S.eta = fmin(S.eta, ETAMXF);
             bdf_rescale(b, S);
             break;
           }
-          if (uni(S.q) > 1) {
+          if (S.q > 1) {
             S.eta = fmax(ETAMIN, S.hmin / fabs(S.h));
             bdf_adjust_order(b, S, -1);
             S.L = S.q;
@@ -653,87 +640,79 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           break;
         }
         case ST_STEP_COMPLETE: {
-          // the integrator's integer state and the branch-deciding doubles as wave-uniform values (SGPRs,
-          // scalar branches): read from LDS they look lane-varying and every test becomes an exec-mask branch
-          const double dsm = uni(c.dsm);
-          const int nst = uni(S.nst) + 1;
-          S.nst = nst;
+          const double dsm = c.dsm;
+          S.nst++;
           c.nst++;
           S.hu = S.h;
-          const int q = uni(S.q), L = uni(S.L);
 #pragma unroll
           for (int i = QMAX; i >= 2; --i)
-            if (i <= q) S.tau[i] = S.tau[i - 1];
-          if (q == 1 && nst > 1) S.tau[2] = S.tau[1];
+            if (i <= S.q) S.tau[i] = S.tau[i - 1];
+          if (S.q == 1 && S.nst > 1) S.tau[2] = S.tau[1];
           S.tau[1] = S.h;
 #pragma unroll
           for (int j = 0; j <= QMAX; ++j)
-            if (j <= q) b.zn[j] += S.l[j] * b.acor;
-          int qwait = uni(S.qwait) - 1;
-          if (qwait == 1 && q != QMAX) {
+            if (j <= S.q) b.zn[j] += S.l[j] * b.acor;
+          S.qwait--;
+          if (S.qwait == 1 && S.q != QMAX) {
             b.zn[QMAX] = b.acor;
             S.saved_tq5 = S.tq[5];
           }
-          if (uni(S.etamax) == 1.0) {
-            if (qwait < 2) qwait = 2;
-            S.qprime = q;
+          if (S.etamax == 1.0) {
+            if (S.qwait < 2) S.qwait = 2;
+            S.qprime = S.q;
             S.hprime = S.h;
             S.eta = 1.0;
           } else {
-            const double etaq = 1.0 / (eta_root(BIAS2 * dsm, L) + ADDON);
-            if (qwait != 0) {
+            const double etaq = 1.0 / (eta_root(BIAS2 * dsm, S.L) + ADDON);
+            if (S.qwait != 0) {
               S.eta = etaq;
-              S.qprime = q;
+              S.qprime = S.q;
             } else {
-              qwait = 2;
+              S.qwait = 2;
               double etaqm1 = 0.0, etaqp1 = 0.0;
-              if (q > 1) {
+              if (S.q > 1) {
                 double znq = 0.0;
 #pragma unroll
                 for (int j = 0; j <= QMAX; ++j)
-                  if (j == q) znq = b.zn[j];
+                  if (j == S.q) znq = b.zn[j];
                 const double ddn = wrms_lane(act ? znq : 0.0, b.ewt, n) * S.tq[1];
-                etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, q) + ADDON);
+                etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, S.q) + ADDON);
               }
-              const double stq5 = uni(S.saved_tq5);
-              if (q != QMAX && stq5 != 0.0) {
+              if (S.q != QMAX && S.saved_tq5 != 0.0) {
                 const double hr = S.h / S.tau[2];
                 double hrL = hr;
-                for (int j = 1; j < L; ++j) hrL *= hr;
-                const double cquot = (S.tq[5] / stq5) * hrL;
+                for (int j = 1; j < S.L; ++j) hrL *= hr;
+                const double cquot = (S.tq[5] / S.saved_tq5) * hrL;
                 const double tv = act ? b.acor - cquot * b.zn[QMAX] : 0.0;
                 const double dup = wrms_lane(tv, b.ewt, n) * S.tq[3];
-                etaqp1 = 1.0 / (eta_root(BIAS3 * dup, L + 1) + ADDON);
+                etaqp1 = 1.0 / (eta_root(BIAS3 * dup, S.L + 1) + ADDON);
               }
-              const double etam = uni(fmax(etaqm1, fmax(etaq, etaqp1)));
+              const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
               if (etam < THRESH) {
                 S.eta = 1.0;
-                S.qprime = q;
+                S.qprime = S.q;
               } else if (etam == etaq) {
                 S.eta = etaq;
-                S.qprime = q;
+                S.qprime = S.q;
               } else if (etam == etaqm1) {
                 S.eta = etaqm1;
-                S.qprime = q - 1;
+                S.qprime = S.q - 1;
               } else {
                 S.eta = etaqp1;
-                S.qprime = q + 1;
+                S.qprime = S.q + 1;
                 b.zn[QMAX] = b.acor;
               }
             }
-            const double eta = uni(S.eta);
-            if (eta < THRESH) {
+            if (S.eta < THRESH) {
               S.eta = 1.0;
               S.hprime = S.h;
             } else {
-              const double e2 = fmin(eta, S.etamax);
-              const double e3 = e2 / fmax(1.0, fabs(S.h) * S.hmax_inv * e2);
-              S.eta = e3;
-              S.hprime = S.h * e3;
+              S.eta = fmin(S.eta, S.etamax);
+              S.eta /= fmax(1.0, fabs(S.h) * S.hmax_inv * S.eta);
+              S.hprime = S.h * S.eta;
             }
           }
-          S.qwait = qwait;
-          S.etamax = (nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+          S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
           {  // runaway guard on the accepted state: a mass fraction far below 0, or T off the thermo range
              // (energy runs); it ends the reactor through ST_STEP_END's failure exit
             const double z0 = b.zn[0];

@@ -816,10 +816,9 @@ __device__ __forceinline__ double wrms_lane(double v, double ewt, int n) {
 template <class BB>
 __device__ __forceinline__ void bdf_rescale(BB& b, BdfS& S) {
   double factor = S.eta;
-  const int q = uni(S.q);
 #pragma unroll
   for (int j = 1; j <= QMAX; ++j) {
-    if (j <= q) {
+    if (j <= S.q) {
       b.zn[j] *= factor;
       factor *= S.eta;
     }
@@ -832,7 +831,7 @@ __device__ __forceinline__ void bdf_rescale(BB& b, BdfS& S) {
 template <class BB>
 __device__ __forceinline__ void bdf_predict(BB& b, BdfS& S) {
   S.tn += S.h;
-  const int q = uni(S.q);
+  const int q = S.q;
   double z[QMAX + 1];
 #pragma unroll
   for (int j = 0; j <= QMAX; ++j) z[j] = b.zn[j];
@@ -848,7 +847,7 @@ __device__ __forceinline__ void bdf_predict(BB& b, BdfS& S) {
 template <class BB>
 __device__ __forceinline__ void bdf_restore(BB& b, BdfS& S, double saved_t) {
   S.tn = saved_t;
-  const int q = uni(S.q);
+  const int q = S.q;
   double z[QMAX + 1];
 #pragma unroll
   for (int j = 0; j <= QMAX; ++j) z[j] = b.zn[j];
@@ -863,7 +862,7 @@ __device__ __forceinline__ void bdf_restore(BB& b, BdfS& S, double saved_t) {
 
 template <class BB>
 __device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
-  const int q = uni(S.q);
+  const int q = S.q;
   double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = S.h;
   S.l[0] = S.l[1] = 1.0;
 #pragma unroll
@@ -894,7 +893,7 @@ __device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
   const double A2 = 1.0 + q * A1;
   S.tq[2] = fabs(A1 / (alpha0 * A2));
   S.tq[5] = fabs(A2 * xistar_inv / (lq * xi_inv));
-  if (uni(S.qwait) == 1) {
+  if (S.qwait == 1) {
     if (q > 1) {
       const double Cc = xistar_inv / lq;
       const double A3 = alpha0 + 1.0 / q;
@@ -914,14 +913,13 @@ __device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
   S.tq[4] = CORTES / S.tq[2];
   S.rl1 = 1.0 / S.l[1];
   S.gamma = S.h * S.rl1;
-  const int nst = uni(S.nst);
-  if (nst == 0) S.gammap = S.gamma;
-  S.gamrat = (nst > 0) ? S.gamma / S.gammap : 1.0;
+  if (S.nst == 0) S.gammap = S.gamma;
+  S.gamrat = (S.nst > 0) ? S.gamma / S.gammap : 1.0;
 }
 
 template <class BB>
 __device__ __forceinline__ void bdf_adjust_order(BB& b, BdfS& S, int deltaq) {
-  const int q = uni(S.q);
+  const int q = S.q;
 #pragma unroll
   for (int i = 0; i <= QMAX; ++i) S.l[i] = 0.0;
   S.l[2] = 1.0;
@@ -974,11 +972,10 @@ __device__ __forceinline__ void bdf_adjust_order(BB& b, BdfS& S, int deltaq) {
 template <class BB>
 __device__ __forceinline__ double dky0_lane(const BB& b, const BdfS& S, double t) {
   const double sc = (t - S.tn) / S.h;
-  const int q = uni(S.q);
   double v = 0.0;
 #pragma unroll
   for (int j = QMAX; j >= 0; --j)
-    if (j <= q) v = b.zn[j] + sc * v;
+    if (j <= S.q) v = b.zn[j] + sc * v;
   return v;
 }
 
