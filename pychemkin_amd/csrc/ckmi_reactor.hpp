@@ -813,8 +813,8 @@ __device__ __forceinline__ double wrms_lane(double v, double ewt, int n) {
   return sqrt(wave_sum(x * x) / n);
 }
 
-template <class BB>
-__device__ __forceinline__ void bdf_rescale(BB& b, BdfS& S) {
+template <class BB, class SS>
+__device__ __forceinline__ void bdf_rescale(BB& b, SS& S) {
   double factor = S.eta;
 #pragma unroll
   for (int j = 1; j <= QMAX; ++j) {
@@ -828,8 +828,8 @@ __device__ __forceinline__ void bdf_rescale(BB& b, BdfS& S) {
 }
 
 // zn_{j-1} += zn_j for k = 1..q, j = q..k (Pascal-triangle prediction), in registers
-template <class BB>
-__device__ __forceinline__ void bdf_predict(BB& b, BdfS& S) {
+template <class BB, class SS>
+__device__ __forceinline__ void bdf_predict(BB& b, SS& S) {
   S.tn += S.h;
   const int q = S.q;
   double z[QMAX + 1];
@@ -844,8 +844,8 @@ __device__ __forceinline__ void bdf_predict(BB& b, BdfS& S) {
   for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
-template <class BB>
-__device__ __forceinline__ void bdf_restore(BB& b, BdfS& S, double saved_t) {
+template <class BB, class SS>
+__device__ __forceinline__ void bdf_restore(BB& b, SS& S, double saved_t) {
   S.tn = saved_t;
   const int q = S.q;
   double z[QMAX + 1];
@@ -860,8 +860,8 @@ __device__ __forceinline__ void bdf_restore(BB& b, BdfS& S, double saved_t) {
   for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
-template <class BB>
-__device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
+template <class BB, class SS>
+__device__ __forceinline__ void bdf_set(BB& b, SS& S) {
   const int q = S.q;
   double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = S.h;
   S.l[0] = S.l[1] = 1.0;
@@ -881,14 +881,14 @@ __device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
     }
     alpha0 -= 1.0 / q;
     xistar_inv = -S.l[1] - alpha0;
-    hsum += pick(S.tau, q - 1);
+    hsum += S.tau[q - 1];
     xi_inv = S.h / hsum;
     alpha0_hat = -S.l[1] - xi_inv;
 #pragma unroll
     for (int i = QMAX; i >= 1; --i)
       if (i <= q) S.l[i] += S.l[i - 1] * xistar_inv;
   }
-  const double lq = pick(S.l, q);
+  const double lq = S.l[q];
   const double A1 = 1.0 - alpha0_hat + alpha0;
   const double A2 = 1.0 + q * A1;
   S.tq[2] = fabs(A1 / (alpha0 * A2));
@@ -903,7 +903,7 @@ __device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
     } else {
       S.tq[1] = 1.0;
     }
-    hsum += pick(S.tau, q);
+    hsum += S.tau[q];
     xi_inv = S.h / hsum;
     const double A5 = alpha0 - 1.0 / (q + 1);
     const double A6 = alpha0_hat - xi_inv;
@@ -917,8 +917,8 @@ __device__ __forceinline__ void bdf_set(BB& b, BdfS& S) {
   S.gamrat = (S.nst > 0) ? S.gamma / S.gammap : 1.0;
 }
 
-template <class BB>
-__device__ __forceinline__ void bdf_adjust_order(BB& b, BdfS& S, int deltaq) {
+template <class BB, class SS>
+__device__ __forceinline__ void bdf_adjust_order(BB& b, SS& S, int deltaq) {
   const int q = S.q;
 #pragma unroll
   for (int i = 0; i <= QMAX; ++i) S.l[i] = 0.0;
@@ -928,7 +928,7 @@ __device__ __forceinline__ void bdf_adjust_order(BB& b, BdfS& S, int deltaq) {
 #pragma unroll
     for (int j = 1; j < QMAX; ++j) {
       if (j < q) {
-        hsum += pick(S.tau, j + 1);
+        hsum += S.tau[j + 1];
         const double xi = hsum / S.hscale;
         prod *= xi;
         alpha0 -= 1.0 / (j + 1);
@@ -969,8 +969,8 @@ __device__ __forceinline__ void bdf_adjust_order(BB& b, BdfS& S, int deltaq) {
   }
 }
 
-template <class BB>
-__device__ __forceinline__ double dky0_lane(const BB& b, const BdfS& S, double t) {
+template <class BB, class SS>
+__device__ __forceinline__ double dky0_lane(const BB& b, const SS& S, double t) {
   const double sc = (t - S.tn) / S.h;
   double v = 0.0;
 #pragma unroll
