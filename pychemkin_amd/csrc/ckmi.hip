@@ -132,14 +132,8 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
   WaveLds L;
   L.base = ows;
   const int oS = ows + slice_vec_bytes(img.G);
-#ifdef CKMI_LANE_SCALARS  // A/B: the integrator scalars in lane-resident VGPRs (ckmi_run.hpp LaneFile)
-  LaneFile lfile{0.0, 0, opaque_lane(threadIdx.x % WAVE)};
-  BdfR S(lfile);
-  CtlR c(lfile);
-#else
   BdfS& S = *lds_at<BdfS>(oS);
   Ctl& c = *lds_at<Ctl>(oS + align16((int)sizeof(BdfS)));
-#endif
   Ign& g = *lds_at<Ign>(oS + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)));
   // the wave's parked Jacobian, rounded to FP32: M = I - gamma J is rebuilt from it at every
   // setup (5.6 per J); the modified Newton iteration only needs an approximate M, and half

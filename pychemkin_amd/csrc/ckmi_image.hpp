@@ -158,25 +158,6 @@ constexpr double E2T_INV_L = 92.332482616893656;
 constexpr double E2T_L_HI = 0x1.62e42fefa39efp-7;
 constexpr double E2T_L_LO = 0x1.abc9e3b39803fp-62;
 #endif
-#ifdef CKMI_FEXP_POLY
-// Table-free variant (A/B): x = k ln2 + r, |r| <= ln2/2, e^r - 1 = r + r^2 (c2 + ... + c13 r^11) with
-// the tail by Estrin; <= 1.04 ulp against long double exp over [-740, 709] (2e7 points).  No LDS read:
-// the strip's exp leaves its LDS round trip off the critical path at the cost of 8 more FMAs.
-__device__ __forceinline__ double fexp(double x, const double*) {
-  constexpr double INV_L = 1.4426950408889634, L_HI = 0x1.62e42fefa39efp-1, L_LO = 0x1.abc9e3b39803fp-56;
-  x = x < -1000.0 ? -1000.0 : (x > 1000.0 ? 1000.0 : x);
-  const double kd = __builtin_rint(x * INV_L);
-  const double r = fma(kd, -L_LO, fma(kd, -L_HI, x));
-  const int k = (int)kd;
-  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-  const double p23 = fma(r, 1.0 / 6.0, 0.5), p45 = fma(r, 1.0 / 120.0, 1.0 / 24.0),
-               p67 = fma(r, 1.0 / 5040.0, 1.0 / 720.0), p89 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0),
-               pab = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0), pcd = fma(r, 1.0 / 6227020800.0, 1.0 / 479001600.0);
-  const double q0 = fma(r2, p45, p23), q1 = fma(r2, p89, p67), q2 = fma(r2, pcd, pab);
-  const double tail = fma(r8, q2, fma(r4, q1, q0));
-  return ldexp(1.0 + fma(r2, tail, r), k);
-}
-#else
 __device__ __forceinline__ double fexp(double x, const double* e2t) {
   constexpr double INV_L = E2T_INV_L, L_HI = E2T_L_HI, L_LO = E2T_L_LO;
   x = x < -1000.0 ? -1000.0 : (x > 1000.0 ? 1000.0 : x);
@@ -188,7 +169,6 @@ __device__ __forceinline__ double fexp(double x, const double* e2t) {
   const double t = e2t[k & (E2T_N - 1)];
   return ldexp(fma(t, p, t), k >> E2T_SHIFT);
 }
-#endif
 
 // ------------------------------------------------------------------ NASA-7 (lane = species)
 struct Thermo7 {

@@ -276,6 +276,29 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
       if (first[k] < 0) first[k] = pos;
       last[k] = pos;
     }
+  // wdot accumulators in LDS instead of registers (round 4): each species gets an LDS column slot of
+  // the wave (slot * 64 + lane, so every lane updates its own column: conflict-free ds_add_f64, no
+  // read-modify-write wait) from its first to its last reaction -- interval colouring of the sliding
+  // window, 38 slots for GRI-3.0 (19.5 KB per wave).  The registers it frees are the ones the
+  // 2-wave allocation spilled to scratch (2.4x the algorithmic HBM traffic, round-3 verdict).  Used
+  // when the window fits 4 x wpe waves per CU in 160 KB of LDS; CKMI_JIT_WLDS=0/1 forces it (A/B).
+  std::vector<int> wslot(KK, -1);
+  int nslot = 0;
+  {
+    std::vector<int> free_slots;
+    for (int pos = 0; pos < II; ++pos) {
+      for (int k : used[order[pos]])
+        if (first[k] == pos) {
+          if (free_slots.empty()) free_slots.push_back(nslot++);
+          wslot[k] = free_slots.back();
+          free_slots.pop_back();
+        }
+      for (int k : used[order[pos]])
+        if (last[k] == pos) free_slots.push_back(wslot[k]);
+    }
+  }
+  bool wlds = nslot > 0 && (size_t)nslot * 64 * 8 * 4 * wpe <= 160 * 1024;
+  if (const char* e = std::getenv("CKMI_JIT_WLDS")) wlds = e[0] == '1' && nslot > 0;
   std::ostringstream o;
   o << "#define CKJ_RU " << lit(1.3806504e-16 * 6.02214179e23) << "\n";  // = ckmi_device.hpp RU
   o << kPrelude;
@@ -283,6 +306,7 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
     << "))) ckjit_rop_k" << KK << "_i" << II << "(int n, const double* __restrict__ Tv, "
        "const double* __restrict__ Pv, const double* __restrict__ Yv, double* __restrict__ wd, "
        "double* __restrict__ cpo, double* __restrict__ ho, const double* __restrict__ prm) {\n";
+  if (wlds) o << "  __shared__ double wl[" << nslot * 64 << "];\n";
   o << "  const int s0 = blockIdx.x * 64 + threadIdx.x;\n  const bool live = s0 < n;\n"
        "  const size_t s = live ? s0 : n - 1;\n  const size_t ns = n;\n";
   o << "  const double T = Tv[s], P = Pv[s];\n  const double lnT = log(T), invT = 1.0 / T;\n";
@@ -344,7 +368,9 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
   auto species = [&](int k) {
     const int b = TH + 15 * k;
     o << "  { // species " << k << "\n    const double y = Yl[" << k << " * ns + s] * prm[" << k << "];\n";
-    o << "    c" << k << " = rhoc * y;\n    w" << k << " = 0.0;\n";
+    o << "    c" << k << " = rhoc * y;\n";
+    if (!wlds) o << "    w" << k << " = 0.0;\n";
+    else if (wslot[k] >= 0) o << "    wl[" << wslot[k] * 64 << " + threadIdx.x] = 0.0;\n";
     o << "    const bool hi = T > prm[" << b << "];\n";
     for (int c = 0; c < 7; ++c)
       o << "    const double a" << c << " = hi ? prm[" << b + 8 + c << "] : prm[" << b + 1 + c << "];\n";
@@ -365,7 +391,11 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
     }
     o << "    cpm = fma(y, cpR, cpm);\n    hm = fma(y, hRT, hm);\n  }\n";
   };
-  auto retire = [&](int k) { o << "  if (live) wd[" << k << " * ns + s] = w" << k << ";\n"; };
+  auto retire = [&](int k) {
+    if (!wlds) o << "  if (live) wd[" << k << " * ns + s] = w" << k << ";\n";
+    else if (wslot[k] >= 0) o << "  if (live) wd[" << k << " * ns + s] = wl[" << wslot[k] * 64 << " + threadIdx.x];\n";
+    else o << "  if (live) wd[" << k << " * ns + s] = 0.0;\n";
+  };
   auto prod = [&](const std::vector<int>& v, const char* a) {
     std::string s;
     for (size_t j = 0; j < v.size(); ++j) s += (j ? " * " : "") + std::string(a) + std::to_string(v[j]);
@@ -582,6 +612,13 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
     }
     for (auto& kv : net) {
       if (kv.second == 0.0) continue;
+      if (wlds) {
+        const std::string a = "&wl[" + std::to_string(wslot[kv.first] * 64) + " + threadIdx.x]";
+        if (kv.second == 1.0) o << "    atomicAdd(" << a << ", q);\n";
+        else if (kv.second == -1.0) o << "    atomicAdd(" << a << ", -q);\n";
+        else o << "    atomicAdd(" << a << ", " << lit(kv.second) << " * q);\n";
+        continue;
+      }
       if (kv.second == 1.0) o << "    w" << kv.first << " += q;\n";
       else if (kv.second == -1.0) o << "    w" << kv.first << " -= q;\n";
       else o << "    w" << kv.first << " = fma(" << lit(kv.second) << ", q, w" << kv.first << ");\n";
@@ -615,8 +652,9 @@ int jit_rop_compile(const std::string& src, std::vector<char>& code, std::string
     log = "hiprtcCreateProgram failed";
     return 1;
   }
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+  // -munsafe-fp-atomics: the LDS accumulators' atomicAdd is the native ds_add_f64 (not a CAS loop)
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=fast", "-munsafe-fp-atomics"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 5, opts);
   size_t ls = 0;
   hiprtcGetProgramLogSize(prog, &ls);
   if (ls > 1) {

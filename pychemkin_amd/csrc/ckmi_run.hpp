@@ -98,93 +98,6 @@ struct Ctl {
   double st_h0, st_tout, st_h, is_hg, is_hub, is_hlb, is_t0;
 };
 
-// ------------------------------------------------------------------ lane-resident integrator scalars
-// The wave kernel keeps the integrator's wave-uniform scalars (BdfS and Ctl: 56 doubles, 34 ints) in
-// one double and one int VGPR per lane, field j in lane j: reading a field is a v_readlane into an
-// SGPR (a few cycles, usable as an operand at once), writing one a lane-select.  In LDS (round 1-3)
-// every read was a ds_read round trip behind the strip gathers and atomics of 11 other waves: the
-// bookkeeping between RHS calls took a third of a step.  The proxies below keep the member syntax of
-// BdfS / Ctl (S.h, S.l[i], c.mm++ ...), so the shared BDF helpers compile for either storage.
-struct LaneFile {
-  double d;  // lane j: double field j
-  int i;     // lane j: int field j
-  int lane;  // this lane's index
-};
-__device__ __forceinline__ double lf_get(double r, int j) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(r), j);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(r), j);
-  return __hiloint2double(hi, lo);
-}
-// write field j: the uniform value x into lane j (one compare, two selects)
-__device__ __forceinline__ double lf_set(double r, int lane, int j, double x) { return lane == j ? uni(x) : r; }
-struct PD {  // double field proxy
-  LaneFile& f;
-  int j;
-  __device__ __forceinline__ operator double() const { return lf_get(f.d, j); }
-  __device__ __forceinline__ PD& operator=(double x) {
-    f.d = lf_set(f.d, f.lane, j, x);
-    return *this;
-  }
-  __device__ __forceinline__ PD& operator=(const PD& o) { return *this = (double)o; }
-  __device__ __forceinline__ PD& operator+=(double x) { return *this = (double)*this + x; }
-  __device__ __forceinline__ PD& operator-=(double x) { return *this = (double)*this - x; }
-  __device__ __forceinline__ PD& operator*=(double x) { return *this = (double)*this * x; }
-  __device__ __forceinline__ PD& operator/=(double x) { return *this = (double)*this / x; }
-};
-struct PI {  // int field proxy
-  LaneFile& f;
-  int j;
-  __device__ __forceinline__ operator int() const { return __builtin_amdgcn_readlane(f.i, j); }
-  __device__ __forceinline__ PI& operator=(int x) {
-    f.i = f.lane == j ? __builtin_amdgcn_readfirstlane(x) : f.i;
-    return *this;
-  }
-  __device__ __forceinline__ PI& operator=(const PI& o) { return *this = (int)o; }
-  __device__ __forceinline__ PI& operator+=(int x) { return *this = (int)*this + x; }
-  __device__ __forceinline__ PI& operator-=(int x) { return *this = (int)*this - x; }
-  __device__ __forceinline__ PI& operator++() { return *this += 1; }
-  __device__ __forceinline__ int operator++(int) {
-    const int v = *this;
-    *this = v + 1;
-    return v;
-  }
-  __device__ __forceinline__ PI& operator--() { return *this -= 1; }
-  __device__ __forceinline__ int operator--(int) {
-    const int v = *this;
-    *this = v - 1;
-    return v;
-  }
-};
-template <int B>
-struct PDA {  // double array field at lanes B, B + 1, ...
-  LaneFile& f;
-  __device__ __forceinline__ PD operator[](int k) const { return PD{f, B + k}; }
-};
-// BdfS over the lane file (same member names)
-struct BdfR {
-  LaneFile& f;
-  PD h{f, 0}, hscale{f, 1}, hprime{f, 2}, eta{f, 3}, etamax{f, 4}, hmax_inv{f, 5}, hmin{f, 6}, tn{f, 7}, rl1{f, 8},
-      gamma{f, 9}, gammap{f, 10}, gamrat{f, 11}, crate{f, 12}, acnrm{f, 13}, saved_tq5{f, 14}, hu{f, 15};
-  PDA<16> l{f};   // [QMAX + 1]
-  PDA<22> tq{f};  // [6]
-  PDA<28> tau{f}; // [QMAX + 2]
-  PD rtol{f, 35}, atol{f, 36};
-  PI q{f, 0}, qprime{f, 1}, qwait{f, 2}, L{f, 3}, nst{f, 4}, nstlp{f, 5}, nstlj{f, 6}, jcur{f, 7}, ncf_tot{f, 8},
-      nef_tot{f, 9}, nlu{f, 10}, nfe{f, 11}, nje{f, 12}, nni{f, 13}, nneg{f, 14};
-  __device__ explicit BdfR(LaneFile& lf) : f(lf) {}
-};
-// Ctl over the lane file (same member names)
-struct CtlR {
-  LaneFile& f;
-  PI r{f, 15}, first{f, 16}, nflag{f, 17}, convfail{f, 18}, call_setup{f, 19}, failed{f, 20}, mm{f, 21}, ncf{f, 22},
-      nef{f, 23}, rc{f, 24}, isave{f, 25}, icrit{f, 26}, ncrit{f, 27}, status{f, 28}, nst{f, 29}, stopped{f, 30},
-      is_count{f, 31}, max_steps{f, 32}, nadap{f, 33};
-  PD avar_last{f, 37}, delp{f, 38}, saved_t{f, 39}, told{f, 40}, dsm{f, 41}, tc{f, 42}, tend{f, 43}, hmax{f, 44},
-      T0{f, 45}, yguard{f, 46}, tguard_lo{f, 47}, tguard_hi{f, 48}, st_h0{f, 49}, st_tout{f, 50}, st_h{f, 51},
-      is_hg{f, 52}, is_hub{f, 53}, is_hlb{f, 54}, is_t0{f, 55};
-  __device__ explicit CtlR(LaneFile& lf) : f(lf) {}
-};
-
 // Per-wave LDS slice: 6 species vectors, third-body sums, integrator scalars, control state,
 // ignition monitor.
 __host__ __device__ constexpr int align16(int b) { return (b + 15) & ~15; }
