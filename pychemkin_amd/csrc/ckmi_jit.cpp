@@ -276,12 +276,12 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
       if (first[k] < 0) first[k] = pos;
       last[k] = pos;
     }
-  // wdot accumulators in LDS instead of registers (round 4): each species gets an LDS column slot of
-  // the wave (slot * 64 + lane, so every lane updates its own column: conflict-free ds_add_f64, no
-  // read-modify-write wait) from its first to its last reaction -- interval colouring of the sliding
-  // window, 38 slots for GRI-3.0 (19.5 KB per wave).  The registers it frees are the ones the
-  // 2-wave allocation spilled to scratch (2.4x the algorithmic HBM traffic, round-3 verdict).  Used
-  // when the window fits 4 x wpe waves per CU in 160 KB of LDS; CKMI_JIT_WLDS=0/1 forces it (A/B).
+  // Opt-in (CKMI_JIT_WLDS=1, A/B only): the wdot accumulators in LDS instead of registers -- each
+  // species gets an LDS column slot of the wave (slot * 64 + lane: every lane updates its own column,
+  // conflict-free ds_add_f64, no read-modify-write wait) from its first to its last reaction, interval
+  // colouring of the sliding window (38 slots, 19.5 KB per wave for GRI-3.0).  It frees registers the
+  // 2-wave allocation spilled: HBM traffic per 10M-state launch 21.4 -> 17.2 GB, but 12.5 % SLOWER
+  // (874 -> 764 M states/s, profiles/r04f_ab_rop_wlds.log): the scratch traffic is not what bounds it.
   std::vector<int> wslot(KK, -1);
   int nslot = 0;
   {
@@ -297,8 +297,9 @@ bool jit_rop_generate(const ckmi_mech_desc* d, std::string& src, std::vector<dou
         if (last[k] == pos) free_slots.push_back(wslot[k]);
     }
   }
-  bool wlds = nslot > 0 && (size_t)nslot * 64 * 8 * 4 * wpe <= 160 * 1024;
-  if (const char* e = std::getenv("CKMI_JIT_WLDS")) wlds = e[0] == '1' && nslot > 0;
+  bool wlds = false;
+  if (const char* e = std::getenv("CKMI_JIT_WLDS"))
+    wlds = e[0] == '1' && nslot > 0 && (size_t)nslot * 64 * 8 * 4 * wpe <= 160 * 1024;
   std::ostringstream o;
   o << "#define CKJ_RU " << lit(1.3806504e-16 * 6.02214179e23) << "\n";  // = ckmi_device.hpp RU
   o << kPrelude;
