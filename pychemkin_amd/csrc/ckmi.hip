@@ -1367,17 +1367,19 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   const double dzero = 0.0;
   I.o_gsp = gsp.empty() ? put(&zero, 4) : put(gsp.data(), gsp.size() * 4);
   I.o_geff = geff.empty() ? put(&dzero, 8) : put(geff.data(), geff.size() * 8);
-  // dense efficiency rows: only the reactor kernel's CKMI_MG_DENSE variant reads them, and only for
-  // KK <= 63; larger mechanisms get a one-row stub so that the image fits in LDS (G x KKp grows fast)
-#ifdef CKMI_MG_DENSE
-  const bool dense = KK <= SP_ONE;
+  // transposed dense efficiency table geffT[k][17] (64 species rows, stride 17: conflict-free) for
+  // the wave kernel (CKMI_MG_SPARSE restores the sparse loop); only for KK <= 63 and G <= 16, else a stub
+#ifndef CKMI_MG_SPARSE
+  // ... and only while the 64-wide launch (12 waves) still fits the 160 KB of LDS with it
+  const size_t lds_with = blob.size() + 64 * 17 * 8 + 16 * E2T_N + jscratch_bytes<64>() + 12 * (size_t)slice_bytes(G);
+  const bool dense = KK <= SP_ONE && G <= 16 && lds_with <= 160 * 1024;
 #else
-  const bool dense = false;  // only the CKMI_MG_DENSE reactor variant reads the dense rows
+  const bool dense = false;
 #endif
-  std::vector<double> geffd(dense ? (size_t)std::max(G, 1) * KKp : (size_t)2, 0.0);
+  std::vector<double> geffd(dense ? (size_t)64 * 17 : (size_t)2, 0.0);
   for (int g = 0; dense && g < G; ++g)
-    for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)g * KKp + gsp[e]] = geff[e];
-  I.o_geffd = put(geffd.data(), geffd.size() * 8);
+    for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)gsp[e] * 17 + g] = geff[e];
+  I.o_geffd = put(geffd.data(), geffd.size() * 8);  // MechView::mgt() tells the two sizes apart
   {
     double e2t[E2T_N];  // 2^(j / E2T_N): E2T_N doubles fill the 64 LDS banks once (conflict-free gathers)
     for (int j = 0; j < E2T_N; ++j) e2t[j] = (double)std::exp2((long double)j / (long double)E2T_N);

@@ -75,6 +75,9 @@ struct MechView {
   __device__ __forceinline__ const double* geff() const { return lds_at<const double>(o_geff); }
   __device__ __forceinline__ const double* geffd() const { return lds_at<const double>(o_geffd); }
   __device__ __forceinline__ const double* e2t() const { return lds_at<const double>(o_e2t); }
+  // the transposed dense third-body table is present (64 x 17 doubles; a 2-double stub otherwise):
+  // told by its size, so that the view needs no extra field (every SGPR of it is live in the kernels)
+  __device__ __forceinline__ bool mgt() const { return o_e2t - o_geffd > 16; }
 };
 
 // view of an image staged at LDS byte offset `base`

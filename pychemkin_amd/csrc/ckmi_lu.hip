@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <utility>
 
 #include "../../include/ckmi.h"
 
@@ -42,6 +43,22 @@ constexpr bool LU_EXPT_NOSWAP = false;
 #endif
 
 typedef double d4 __attribute__((ext_vector_type(4)));
+
+#ifdef CKMI_LU_PHASE  // profiling build only: wave-0 cycles per factorisation step, summed over the launch
+__device__ unsigned long long g_lu_phase[12];
+#define LU_PH(k)                                                              \
+  do {                                                                        \
+    const unsigned long long t2_ = __builtin_amdgcn_s_memtime();              \
+    if (threadIdx.x == 0) ph_[k] += t2_ - t1_;                                \
+    t1_ = t2_;                                                                \
+  } while (0)
+#define LU_PHP , unsigned long long (&ph_)[12], unsigned long long& t1_
+#define LU_PHA , ph_, t1_
+#else
+#define LU_PH(k) (void)0
+#define LU_PHP
+#define LU_PHA
+#endif
 
 __device__ __forceinline__ d4 mfma16(double a, double b, d4 c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -87,15 +104,94 @@ struct LuSmem {
   double P[NP * PLD];                 // panel block column, indexed by global row
   double X[32 * NP];                  // row-exchange buffer, then the U12 block row [16][NP]
   double Linv[TB * PLD];
-  int src[32], dst[32];     // slot q < 32: row dst[q] receives the old row src[q]
-  int sslot[NP], dslot[NP]; // per row: the slot it is the source / destination of, or -1
+  int sslot[NP], dslot[NP]; // per row: the slot q < 32 it is the source / destination of, or -1
   int piv[TB];
   int info;
+#ifndef CKMI_LU_PANEL_LDS
+  double TS[((NB * NB + LU_WAVES - 1) / LU_WAVES) * 4 * WAVE];  // wave 0's tiles, parked during the panel
+#endif
 };
+
+// L11^-1 (unit lower) by forward substitution on the identity, right-looking over columns m of
+// L11: lane (i, g) holds X[i][g + 4k], k = 0..3; row m of X is lane m of each 16-lane row, brought
+// to the whole row by DPP row_newbcast (the step index is a compile-time constant), so a step is
+// 8 DPP moves and 4 FMAs instead of 4 LDS permutes
+template <int MM>
+__device__ __forceinline__ double dpp_row_bcast(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), 0x150 + MM, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), 0x150 + MM, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+template <int... MM>
+__device__ __forceinline__ void l11_steps(double (&x)[4], const double (&lm)[TB], std::integer_sequence<int, MM...>) {
+  (
+      [&] {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = fma(-lm[MM], dpp_row_bcast<MM>(x[k]), x[k]);
+      }(),
+      ...);
+}
+template <int NB>
+__device__ __forceinline__ void l11_inverse(LuSmem<NB>& S, int r0, int lane) {
+  constexpr int PLD = LuSmem<NB>::PLD;
+  const int i = lane & 15, g = lane >> 4;
+  double x[4], lm[TB];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = (i == g + 4 * k) ? 1.0 : 0.0;
+#pragma unroll
+  for (int mm = 0; mm < TB - 1; ++mm) lm[mm] = i > mm ? S.P[(r0 + i) * PLD + mm] : 0.0;
+  lm[TB - 1] = 0.0;
+  l11_steps(x, lm, std::make_integer_sequence<int, TB - 1>{});
+#pragma unroll
+  for (int k = 0; k < 4; ++k) S.Linv[i * PLD + g + 4 * k] = x[k];
+}
+
+// Step 2 tail: L11^-1 and the net row permutation of the panel's interchanges (wave 0).
+template <int NB>
+__device__ __forceinline__ void panel_finish(LuSmem<NB>& S, int K, int lane LU_PHP) {
+  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD;
+  const int r0 = K * TB;
+  l11_inverse<NB>(S, r0, lane);
+  LU_PH(9);
+  // Net row permutation of the 16 interchanges.  Lanes 0..15 track rows r0 + l, lanes 16..31 the
+  // pivot rows; each lane's `val` is the original row whose content its row holds now.
+  const int key = lane < TB ? r0 + lane : (lane < 2 * TB ? S.piv[lane - TB] : -1);
+  int val = key;
+#pragma unroll
+  for (int c = 0; c < TB; ++c) {
+    const int a = r0 + c, b = S.piv[c];
+    if (a != b) {
+      const uint64_t ma = __ballot(key == a), mb = __ballot(key == b);
+      const int va = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)ma) - 1);
+      const int vb = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)mb) - 1);
+      if (key == a) val = vb;
+      if (key == b) val = va;
+    }
+  }
+  // keep the first lane of each key whose row actually changed; slot = lane
+  bool rep = key >= 0 && val != key;
+#pragma unroll
+  for (int j = 0; j < 2 * TB; ++j) {
+    const int kj = __builtin_amdgcn_readlane(key, j);
+    if (j < lane && kj == key) rep = false;
+  }
+  // row -> slot tables: every tile lane then finds its rows' slots with independent LDS reads
+  // (no serial walk over the slots)
+  for (int i = lane; i < NP; i += WAVE) {
+    S.sslot[i] = -1;
+    S.dslot[i] = -1;
+  }
+  wave_lds_sync();
+  if (rep) {
+    S.sslot[val] = lane;
+    S.dslot[key] = lane;
+  }
+  LU_PH(10);
+}
 
 // Step 2: wave 0 factors panel K in LDS.  Rows K*16 .. NP-1, columns 0..15 of S.P.
 template <int NB>
-__device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int n) {
+__device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int n LU_PHP) {
   constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
   const int r0 = K * TB;
 #pragma unroll
@@ -152,59 +248,136 @@ __device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int
     }
     wave_lds_sync();
   }
-  // L11^-1 (unit lower) by forward substitution on the identity, right-looking over columns m
-  // of L11: lane (i, g) holds X[i][g + 4k], k = 0..3; row m is read from lane m + 16 g
-  {
-    const int i = lane & 15, g = lane >> 4;
-    double x[4];
+  panel_finish<NB>(S, K, lane LU_PHA);
+}
+
+// exact int min over the wave
+__device__ __forceinline__ int wave_min_i32(int v) {
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, false));
+  return min(min(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             min(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
+// Step 2, register form (default): wave 0 holds the panel rows in VGPRs for the 16 pivot steps
+// (lane l: rows r0 + l + 64 q at the start).  Rows are never moved: each carries its current
+// position pos (LAPACK's row index after the interchanges so far), an interchange swaps two
+// positions, and a row is finished once its position is below the current column.  So a pivot
+// step is a max reduction, a position swap, one broadcast of the pivot row through LDS and the
+// rank-1 update in registers; the rows go back to S.P at their final positions.  Wave 0 parks
+// its own matrix tiles in LDS around the call (kernel register budget: 2 waves per SIMD).
+// Same arithmetic, pivots (first position of maximal |a|) and factors as panel_factor.
+template <int NB>
+__device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, int K, int lane, int n LU_PHP) {
+  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
+  constexpr int NOPOS = 1 << 30;
+  const int r0 = K * TB;
+  double x[NQ][TB];
+  int pos[NQ];  // current position, or -1 (no row: beyond NP)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = (i == g + 4 * k) ? 1.0 : 0.0;
-#pragma unroll 1
-    for (int mm = 0; mm < TB - 1; ++mm) {
-      const double lm = i > mm ? S.P[(r0 + i) * PLD + mm] : 0.0;
+  for (int q = 0; q < NQ; ++q) {
+    const int r = r0 + lane + WAVE * q;
+    pos[q] = r < NP ? r : -1;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = fma(-lm, __shfl(x[k], mm + 16 * g), x[k]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) S.Linv[i * PLD + g + 4 * k] = x[k];
+    for (int c = 0; c < TB; ++c) x[q][c] = r < NP ? S.P[r * PLD + c] : 0.0;
   }
-  // Net row permutation of the 16 interchanges.  Lanes 0..15 track rows r0 + l, lanes 16..31 the
-  // pivot rows; each lane's `val` is the original row whose content its row holds now.
-  const int key = lane < TB ? r0 + lane : (lane < 2 * TB ? S.piv[lane - TB] : -1);
-  int val = key;
+  double* sb = S.X;  // the pivot row
+  LU_PH(7);
 #pragma unroll
   for (int c = 0; c < TB; ++c) {
-    const int a = r0 + c, b = S.piv[c];
-    if (a != b) {
-      const uint64_t ma = __ballot(key == a), mb = __ballot(key == b);
-      const int va = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)ma) - 1);
-      const int vb = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)mb) - 1);
-      if (key == a) val = vb;
-      if (key == b) val = va;
+    const int col = r0 + c;
+    // this lane's best active row: largest |a|, then the smallest position; its reciprocal is
+    // taken now, beside the wave reduction, instead of after the pivot row arrives
+    double best = -1.0, bval = 1.0;
+    int bpos = NOPOS;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const double v = pos[q] >= col ? fabs(x[q][c]) : -1.0;
+      const bool take = v > best || (v == best && pos[q] < bpos);
+      best = take ? v : best;
+      bval = take ? x[q][c] : bval;
+      bpos = take ? pos[q] : bpos;
+    }
+    const double rb = 1.0 / bval;
+    const double maxv = wave_max(best);
+    uint64_t cand = __ballot(best == maxv);
+    int p = __builtin_amdgcn_readlane(bpos, (int)__ffsll((unsigned long long)cand) - 1);
+    if (__builtin_popcountll(cand) > 1) {  // ties: the first position
+      p = __builtin_amdgcn_readfirstlane(wave_min_i32(best == maxv ? bpos : NOPOS));
+      cand = __ballot(best == maxv && bpos == p);
+    }
+    p = __builtin_amdgcn_readfirstlane(p);
+    if (lane == 0) S.piv[c] = p;
+    if (maxv != 0.0) {
+      const double rp = bcast(rb, (int)__ffsll((unsigned long long)cand) - 1);
+      // the pivot row (position p) to LDS; then it takes position col and the row at col takes p.
+      // No wave barrier around sb: one wave's LDS operations execute in issue order, so the
+      // reads below see this store and the next column's store follows these reads.  The empty
+      // asm with a memory clobber keeps the compiler from hoisting the reads above the store
+      // (per thread, a load after a conditional store may legally become load + select).
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if (pos[q] == p) {
+#pragma unroll
+          for (int cc = 0; cc < TB; ++cc)
+            if (cc > c) sb[cc] = x[q][cc];
+        }
+      }
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) pos[q] = pos[q] == p ? col : (pos[q] == col ? p : pos[q]);
+      double prow[TB];
+#pragma unroll
+      for (int cc = 0; cc < TB; ++cc) prow[cc] = cc > c ? sb[cc] : 0.0;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        if (pos[q] > col) {
+          const double l = x[q][c] * rp;
+          x[q][c] = l;
+#pragma unroll
+          for (int cc = 0; cc < TB; ++cc)  // (a constant trip count: unrolled before the c loop is)
+            if (cc > c) x[q][cc] = fma(-l, prow[cc], x[q][cc]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) pos[q] = pos[q] == p ? col : (pos[q] == col ? p : pos[q]);
+      if (lane == 0 && S.info == 0 && col < n) S.info = col + 1;  // LAPACK: U(col, col) is exactly zero
     }
   }
-  // keep the first lane of each key whose row actually changed; slot = lane
-  bool rep = key >= 0 && val != key;
+  LU_PH(8);
+  // rows back to S.P at their final positions; the net permutation is read off the positions:
+  // the content of row r0 + l + 64 q moved to pos[q] (at most 32 rows move), slots by prefix count
 #pragma unroll
-  for (int j = 0; j < 2 * TB; ++j) {
-    const int kj = __builtin_amdgcn_readlane(key, j);
-    if (j < lane && kj == key) rep = false;
+  for (int q = 0; q < NQ; ++q) {
+    if (pos[q] >= 0) {
+#pragma unroll
+      for (int c = 0; c < TB; ++c) S.P[pos[q] * PLD + c] = x[q][c];
+    }
   }
-  if (lane < 2 * TB) {
-    S.dst[lane] = key;
-    S.src[lane] = val;
-  }
-  // row -> slot tables: every tile lane then finds its rows' slots with independent LDS reads
-  // (no serial walk over the slots)
   for (int i = lane; i < NP; i += WAVE) {
     S.sslot[i] = -1;
     S.dslot[i] = -1;
   }
-  wave_lds_sync();
-  if (rep) {
-    S.sslot[val] = lane;
-    S.dslot[key] = lane;
+  int base = 0;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int r = r0 + lane + WAVE * q;
+    const bool moved = pos[q] >= 0 && pos[q] != r;
+    const uint64_t m = __ballot(moved);
+    const int sl = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (moved) {  // (after the -1 fill: same wave, LDS order)
+      S.sslot[r] = sl;
+      S.dslot[pos[q]] = sl;
+    }
+    base += __builtin_popcountll(m);
   }
+  wave_lds_sync();
+  LU_PH(10);
+  l11_inverse<NB>(S, r0, lane);
+  LU_PH(9);
 }
 
 template <int NB>
@@ -216,6 +389,9 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
   const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lc0 = lane & 15, lg0 = lane >> 4;
 
+#ifdef CKMI_LU_PHASE
+  unsigned long long ph_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t1_ = __builtin_amdgcn_s_memtime();
+#endif
   for (int sys = blockIdx.x; sys < nsys; sys += gridDim.x) {
     double* As = A + (size_t)sys * n * n;
     d4 t[NT];
@@ -239,6 +415,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       }
     }
     if (threadIdx.x == 0) S.info = 0;
+    LU_PH(0);
 
     for (int K = 0; K < NB; ++K) {
       // laundered per panel: keeps the per-tile indices and LDS addresses from being hoisted
@@ -256,9 +433,26 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         }
       }
       __syncthreads();
+      LU_PH(1);
       // 2. factor the panel
-      if (w == 0) panel_factor<NB>(S, K, lane, n);
+#ifdef CKMI_LU_PANEL_LDS
+      if (w == 0) panel_factor<NB>(S, K, lane, n LU_PHA);
+#else
+      if (w == 0) {
+        // park the tiles: the panel's 48 doubles per lane take their registers meanwhile
+#pragma unroll
+        for (int s = 0; s < NT; ++s)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S.TS[(4 * s + r) * WAVE + lane] = t[s][r];
+        panel_factor_reg<NB>(S, K, lane, n LU_PHA);
+#pragma unroll
+        for (int s = 0; s < NT; ++s)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t[s][r] = S.TS[(4 * s + r) * WAVE + lane];
+      }
+#endif
       __syncthreads();
+      LU_PH(2);
       // 3. row interchanges in the other block columns (sources out), factored panel back in
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
@@ -289,6 +483,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         }
       }
       __syncthreads();
+      LU_PH(3);
       // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (X reused as [16][NP])
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
@@ -304,6 +499,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         }
       }
       __syncthreads();
+      LU_PH(4);
       // 5. trailing update A22 -= L21 U12
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
@@ -317,6 +513,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       }
       if (threadIdx.x < TB && K * TB + threadIdx.x < n) ipiv[(size_t)sys * n + K * TB + threadIdx.x] = S.piv[threadIdx.x];
       __syncthreads();  // P, X and piv are rewritten by the next panel
+      LU_PH(5);
     }
     // opaque copies: otherwise the 4 NT store addresses are CSE'd with the load addresses and
     // held in VGPRs through the whole factorisation
@@ -336,7 +533,12 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
     }
     if (threadIdx.x == 0) info[sys] = S.info;
     __syncthreads();  // S.info
+    LU_PH(6);
   }
+#ifdef CKMI_LU_PHASE
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 12; ++k) atomicAdd(&g_lu_phase[k], ph_[k]);
+#endif
 }
 
 // One wave per right-hand side: x = U^-1 L^-1 P b, in place in B[sys][n].
@@ -397,6 +599,17 @@ const factor_fn kFactor[LU_NB_MAX] = {launch_factor<1>, launch_factor<2>, launch
 }  // namespace
 
 extern "C" {
+
+#ifdef CKMI_LU_PHASE
+int ckmi_lu_phase_get(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_lu_phase), sizeof(unsigned long long) * 12) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lu_phase), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 const char* ckmi_lu_last_error(void) { return g_lu_err.c_str(); }
 

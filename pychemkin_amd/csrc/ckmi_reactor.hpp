@@ -300,6 +300,11 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
     L.gRT()[SP_ONE] = 0.0;
     L.hRT()[SP_ONE] = 0.0;
   }
+#ifndef CKMI_MG_SPARSE
+  else if (lane > KK) {
+    C[lane - 1] = 0.0;  // C[KK..62] = 0: the transposed third-body table reads whole 16-row quarters
+  }
+#endif
   const double Ctot = rho * sumYW;  // = sum_k C_k, without a second reduction
   double* Jsh = lds_at<double>(oJ);
   if (with_j) {
@@ -307,19 +312,31 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   }
   wave_lds_sync();
   // third-body concentrations [M]_g = Ctot + sum_k (eff_gk - 1) C_k, lane g
-#ifdef CKMI_MG_DENSE
-  for (int g = lane; g < V.G; g += WAVE) {
-    const double* e = V.geffd() + g * V.KKp;
-    double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
-    int k = 0;
-    for (; k + 4 <= KK; k += 4) {
-      m0 = fma(e[k], C[k], m0);
-      m1 = fma(e[k + 1], C[k + 1], m1);
-      m2 = fma(e[k + 2], C[k + 2], m2);
-      m3 = fma(e[k + 3], C[k + 3], m3);
+#ifndef CKMI_MG_SPARSE
+  if (V.mgt()) {
+    // transposed dense table geffT[k][17] (zero rows k >= KK): lane = g + 16 q sums the species
+    // quarter q, the four partials meet in the ek() scratch row (written later, in the Jacobian pass)
+    const int g = lane & 15, q = lane >> 4;
+    const double* e = V.geffd() + (16 * q) * 17 + g;
+    const double* c = C + 16 * q;
+    double m0 = 0.0, m1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+      m0 = fma(e[i * 17], c[i], m0);
+      m1 = fma(e[(i + 1) * 17], c[i + 1], m1);
     }
-    for (; k < KK; ++k) m0 = fma(e[k], C[k], m0);
-    L.Mg()[g] = Ctot + ((m0 + m1) + (m2 + m3));
+    L.ek()[lane] = m0 + m1;
+    wave_lds_sync();
+    if (lane < V.G) {
+      const double* p = L.ek() + lane;
+      L.Mg()[lane] = Ctot + ((p[0] + p[16]) + (p[32] + p[48]));
+    }
+  } else {
+    for (int g = lane; g < V.G; g += WAVE) {
+      double m = Ctot;
+      for (int p = V.gptr()[g]; p < V.gptr()[g + 1]; ++p) m += V.geff()[p] * C[V.gsp()[p]];
+      L.Mg()[g] = m;
+    }
   }
 #else
   for (int g = lane; g < V.G; g += WAVE) {
