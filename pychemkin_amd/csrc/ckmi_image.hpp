@@ -206,15 +206,18 @@ struct Rxn {
 // Troe / SRI falloff, reverse rates from equilibrium or explicit REV parameters).
 // PLOG = false compiles the mechanism-without-PLOG kernels exactly as before PLOG existed (the
 // PLOG branch costs 2-4 % of rate throughput in register allocation even when never taken).
-template <bool PLOG = false>
+// PRE: the Arrhenius parameters come in as pA (lnA, beta, Ea), loaded ahead by the caller.
+template <bool PLOG = false, bool PRE = false>
 __device__ __forceinline__ Rxn eval_rxn_img(const MechView& V, int i, uint32_t inf, uint32_t rs, uint32_t ps,
                                             uint32_t nuw, double T, double lnT, double invT, double lnPRT, double P,
                                             const double* C, const double* gRT, const double* hRT, const double* Mg,
-                                            bool need_h, int pslot = -1, double plnf = 0.0, double gfac = 1.0) {
+                                            bool need_h, int pslot = -1, double plnf = 0.0, double gfac = 1.0,
+                                            const double* pA = nullptr) {
   constexpr double INV_LN10 = 0.43429448190325176;
   const int type = rx_type(inf);
   // pslot / plnf: per-reactor A-factor perturbation (brute-force sensitivity)
-  const double lnA = V.lnA()[i] + (i == pslot ? plnf : 0.0), b = V.beta()[i], Ea = V.Ea()[i];
+  const double lnA = (PRE ? pA[0] : V.lnA()[i]) + (i == pslot ? plnf : 0.0);
+  const double b = PRE ? pA[1] : V.beta()[i], Ea = PRE ? pA[2] : V.Ea()[i];
   double lnkinf = lnA + b * lnT - Ea * invT;
   double dlkf = (b + Ea * invT) * invT;
   double t13 = 0.0, t23 = 0.0;  // Landau-Teller T^(-1/3), T^(-2/3)

@@ -348,9 +348,30 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
   wave_lds_sync();
   SUB_PHASE(0);
   const int IIp = V.IIp;
+#ifdef CKMI_STRIP_PF
+  // the next strip's reaction record is loaded before this strip's work (the loads cannot move
+  // above this strip's LDS atomics on their own: the image and the accumulators may alias)
+  uint32_t inf_n = V.info()[lane], rs_n = V.rsp()[lane], ps_n = V.psp()[lane], nu_n = V.nu()[lane];
+  double pa_n[3] = {V.lnA()[lane], V.beta()[lane], V.Ea()[lane]};
+#endif
   for (int base = 0; base < IIp; base += WAVE) {
     const int i = base + lane;
+#ifdef CKMI_STRIP_PF
+    const uint32_t inf = inf_n, rs_c = rs_n, ps_c = ps_n, nu_c = nu_n;
+    const double pa[3] = {pa_n[0], pa_n[1], pa_n[2]};
+    if (base + WAVE < IIp) {
+      const int j = i + WAVE;
+      inf_n = V.info()[j];
+      rs_n = V.rsp()[j];
+      ps_n = V.psp()[j];
+      nu_n = V.nu()[j];
+      pa_n[0] = V.lnA()[j];
+      pa_n[1] = V.beta()[j];
+      pa_n[2] = V.Ea()[j];
+    }
+#else
     const uint32_t inf = V.info()[i];
+#endif
     const int nr = rx_nr(inf), np = rx_np(inf);
     if constexpr (PL) {
       if (inf & RX_GEN) {  // FORD / RORD / non-integral coefficients: real nu and orders
@@ -366,9 +387,15 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
       }
     }
     if (nr + np != 0) {
+#ifdef CKMI_STRIP_PF
+      const uint32_t rs = rs_c, ps = ps_c, nuw = nu_c;
+      const Rxn e = eval_rxn_img<PL, true>(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(),
+                                       false, R.pslot, R.plnf, R.gfac, pa);
+#else
       const uint32_t rs = V.rsp()[i], ps = V.psp()[i], nuw = V.nu()[i];
       const Rxn e = eval_rxn_img<PL>(V, i, inf, rs, ps, nuw, T, lnT, invT, lnPRT, P, C, L.gRT(), L.hRT(), L.Mg(), false,
                                  R.pslot, R.plnf, R.gfac);
+#endif
       const double q = e.mfac * (e.kf * e.pf - e.kr * e.pr);
 #ifdef CKMI_EXPT_NOATOM  // timing experiment only: plain stores instead of LDS atomics (wrong wdot)
 #pragma unroll
