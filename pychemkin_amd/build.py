@@ -77,9 +77,12 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     lu_obj = os.path.join(OBJ_DIR, "ckmi_lu.o")
     if force or _stale(lu_obj, [LU_SRC, DEPS[-1]]):
         jobs.append((LU_SRC, lu_obj, LU_FLAGS))
-    big_obj = os.path.join(OBJ_DIR, "ckmi_big.o" if default else f"ckmi_big_{'prof' if prof else 'main'}.o")
-    if force or _stale(big_obj, [BIG_SRC] + DEPS):
-        jobs.append((BIG_SRC, big_obj, BIG_FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else [])))
+    # variant flags naming the workgroup kernel (-DCKMI_BIG_...) also build a variant of ckmi_big.hip
+    big_extra = [f for f in extra if "CKMI_BIG" in f]
+    big_tag = "prof" if prof else ("main" if not big_extra else "v_" + os.path.splitext(os.path.basename(out))[0])
+    big_obj = os.path.join(OBJ_DIR, "ckmi_big.o" if default else f"ckmi_big_{big_tag}.o")
+    if force or big_extra or _stale(big_obj, [BIG_SRC] + DEPS):
+        jobs.append((BIG_SRC, big_obj, BIG_FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + big_extra))
     kin_obj = os.path.join(OBJ_DIR, "ckmi_kin.o")
     if force or _stale(kin_obj, [KIN_SRC] + DEPS):
         jobs.append((KIN_SRC, kin_obj, KIN_FLAGS))

@@ -1,6 +1,6 @@
 """A/B timing of libckmi variants on the same GPU (alternating processes, same workload).
 
-    python scripts/ab_bench.py pychemkin_amd/_lib/libA.so pychemkin_amd/_lib/libB.so [--reps 3] [--n 16384] [--rop]
+    python scripts/ab_bench.py pychemkin_amd/_lib/libA.so pychemkin_amd/_lib/libB.so [--reps 3] [--n 16384] [--rop | --c5]
 
 Each rep runs every library in its own process (CKMI_LIB=...) on a strided subsample of the
 bench sweep and reports the kernel time from HIP events; prints the per-library median.
@@ -23,9 +23,10 @@ for _k in [k for k in _native.PROTOTYPES if not hasattr(_L, k)]:
     _native.PROTOTYPES.pop(_k)
 _native.ABI_VERSION = _L.ckmi_version()  # an A/B may time an older build of the same reactor entry points
 n = %d
-mech = bench.mechanism()
+c5 = %r
+mech = bench.big_mechanism() if c5 else bench.mechanism()
 dm = _native.DeviceMechanism(mech.to_tables(), device=0)
-T0, P0, Y0, _ = bench.sweep(mech, 1, 0)
+T0, P0, Y0, prob = bench.sweep_c5(mech, 1, 0) if c5 else bench.sweep(mech, 1, 0)
 idx = np.arange(0, len(T0), max(1, len(T0) // n))[:n]
 args = (np.ones(len(idx), np.int32), T0[idx], P0[idx], np.ones(len(idx)), Y0[idx])
 cfg = _native.make_cfg(**bench.RUN)
@@ -76,15 +77,16 @@ def main():
     libs = [a for a in sys.argv[1:] if a.split("@")[0].endswith(".so")]
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
     rop = "--rop" in sys.argv
-    n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else (4_000_000 if rop else 16384)
+    c5 = "--c5" in sys.argv  # configs[4]: the workgroup-per-reactor kernel on the 161-species stand-in
+    n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else (4_000_000 if rop else (2048 if c5 else 16384))
     out = {lib: [] for lib in libs}
     for _ in range(reps):
         for lib in libs:
             path, *sets = lib.split("@")
             env = dict(os.environ, CKMI_LIB=os.path.abspath(path),
-                       AB_TAU_REF=os.path.join(ROOT, "gpurun_out", "ab_tau_%s.npy" % os.path.basename(libs[0].split("@")[0])))
+                       AB_TAU_REF=os.path.join(ROOT, "gpurun_out", "ab_tau_%s%s.npy" % ("c5_" if c5 else "", os.path.basename(libs[0].split("@")[0]))))
             env.update(kv.split("=", 1) for kv in sets)
-            r = subprocess.run([sys.executable, "-c", (ROP_CHILD if rop else CHILD) % (ROOT, n)], env=env, capture_output=True, text=True,
+            r = subprocess.run([sys.executable, "-c", (ROP_CHILD % (ROOT, n) if rop else CHILD % (ROOT, n, c5))], env=env, capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
                 print(r.stderr[-2000:], file=sys.stderr)
