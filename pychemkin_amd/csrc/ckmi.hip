@@ -715,10 +715,11 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
           {  // runaway guard on the accepted state: a mass fraction far below 0, or T off the thermo range
              // (energy runs); it ends the reactor through ST_STEP_END's failure exit
+            // (one ballot, not a max reduction: only "any lane beyond the guard" matters)
             const double z0 = b.zn[0];
-            double v = isp ? -z0 : -1.0;
-            if (lane == 0 && R.energy == 1 && !(z0 >= c.tguard_lo && z0 <= c.tguard_hi)) v = 1e300;
-            c.rc = wave_max(v) > c.yguard ? CKMI_RUN_RUNAWAY : 0;
+            const bool bad = isp ? -z0 > c.yguard
+                                 : (lane == 0 && R.energy == 1 && !(z0 >= c.tguard_lo && z0 <= c.tguard_hi));
+            c.rc = __ballot(bad) != 0 ? CKMI_RUN_RUNAWAY : 0;
           }
           st = ST_STEP_END;
           break;
