@@ -107,8 +107,12 @@ struct LuSmem {
   int sslot[NP], dslot[NP]; // per row: the slot q < 32 it is the source / destination of, or -1
   int piv[TB];
   int info;
-#ifndef CKMI_LU_PANEL_LDS
+#if !defined(CKMI_LU_PANEL_LDS) && !defined(CKMI_LU_LOOKAHEAD)
   double TS[((NB * NB + LU_WAVES - 1) / LU_WAVES) * 4 * WAVE];  // wave 0's tiles, parked during the panel
+#endif
+#ifdef CKMI_LU_LOOKAHEAD
+  double P2[NP * PLD];  // the next panel (look-ahead), alternating with P
+  double SB[TB];        // the pivot row of a panel step
 #endif
 };
 
@@ -132,14 +136,14 @@ __device__ __forceinline__ void l11_steps(double (&x)[4], const double (&lm)[TB]
       ...);
 }
 template <int NB>
-__device__ __forceinline__ void l11_inverse(LuSmem<NB>& S, int r0, int lane) {
+__device__ __forceinline__ void l11_inverse(LuSmem<NB>& S, const double* Pp, int r0, int lane) {
   constexpr int PLD = LuSmem<NB>::PLD;
   const int i = lane & 15, g = lane >> 4;
   double x[4], lm[TB];
 #pragma unroll
   for (int k = 0; k < 4; ++k) x[k] = (i == g + 4 * k) ? 1.0 : 0.0;
 #pragma unroll
-  for (int mm = 0; mm < TB - 1; ++mm) lm[mm] = i > mm ? S.P[(r0 + i) * PLD + mm] : 0.0;
+  for (int mm = 0; mm < TB - 1; ++mm) lm[mm] = i > mm ? Pp[(r0 + i) * PLD + mm] : 0.0;
   lm[TB - 1] = 0.0;
   l11_steps(x, lm, std::make_integer_sequence<int, TB - 1>{});
 #pragma unroll
@@ -151,7 +155,7 @@ template <int NB>
 __device__ __forceinline__ void panel_finish(LuSmem<NB>& S, int K, int lane LU_PHP) {
   constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD;
   const int r0 = K * TB;
-  l11_inverse<NB>(S, r0, lane);
+  l11_inverse<NB>(S, S.P, r0, lane);
   LU_PH(9);
   // Net row permutation of the 16 interchanges.  Lanes 0..15 track rows r0 + l, lanes 16..31 the
   // pivot rows; each lane's `val` is the original row whose content its row holds now.
@@ -270,7 +274,7 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 // its own matrix tiles in LDS around the call (kernel register budget: 2 waves per SIMD).
 // Same arithmetic, pivots (first position of maximal |a|) and factors as panel_factor.
 template <int NB>
-__device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, int K, int lane, int n LU_PHP) {
+__device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, double* sb, int K, int lane, int n LU_PHP) {
   constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
   constexpr int NOPOS = 1 << 30;
   const int r0 = K * TB;
@@ -281,9 +285,8 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, int K, int lane,
     const int r = r0 + lane + WAVE * q;
     pos[q] = r < NP ? r : -1;
 #pragma unroll
-    for (int c = 0; c < TB; ++c) x[q][c] = r < NP ? S.P[r * PLD + c] : 0.0;
+    for (int c = 0; c < TB; ++c) x[q][c] = r < NP ? Pp[r * PLD + c] : 0.0;
   }
-  double* sb = S.X;  // the pivot row
   LU_PH(7);
 #pragma unroll
   for (int c = 0; c < TB; ++c) {
@@ -354,7 +357,7 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, int K, int lane,
   for (int q = 0; q < NQ; ++q) {
     if (pos[q] >= 0) {
 #pragma unroll
-      for (int c = 0; c < TB; ++c) S.P[pos[q] * PLD + c] = x[q][c];
+      for (int c = 0; c < TB; ++c) Pp[pos[q] * PLD + c] = x[q][c];
     }
   }
   for (int i = lane; i < NP; i += WAVE) {
@@ -376,7 +379,7 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, int K, int lane,
   }
   wave_lds_sync();
   LU_PH(10);
-  l11_inverse<NB>(S, r0, lane);
+  l11_inverse<NB>(S, Pp, r0, lane);
   LU_PH(9);
 }
 
@@ -444,7 +447,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         for (int s = 0; s < NT; ++s)
 #pragma unroll
           for (int r = 0; r < 4; ++r) S.TS[(4 * s + r) * WAVE + lane] = t[s][r];
-        panel_factor_reg<NB>(S, K, lane, n LU_PHA);
+        panel_factor_reg<NB>(S, S.P, S.X, K, lane, n LU_PHA);
 #pragma unroll
         for (int s = 0; s < NT; ++s)
 #pragma unroll
@@ -453,7 +456,52 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
 #endif
       __syncthreads();
       LU_PH(2);
-      // 3. row interchanges in the other block columns (sources out), factored panel back in
+      // 3. row interchanges in the other block columns (sources out), factored panel back in.
+      // The slot numbers of all of this wave's rows are loaded first, unconditionally (straight-line
+      // LDS reads, one wait), so the lane-masked moves below do not wait on one lookup at a time.
+#ifndef CKMI_LU_XCHG_SERIAL
+      {
+        int qs[NT][4];
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w + LU_WAVES * s;
+          const int I = min(ti / NB, NB - 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qs[s][r] = S.sslot[I * TB + lg + 4 * r];
+        }
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w + LU_WAVES * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (qs[s][r] >= 0) S.X[qs[s][r] * NP + J * TB + lc] = t[s][r];
+          } else if (ti < NB * NB && J == K && I >= K) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[s][r] = S.P[(I * TB + lg + 4 * r) * PLD + lc];
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w + LU_WAVES * s;
+          const int I = min(ti / NB, NB - 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) qs[s][r] = S.dslot[I * TB + lg + 4 * r];
+        }
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w + LU_WAVES * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (qs[s][r] >= 0) t[s][r] = S.X[qs[s][r] * NP + J * TB + lc];
+          }
+        }
+      }
+#else
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
         const int ti = w + LU_WAVES * s;
@@ -482,6 +530,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           }
         }
       }
+#endif
       __syncthreads();
       LU_PH(3);
       // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (X reused as [16][NP])
@@ -541,6 +590,188 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
 #endif
 }
 
+#ifdef CKMI_LU_LOOKAHEAD
+// Look-ahead form: wave 0 owns no tiles and only factors panels; waves 1..7 own the 121 tiles
+// (tile ti = (w - 1) + 7 s).  Per panel K, with panel K already factored into P[K & 1]:
+//   (a) interchanges of panel K on the tile rows (and the panel column's tiles read back);
+//   (b) U12 = L11^-1 A12 on block row K;
+//   (c) the trailing update of block column K + 1 only, whose tiles then go to P[(K + 1) & 1];
+//   (d) wave 0 factors panel K + 1 while waves 1..7 finish the trailing update of columns > K + 1.
+// So the panel of step K + 1 (wave 0, one SIMD) overlaps the MFMA update of step K instead of
+// following it.  Same arithmetic per element as lu_factor_kernel: bitwise the same factors.
+template <int NB>
+__global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel_la(int nsys, int n, double* __restrict__ A,
+                                                                      int* __restrict__ ipiv, int* __restrict__ info) {
+  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, TW = LU_WAVES - 1, NT = (NB * NB + TW - 1) / TW;
+  __shared__ LuSmem<NB> S;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const int lc0 = lane & 15, lg0 = lane >> 4;
+#ifdef CKMI_LU_PHASE
+  unsigned long long ph_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t1_ = __builtin_amdgcn_s_memtime();
+#endif
+  for (int sys = blockIdx.x; sys < nsys; sys += gridDim.x) {
+    double* As = A + (size_t)sys * n * n;
+    d4 t[NT];
+    {
+      int w = w0, lc = lc0, lg = lg0, nl = n;
+      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg), "+s"(nl));
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w - 1 + TW * s;
+        const int I = ti / NB, J = ti % NB;
+        const int col = J * TB + lc;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = I * TB + lg + 4 * r;
+          double v = row == col ? 1.0 : 0.0;
+          if (w > 0 && ti < NB * NB && row < nl && col < nl) v = As[(size_t)row * nl + col];
+          t[s][r] = v;
+        }
+      }
+      // panel 0 to P
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w - 1 + TW * s;
+        if (w > 0 && ti < NB * NB && ti % NB == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) S.P[((ti / NB) * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+        }
+      }
+    }
+    if (threadIdx.x == 0) S.info = 0;
+    __syncthreads();
+    if (w0 == 0) {
+      panel_factor_reg<NB>(S, S.P, S.SB, 0, lane, n LU_PHA);
+#pragma unroll
+      for (int s = 0; s < NT; ++s) t[s] = d4{0.0, 0.0, 0.0, 0.0};  // wave 0 holds no tiles
+    }
+    __syncthreads();
+    LU_PH(0);
+    for (int K = 0; K < NB; ++K) {
+      int w = w0, lc = lc0, lg = lg0;
+      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg));
+      double* Pc = (K & 1) ? S.P2 : S.P;
+      double* Pn = (K & 1) ? S.P : S.P2;
+      // (a) interchanges of panel K; the panel column's tiles take their factored values
+      if (w > 0) {
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w - 1 + TW * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && J != K && I >= K) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int q = S.sslot[I * TB + lg + 4 * r];
+              if (q >= 0) S.X[q * NP + J * TB + lc] = t[s][r];
+            }
+          } else if (ti < NB * NB && J == K && I >= K) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) t[s][r] = Pc[(I * TB + lg + 4 * r) * PLD + lc];
+          }
+        }
+      }
+      __syncthreads();
+      if (w > 0) {
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w - 1 + TW * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && J != K && I >= K) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int q = S.dslot[I * TB + lg + 4 * r];
+              if (q >= 0) t[s][r] = S.X[q * NP + J * TB + lc];
+            }
+          }
+        }
+      }
+      __syncthreads();
+      LU_PH(3);
+      // (b) U12 = L11^-1 A12 on block row K, to X as [16][NP]
+      if (w > 0) {
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w - 1 + TW * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && I == K && J > K) {
+            d4 u = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) u = mfma16(S.Linv[lc * PLD + 4 * kk + lg], t[s][kk], u);
+            t[s] = u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S.X[(lg + 4 * r) * NP + J * TB + lc] = u[r];
+          }
+        }
+      }
+      __syncthreads();
+      LU_PH(4);
+      // (c) block column K + 1: trailing update, then the next panel's tiles to Pn
+      if (w > 0 && K + 1 < NB) {
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w - 1 + TW * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && I > K && J == K + 1) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              t[s] = mfma16(-Pc[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pn[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+          }
+        }
+      }
+      __syncthreads();
+      LU_PH(1);
+      // (d) wave 0: pivots of K out, then panel K + 1; waves 1..7: the rest of the trailing update
+      if (w == 0) {
+        if (lane < TB && K * TB + lane < n) ipiv[(size_t)sys * n + K * TB + lane] = S.piv[lane];
+        if (K + 1 < NB) panel_factor_reg<NB>(S, Pn, S.SB, K + 1, lane, n LU_PHA);
+#pragma unroll
+        for (int s = 0; s < NT; ++s) t[s] = d4{0.0, 0.0, 0.0, 0.0};  // wave 0 holds no tiles
+      } else {
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w - 1 + TW * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && I > K && J > K + 1) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              t[s] = mfma16(-Pc[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
+          }
+        }
+      }
+      LU_PH(2);
+      __syncthreads();
+      LU_PH(5);
+    }
+    int n_st = n, lc_st = lc0, lg = lg0, w = w0;
+    double* Ast = As;
+    asm volatile("" : "+s"(n_st), "+v"(lc_st), "+s"(Ast), "+v"(lg), "+s"(w));
+    if (w > 0) {
+#pragma unroll
+      for (int s = 0; s < NT; ++s) {
+        const int ti = w - 1 + TW * s;
+        const int I = ti / NB, J = ti % NB;
+        const int col = J * TB + lc_st;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = I * TB + lg + 4 * r;
+          if (ti < NB * NB && row < n_st && col < n_st) Ast[(size_t)row * n_st + col] = t[s][r];
+        }
+      }
+    }
+    if (threadIdx.x == 0) info[sys] = S.info;
+    __syncthreads();
+    LU_PH(6);
+  }
+#ifdef CKMI_LU_PHASE
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 12; ++k) atomicAdd(&g_lu_phase[k], ph_[k]);
+#endif
+}
+#endif
+
 // One wave per right-hand side: x = U^-1 L^-1 P b, in place in B[sys][n].
 constexpr int SOLVE_WAVES = 4;
 __global__ __launch_bounds__(SOLVE_WAVES* WAVE) void lu_solve_kernel(int nsys, int n, const double* __restrict__ LU,
@@ -587,7 +818,11 @@ thread_local std::string g_lu_err;
 template <int NB>
 hipError_t launch_factor(int nsys, int n, double* A, int* ipiv, int* info, hipStream_t st) {
   const int grid = nsys < 8192 ? nsys : 8192;
+#ifdef CKMI_LU_LOOKAHEAD
+  hipLaunchKernelGGL(lu_factor_kernel_la<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
+#else
   hipLaunchKernelGGL(lu_factor_kernel<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
+#endif
   return hipGetLastError();
 }
 
