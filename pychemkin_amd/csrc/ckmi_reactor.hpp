@@ -904,6 +904,85 @@ __device__ __forceinline__ void bdf_restore(BB& b, SS& S, double saved_t) {
   for (int j = 0; j < QMAX; ++j) b.zn[j] = z[j];
 }
 
+#ifndef CKMI_BDFSET_LDS
+// The coefficient recursion on locals (l[], h, tau) and one store of each result: the same
+// operations in the same order as the form below (bitwise the same values), without a round trip
+// through the LDS-resident integrator state per update.
+template <class BB, class SS>
+__device__ __forceinline__ void bdf_set(BB& b, SS& S) {
+  const int q = S.q;
+  const double h = S.h;
+  double tau[QMAX + 1];
+#pragma unroll
+  for (int i = 0; i <= QMAX; ++i) tau[i] = S.tau[i];
+  double l[QMAX + 1];
+  double xi_inv = 1.0, xistar_inv = 1.0, alpha0 = -1.0, alpha0_hat = -1.0, hsum = h;
+  l[0] = l[1] = 1.0;
+#pragma unroll
+  for (int i = 2; i <= QMAX; ++i) l[i] = 0.0;
+  if (q > 1) {
+#pragma unroll
+    for (int j = 2; j < QMAX; ++j) {
+      if (j < q) {
+        hsum += tau[j - 1];
+        xi_inv = h / hsum;
+        alpha0 -= 1.0 / j;
+#pragma unroll
+        for (int i = QMAX; i >= 1; --i)
+          if (i <= j) l[i] += l[i - 1] * xi_inv;
+      }
+    }
+    alpha0 -= 1.0 / q;
+    xistar_inv = -l[1] - alpha0;
+    double tq1 = tau[0];  // tau[q - 1] with a run-time q, as selects
+#pragma unroll
+    for (int i = 1; i <= QMAX; ++i) tq1 = (i == q - 1) ? tau[i] : tq1;
+    hsum += tq1;
+    xi_inv = h / hsum;
+    alpha0_hat = -l[1] - xi_inv;
+#pragma unroll
+    for (int i = QMAX; i >= 1; --i)
+      if (i <= q) l[i] += l[i - 1] * xistar_inv;
+  }
+  double lq = l[0];
+#pragma unroll
+  for (int i = 1; i <= QMAX; ++i) lq = (i == q) ? l[i] : lq;
+#pragma unroll
+  for (int i = 0; i <= QMAX; ++i) S.l[i] = l[i];
+  const double A1 = 1.0 - alpha0_hat + alpha0;
+  const double A2 = 1.0 + q * A1;
+  const double tq2 = fabs(A1 / (alpha0 * A2));
+  S.tq[2] = tq2;
+  S.tq[5] = fabs(A2 * xistar_inv / (lq * xi_inv));
+  if (S.qwait == 1) {
+    if (q > 1) {
+      const double Cc = xistar_inv / lq;
+      const double A3 = alpha0 + 1.0 / q;
+      const double A4 = alpha0_hat + xi_inv;
+      const double Cpinv = (1.0 - A4 + A3) / A3;
+      S.tq[1] = fabs(Cc * Cpinv);
+    } else {
+      S.tq[1] = 1.0;
+    }
+    double tq = tau[0];  // tau[q]
+#pragma unroll
+    for (int i = 1; i <= QMAX; ++i) tq = (i == q) ? tau[i] : tq;
+    hsum += tq;
+    xi_inv = h / hsum;
+    const double A5 = alpha0 - 1.0 / (q + 1);
+    const double A6 = alpha0_hat - xi_inv;
+    const double Cppinv = (1.0 - A6 + A5) / A2;
+    S.tq[3] = fabs(Cppinv / (xi_inv * (q + 2) * A5));
+  }
+  S.tq[4] = CORTES / tq2;
+  const double rl1 = 1.0 / l[1];
+  const double gamma = h * rl1;
+  S.rl1 = rl1;
+  S.gamma = gamma;
+  if (S.nst == 0) S.gammap = gamma;
+  S.gamrat = (S.nst > 0) ? gamma / S.gammap : 1.0;
+}
+#else
 template <class BB, class SS>
 __device__ __forceinline__ void bdf_set(BB& b, SS& S) {
   const int q = S.q;
@@ -960,6 +1039,8 @@ __device__ __forceinline__ void bdf_set(BB& b, SS& S) {
   if (S.nst == 0) S.gammap = S.gamma;
   S.gamrat = (S.nst > 0) ? S.gamma / S.gammap : 1.0;
 }
+
+#endif
 
 template <class BB, class SS>
 __device__ __forceinline__ void bdf_adjust_order(BB& b, SS& S, int deltaq) {
