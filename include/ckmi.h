@@ -202,6 +202,10 @@ typedef struct {
  * drive bimolecular rates of the wrong sign until the temperature runs away; the guard ends such a
  * reactor at once instead of letting it burn max_steps. */
 #define CKMI_RUN_RUNAWAY 4
+/* plug flow (problem 3) without a PPRO profile: the accepted state has no subsonic solution of the
+ * inviscid momentum equation P + G u = P0 + G u0 any more (P0 + G u0)^2 < 4 G^2 R T / Wbar -- the
+ * tube is choked (thermally, at the isothermal sound speed) and the run ends there */
+#define CKMI_RUN_CHOKED 5
 
 /* Native Chemkin-II interpreter (host only, no GPU): the parse half of KINPreProcess
  * (chemkin_wrapper.py:303-316).  chem.inp text (+ optional therm.dat text; an inline THERMO block
@@ -288,6 +292,18 @@ int ckmi_reactor_run_ex(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, int3
                         const ckmi_reactor_ext* ext, double* tau, double* Tend, double* Pend, double* Vend,
                         double* Yend, int32_t* stats, int32_t nsave, const double* t_save, double* y_save,
                         void* stream);
+
+/* Heat rates of a single-zone engine run (problem 4) on its saved states, evaluated with the
+ * integrator's own right-hand side: the output side of KINAll0D_GetEngineHeatRelease
+ * (engine.py:953-988).  T0, P0 and Y0 [KK] (device) are the cylinder's initial state (they fix its
+ * mass and the Woschni reference state); t [n] and y [n][KK+1] (T, Y; device) the saved states.
+ *   ahrr[n]   apparent heat-release rate m c_v dT/dt + P dV/dt [erg/s] (chemical heat release net of
+ *             the wall loss)
+ *   qloss[n]  wall heat-loss rate h A (T - T_wall) [erg/s] (0 for an adiabatic engine)
+ * Divide by 6 RPM for the rates per crank-angle degree. */
+int ckmi_engine_heat_rates(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, double T0, double P0,
+                           const double* Y0, int32_t n, const double* t, const double* y, double* ahrr,
+                           double* qloss, void* stream);
 
 /* Reactor kernel selection (diagnostic / testing): 0 = automatic (one wave per reactor for KK + 1 <= 64,
  * its Newton inverse stored in FP32 unless rtol < 1e-9; one 4-wave workgroup per reactor above, up to

@@ -353,7 +353,8 @@ static double pfr_pressure(const rctx* c, double t, double tsel, double T, doubl
   }
   *dPdx = 0.0;
   const double q = c->G * c->G * RU * T / Wbar;
-  return 0.5 * (c->Pm + sqrt(c->Pm * c->Pm - 4.0 * q));
+  const double disc = c->Pm * c->Pm - 4.0 * q; /* < 0: choked (clamped; the run ends with status 5) */
+  return 0.5 * (c->Pm + sqrt(disc > 0.0 ? disc : 0.0));
 }
 
 /* Single-zone IC engine (problem 4: Chemkin's ICEN problem, KINAll0D_SetupHCCIInputs, engines/HCCI.py,
@@ -1238,6 +1239,7 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
     if (m->thermo[17 * k + 2] > guard_thi) guard_thi = m->thermo[17 * k + 2];
   }
   guard_tlo *= 0.5;
+  guard_thi *= 2.0; /* margin: legitimately hot runs extrapolate the fits (runaways reach 8-10k K) */
   double tstop_final = tend;
   while (b->tn < tend * (1.0 - 1e-15)) {
     /* clamp the next step to the next critical time */
@@ -1261,6 +1263,11 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
       int bad = cfg->energy == 1 && !(b->zn[0][0] >= guard_tlo && b->zn[0][0] <= guard_thi);
       for (int k = 0; k < KK && !bad; ++k) bad = -b->zn[0][1 + k] > guard_y;
       if (bad) { status = 4; break; }
+    }
+    /* plug flow past the choke point of the momentum equation (include/ckmi.h CKMI_RUN_CHOKED) */
+    if (cfg->problem == 3 && !(cfg->nprof > 0 && cfg->prof_kind == 0)) {
+      const double Wb = mean_wt(m, b->zn[0] + 1);
+      if (ctx.Pm * ctx.Pm - 4.0 * ctx.G * ctx.G * RU * b->zn[0][0] / Wb < 0.0) { status = 5; break; }
     }
     const double tn = b->tn;
     /* solution saving by interpolation */

@@ -24,7 +24,8 @@ LIB_PATH = os.environ.get("CKMI_LIB") or os.path.join(_HERE, "_lib", "libckmi.so
 ABI_VERSION = 2  # CKMI_ABI_VERSION (include/ckmi.h): the layouts of MechDesc / ReactorCfg below
 NSTAT = 8
 STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "nni")
-RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures", 4: "runaway"}
+RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures", 4: "runaway",
+              5: "choked"}
 
 
 class NativeError(RuntimeError):
@@ -79,6 +80,8 @@ PROTOTYPES = {
                                      _P, ct.c_int32, _P, _P, _P]),
     "ckmi_reactor_run_ex": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_int32, _P, _P, _P, _P, _P,
                                         ct.POINTER(ReactorExt), _P, _P, _P, _P, _P, _P, ct.c_int32, _P, _P, _P]),
+    "ckmi_engine_heat_rates": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_double, ct.c_double, _P, ct.c_int32, _P, _P,
+                                          _P, _P, _P]),
     "ckmi_set_reactor_path": (ct.c_int, [ct.c_int32]),
     "ckmi_set_rop_path": (ct.c_int, [ct.c_int32]),
     "ckmi_rop_jit_state": (ct.c_int, [_P, ct.POINTER(ct.c_int32)]),
@@ -476,6 +479,24 @@ class DeviceMechanism:
             res["t_save"] = ts
             res["y_save"] = ys
         return res
+
+    def engine_heat_rates(self, cfg: ReactorCfg, T0: float, P0: float, Y0, t, y):
+        """Apparent heat-release and wall heat-loss rates [erg/s] of an engine run (problem 4) on its
+        saved states t[n], y[n][KK+1], from the integrator's own right-hand side
+        (ckmi_engine_heat_rates; the output side of KINAll0D_GetEngineHeatRelease, engine.py:953-988)."""
+        Y0 = self._dev(Y0).reshape(-1)
+        t = self._dev(t).reshape(-1)
+        n = t.numel()
+        y = self._dev(y).reshape(n, self.KK + 1)
+        if Y0.numel() != self.KK:
+            raise ValueError(f"Y0 must have KK = {self.KK} entries")
+        ahrr = torch.empty(n, dtype=torch.float64, device=self.device)
+        qloss = torch.empty(n, dtype=torch.float64, device=self.device)
+        with torch.cuda.device(self.device):
+            _check(lib().ckmi_engine_heat_rates(self._h, ct.byref(cfg), float(T0), float(P0), _ptr(Y0), n, _ptr(t),
+                                                _ptr(y), _ptr(ahrr), _ptr(qloss), _stream_ptr(self.device)),
+                   "ckmi_engine_heat_rates")
+        return ahrr, qloss
 
 
 def transport_fit(wt: np.ndarray, params: np.ndarray, tlow: float, thigh: float) -> np.ndarray:

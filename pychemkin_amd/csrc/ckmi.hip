@@ -721,6 +721,13 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
                                  : (lane == 0 && R.energy == 1 && !(z0 >= c.tguard_lo && z0 <= c.tguard_hi));
             c.rc = __ballot(bad) != 0 ? CKMI_RUN_RUNAWAY : 0;
           }
+          if constexpr (PF) {  // plug flow past the choke point of the momentum equation (pfr_pressure)
+            if (R.pfr == 1 && R.npv == 0 && c.rc == 0) {
+              const double z0 = b.zn[0];
+              const double sYW = wave_sum(isp ? z0 * V.rwt()[lane - 1] : 0.0);
+              if (R.Pm * R.Pm - 4.0 * R.G * R.G * RU * bcast(z0, 0) * sYW < 0.0) c.rc = CKMI_RUN_CHOKED;
+            }
+          }
           st = ST_STEP_END;
           break;
         }
@@ -872,6 +879,98 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
   }
 #undef REQUEST_F
 #undef START_BEGIN
+}
+
+// ---------------------------------------------------------------- engine heat release
+// Heat rates of an engine run on its saved states (KINAll0D_GetEngineHeatRelease, engine.py:953-988):
+// one wave per state evaluates the integrator's own right-hand side (reactor_rhs, problem 4) there,
+// so the rates are the ones the solution was integrated with, not finite differences of it:
+//   ahrr  = m c_v dT/dt + P dV/dt   [erg/s]  apparent heat release (chemical heat release net of the
+//                                           wall loss: the first law of the closed cylinder)
+//   qloss = hA (T - T_wall)          [erg/s]  wall heat loss (ICHX / Woschni, engine_hA; 0 adiabatic)
+// The per-reactor context is built from the cylinder's initial state as the reactor kernel does.
+template <bool PL>
+__global__ __launch_bounds__(WAVE) void engine_heat_kernel(MechImage img, const DevCfg* __restrict__ dcfg, double T0,
+                                                           double P0, const double* __restrict__ Y0, int n,
+                                                           const double* __restrict__ ts, const double* __restrict__ ys,
+                                                           double* __restrict__ ahrr, double* __restrict__ qloss) {
+  const ckmi_reactor_cfg* __restrict__ cfg = &dcfg->c;
+  stage_image(0, img);
+  const MechView V = make_view(0, img);
+  const int lane = threadIdx.x;
+  WaveLds L;
+  L.base = align16(img.bytes);
+  RunCtx& R = *lds_at<RunCtx>(L.base + slice_vec_bytes(img.G));
+  const int KK = V.KK;
+  const bool isp = lane >= 1 && lane <= KK;
+  const int s = isp ? lane - 1 : 0;
+  const double rw = isp ? V.rwt()[s] : 0.0;
+  const double y0 = lane == 0 ? T0 : (isp ? Y0[s] : 0.0);
+  const double Wbar0 = 1.0 / wave_sum(isp ? y0 * rw : 0.0);
+  if (lane == 0) {
+    R.cfg = cfg;
+    R.pfr = 2;
+    R.conp = 0;
+    R.energy = cfg->energy;
+    R.npv = 0;
+    R.ntp = 0;
+    R.rho0 = P0 * Wbar0 / (RU * T0);
+    double dv;
+    engine_volume(cfg->eng, 0.0, R.V0, dv);
+    R.P0 = P0;
+    R.mass = R.rho0 * R.V0;
+    R.gfac = cfg->gfac;
+    R.qloss = R.htc = R.areaq = 0.0;
+    R.tamb = 300.0;
+    R.nq = R.na = 0;
+    R.a_t = R.a_v = nullptr;
+    R.pslot = -1;
+    R.plnf = 0.0;
+  }
+  {  // gamma of the charge (Woschni's motored pressure) and its temperature, as the reactor kernel
+    const double cpR = isp ? nasa7_img(V, s, T0, log(T0), 1.0 / T0).cpR : 0.0;
+    const double cpm = wave_sum(isp ? y0 * cpR * rw : 0.0);
+    if (lane == 0) {
+      R.G = cpm / (cpm - 1.0 / Wbar0);
+      R.Pm = T0;
+    }
+  }
+  wave_lds_sync();
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const double t = ts[i];
+    const double yl = lane <= KK ? ys[(size_t)i * (KK + 1) + lane] : 0.0;
+    if (lane == 0) R.tsel = t;
+    wave_lds_sync();
+#ifdef CKMI_PHASE_TIMERS
+    unsigned long long sub[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const double fl = reactor_rhs<PL, true>(V, R, t, yl, L, 0, lane, WAVE, false, sub);
+#else
+    const double fl = reactor_rhs<PL, true>(V, R, t, yl, L, 0, lane, WAVE, false);
+#endif
+    const double T = bcast(yl, 0), dTdt = bcast(fl, 0);
+    const double Yk = isp ? yl : 0.0;
+    const double lnT = log(T);
+    const Thermo7 th = isp ? nasa7_img(V, s, T, lnT, 1.0 / T) : Thermo7{0.0, 0.0, 0.0};
+    const double cpk = th.cpR * RU * rw;
+    const double cvm = wave_sum(Yk * (cpk - RU * rw));
+    const double Wbar = 1.0 / wave_sum(Yk * rw);
+    double Vc, dVdt;
+    engine_volume(cfg->eng, t, Vc, dVdt);
+    const double rho = R.mass / Vc;
+    const double P = rho * RU * T / Wbar;
+    double q = 0.0;
+    if (cfg->eng[CKMI_ENG_HTMODEL] == 1.0) {  // the RHS's wall term (reactor_rhs, engine branch)
+      const double cpmass = wave_sum(Yk * cpk);
+      const double xp = fmax(Yk, 0.0) * rw;
+      const double Tw = cfg->eng[CKMI_ENG_TWALL];
+      q = engine_hA(V, R, T, log(0.5 * (T + Tw)), P, rho, Vc, xp / wave_sum(xp), cpmass, isp, s) * (T - Tw);
+    }
+    if (lane == 0) {
+      ahrr[i] = R.mass * cvm * dTdt + P * dVdt;
+      qloss[i] = q;
+    }
+    wave_lds_sync();  // R.tsel and the slice are rewritten for the next state
+  }
 }
 
 // ---------------------------------------------------------------- ROP kernels
@@ -1578,7 +1677,7 @@ int ckmi_mech_create(const ckmi_mech_desc* d, ckmi_mech** out) {
       thi = std::max(thi, d->thermo[17 * k + 2]);
     }
     m->tguard_lo = 0.5 * tlo;
-    m->tguard_hi = thi;
+    m->tguard_hi = 2.0 * thi;  // margin: legitimately hot runs extrapolate the fits (runaways reach 8-10k K)
   }
   // ---- order reactions: elementary, then third-body, then falloff
   std::vector<int> ordr;
@@ -2067,6 +2166,43 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
   if (rc) return rc;
   HIP_CHECK(hipGetLastError());
   return CKMI_OK;
+}
+
+int ckmi_engine_heat_rates(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, double T0, double P0, const double* Y0,
+                           int32_t n, const double* t, const double* y, double* ahrr, double* qloss, void* stream) {
+  if (!m || !cfg || n < 0 || !Y0 || (n > 0 && (!t || !y || !ahrr || !qloss))) return fail(CKMI_ERR_ARG, "bad argument");
+  if (!(T0 > 0.0) || !(P0 > 0.0)) return fail(CKMI_ERR_ARG, "T0 and P0 must be > 0");
+  if (m->KK + 1 > WAVE) return fail(CKMI_ERR_UNSUPPORTED, "engine heat rates need KK + 1 <= 64 (as engine runs)");
+  if (cfg->eng[CKMI_ENG_HTMODEL] == 1.0 && !cfg->tran)
+    return fail(CKMI_ERR_ARG, "the engine's ICHX heat transfer needs the transport fits (cfg->tran)");
+  if (n == 0) return CKMI_OK;
+  DevCfg dc;
+  dc.c = *cfg;
+  if (dc.c.gfac == 0.0) dc.c.gfac = 1.0;
+  dc.ncrit = 0;
+  dc.guard_y = std::max(1e-3, 1e3 * cfg->atol);
+  dc.guard_tlo = m->tguard_lo;
+  dc.guard_thi = m->tguard_hi;
+  const hipStream_t st = (hipStream_t)stream;
+  const size_t lds = (size_t)align16(m->img.bytes) + slice_vec_bytes(m->G) + align16((int)sizeof(RunCtx));
+  const void* fn = m->has_plog ? (const void*)engine_heat_kernel<true> : (const void*)engine_heat_kernel<false>;
+  if (lds > 64 * 1024) HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  const size_t cbytes = (sizeof(DevCfg) + 255) & ~(size_t)255;
+  void* ws = nullptr;
+  HIP_CHECK(hipMallocAsync(&ws, cbytes, st));
+  int rc = stage_cfg(dc, (DevCfg*)ws, st);
+  if (rc == CKMI_OK) {
+    const int grid = std::min(n, 4096);
+    if (m->has_plog)
+      hipLaunchKernelGGL(engine_heat_kernel<true>, dim3(grid), dim3(WAVE), lds, st, m->img, (const DevCfg*)ws, T0, P0,
+                         Y0, n, t, y, ahrr, qloss);
+    else
+      hipLaunchKernelGGL(engine_heat_kernel<false>, dim3(grid), dim3(WAVE), lds, st, m->img, (const DevCfg*)ws, T0, P0,
+                         Y0, n, t, y, ahrr, qloss);
+    HIP_CHECK(hipGetLastError());
+  }
+  HIP_CHECK(hipFreeAsync(ws, st));
+  return rc;
 }
 
 int ckmi_set_reactor_path(int32_t path) {

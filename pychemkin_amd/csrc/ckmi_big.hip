@@ -50,7 +50,8 @@ constexpr int RED_SET = 16;     // doubles per reduction set (two sets alternate
 constexpr int NDQ = 16;         // dq/dC slots per reaction: unit reactions 4 + 4, general ones GEN_SLOTS + GEN_SLOTS
 
 // Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py --big): per-reactor shader
-// cycles per phase into a debug buffer [n][8]: rhs, rhs+J, build, factor, solve, total, -, -.
+// cycles per phase into a debug buffer [n][16]: rhs, rhs+J, build, factor, solve, total, then the
+// factorisation split of wave 0 (MFMA form: own panels, barrier, -, pivot-row gather, MFMA, restore).
 #ifdef CKMI_PHASE_TIMERS
 __device__ unsigned long long* g_big_phase_buf = nullptr;
 #define BPH_T0() const unsigned long long _bph0 = __builtin_amdgcn_s_memtime()
@@ -203,6 +204,28 @@ __device__ __forceinline__ uint64_t row16_max_u64(uint64_t v) {
   return v;
 }
 
+// max of a u64 over the whole wave, in every lane: DPP inside the 16-lane rows, then the gfx950 row
+// swaps (permlane16_swap pairs rows 0-1 and 2-3, permlane32_swap the two halves) -- no readlane / SGPR
+// round trip, no LDS
+__device__ __forceinline__ uint64_t wave_max_u64_all(uint64_t v) {
+  v = row16_max_u64(v);
+  {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    const uint64_t a = ((uint64_t)h[0] << 32) | l[0], b = ((uint64_t)h[1] << 32) | l[1];
+    v = a > b ? a : b;
+  }
+  {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const uint64_t a = ((uint64_t)h[0] << 32) | l[0], b = ((uint64_t)h[1] << 32) | l[1];
+    v = a > b ? a : b;
+  }
+  return v;
+}
+
 // pivot-step header in LDS (double-buffered by step parity)
 struct PivHdr {
   double piv;
@@ -273,7 +296,7 @@ struct BigMatrix {
   __device__ __forceinline__ void step(const BigLds& L, int k, int b, int cn, uint32_t& pivmask, bool& ok, int t,
                                        int wid, int lane
 #ifdef CKMI_PHASE_TIMERS
-                                       , unsigned long long (&fph)[3]
+                                       , unsigned long long (&fph)[6]
 #endif
   ) {
     const int ti = lane & 15, q = lane >> 4;
@@ -371,7 +394,7 @@ struct BigMatrix {
   template <int Bc>
   __device__ __forceinline__ void blocks(const BigLds& L, uint32_t& pivmask, bool& ok, int t, int wid, int lane
 #ifdef CKMI_PHASE_TIMERS
-                                         , unsigned long long (&fph)[3]
+                                         , unsigned long long (&fph)[6]
 #endif
   ) {
     if constexpr (Bc < NB) {
@@ -396,9 +419,9 @@ struct BigMatrix {
 
   // Gauss-Jordan with partial pivoting (largest |a| rounded to fp32, ties to the lowest row).
   // false if a pivot column was exactly zero (the factors are then garbage).
-  __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane
+  __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane, int /*n*/
 #ifdef CKMI_PHASE_TIMERS
-                                         , unsigned long long (&fph)[3]
+                                         , unsigned long long (&fph)[6]
 #endif
   ) {
     const int t = opaque_lane(tid);
@@ -467,6 +490,16 @@ struct BigMatrix {
 // (row ti + 16 r, column 16 c + 4 w + q) is exactly the MFMA C/D map of a^T (col = lane & 15 = ti,
 // row = (lane >> 4) + 4 e = q + 4 e) when the 4 tiles c = 4 g + e form one accumulator, so the
 // registers are updated in place.  One workgroup barrier per panel instead of one per column.
+//
+// The panel's 4 pivot steps are the critical path (the other three waves wait at the barrier).  In
+// the MFMA layout a panel column sits in 16 lanes with 11 rows each, so a step is an 11-deep serial
+// key scan, a column exchange through LDS and a pivot-row gather (round 4: ~2.2k cycles per step).
+// The owner therefore transposes the 4 columns once through LDS into a row-per-lane layout (lane l:
+// rows l, l + 64, l + 128 of all four columns), where a step needs no LDS at all: a 3-candidate key
+// per lane, one whole-wave max (DPP + row swaps), 8 readlanes of the pivot row, and FMAs on the
+// lane's own registers.  The arithmetic (pivot choice, multipliers, update) is exactly that of the
+// per-column form, so the factors are bitwise the same.  Panels whose columns all lie in the
+// identity padding (k0 >= n) are skipped: their steps pivot on their own row and change nothing.
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 struct PanHdr {
@@ -502,12 +535,21 @@ struct BigMatrixM {
     }
   }
 
+  static constexpr int NJ = (NC + 63) / 64;  // rows per lane in the transposed panel
+
+  // row r of the matrix has been a pivot row: bit (r & 63) of dm[r >> 6] (wave-uniform masks)
+  __device__ __forceinline__ static void mark_done(uint64_t (&dm)[NJ], int p) {
+    const uint64_t bit = 1ull << (p & 63);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dm[j] |= (p >> 6) == j ? bit : 0ull;  // selects, not a dynamic index
+  }
+
   // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo
   template <int C>
-  __device__ __forceinline__ void panel(const BigLds& L, int wo, int par, uint32_t& pivmask, bool& ok, int t, int wid,
+  __device__ __forceinline__ void panel(const BigLds& L, int wo, int par, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                         int lane
 #ifdef CKMI_PHASE_TIMERS
-                                        , unsigned long long (&fph)[3]
+                                        , unsigned long long (&fph)[6]
 #endif
   ) {
 #ifdef CKMI_PHASE_TIMERS
@@ -522,7 +564,86 @@ struct BigMatrixM {
     double* Pb = lds_at<double>(L.xpart) + par * 4 * NC;             // [4 s][NC] P of the panel
     double* Rb = lds_at<double>(L.xpart) + 8 * NC + wid * 16 * NB;  // [4 s][NB c][4 q] pivot rows, per wave
     PanHdr* hdr = lds_at<PanHdr>(L.phdr) + par;
+#ifndef CKMI_BIG_PANEL_COLS
     if (wid == wo) {
+      // the panel's columns into Pb ([s][NC], as published below) and back, row-per-lane
+#pragma unroll
+      for (int r = 0; r < NB; ++r) Pb[q * NC + ti + 16 * r] = a[r][G][E];
+      wave_lds_sync();
+      double y[NJ][4];
+      uint64_t rid[NJ];  // low key word: 0xffffffff - row (ties go to the lowest row)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = lane + 64 * j;
+        rid[j] = 0xffffffffu - (uint32_t)row;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) y[j][s] = row < NC ? Pb[s * NC + row] : 0.0;
+      }
+      int ps[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        uint64_t key = 0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
+          const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
+          if (cand && kr > key) key = kr;
+        }
+        key = wave_max_u64_all(key);
+        const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)key);
+        const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
+        if (khi == 0u) ok = false;
+        const int p = (int)(0xffffffffu - klo);
+        ps[s] = p;
+        const int pl = p & 63, pj = p >> 6;
+        // the pivot row's entries of the 4 panel columns (wave-uniform, from lane pl)
+        double pv[4];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          double v = y[0][s2];
+#pragma unroll
+          for (int j = 1; j < NJ; ++j) v = pj == j ? y[j][s2] : v;
+          pv[s2] = bcast(v, pl);
+        }
+        const double piv = pv[s];
+        const double rcp = rcp_nr(piv);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const bool isp = lane + 64 * j == p;
+          const double g = isp ? (piv - 1.0) * rcp : y[j][s] * rcp;
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) y[j][s2] = s2 == s ? (isp ? rcp : -g) : fma(-g, pv[s2], y[j][s2]);
+        }
+        mark_done(dm, p);
+      }
+      // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = lane + 64 * j;
+        if (row < NC) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) Pb[s * NC + row] = y[j][s];
+        }
+      }
+      if (lane < 4) {
+        const int pl = lane == 0 ? ps[0] : (lane == 1 ? ps[1] : (lane == 2 ? ps[2] : ps[3]));
+        lds_at<int>(L.perm)[k0 + lane] = pl;
+        lds_at<int>(L.rank)[pl] = k0 + lane;
+        hdr->p[lane] = pl;
+      }
+      if (lane == 0) hdr->ok = ok ? 1 : 0;
+    }
+#else  // A/B reference: the round-4 per-column pivot steps in the MFMA layout
+    if (wid == wo) {
+      uint32_t pivmask = 0u;  // bit r: row ti + 16 r has been a pivot row
+#pragma unroll
+      for (int r = 0; r < NB; ++r) {
+        const int row = ti + 16 * r;
+        uint64_t m = dm[0];
+#pragma unroll
+        for (int j = 1; j < NJ; ++j) m = (row >> 6) == j ? dm[j] : m;
+        if ((m >> (row & 63)) & 1ull) pivmask |= 1u << r;
+      }
       double x[NB];
 #pragma unroll
       for (int r = 0; r < NB; ++r) x[r] = a[r][G][E];
@@ -586,6 +707,7 @@ struct BigMatrixM {
       }
       if (lane == 0) hdr->ok = ok ? 1 : 0;
     }
+#endif
     PPH(0);
     __syncthreads();  // the panel's P' and pivots are published
     PPH(1);
@@ -597,7 +719,7 @@ struct BigMatrixM {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int tip = pr[s] & 15, rp = pr[s] >> 4;
-      if (ti == tip) pivmask |= 1u << rp;
+      mark_done(dm, pr[s]);
 #pragma unroll
       for (int r = 0; r < NB; ++r) {
         if (r == rp) {  // uniform: one scalar branch selects the register row
@@ -610,6 +732,7 @@ struct BigMatrixM {
       }
     }
     wave_lds_sync();
+    PPH(3);
     // A = U^T (lane: column j = lane & 15 of the group, panel step lane >> 4), B = P'^T
     double A[NG];
 #pragma unroll
@@ -626,6 +749,15 @@ struct BigMatrixM {
 #pragma unroll
       for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
     }
+#ifdef CKMI_PHASE_TIMERS
+    {  // the MFMA results have landed before the stamp
+      double chk = 0.0;
+#pragma unroll
+      for (int r = 0; r < NB; ++r) chk += a[r][NG - 1][0];
+      if (chk == 12345.678) fph[4] += 1;
+    }
+#endif
+    PPH(4);
     if (wid == wo) {  // the panel columns keep their processed values
 #pragma unroll
       for (int r = 0; r < NB; ++r) a[r][G][E] = Pb[q * NC + ti + 16 * r];
@@ -638,36 +770,47 @@ struct BigMatrixM {
       if (chk == 12345.678) fph[2] += 1;
     }
 #endif
-    PPH(2);
+    PPH(5);
 #undef PPH
   }
 
 #ifdef CKMI_PHASE_TIMERS
 #define FPH_ARG , fph
-#define FPH_PARAM , unsigned long long (&fph)[3]
+#define FPH_PARAM , unsigned long long (&fph)[6]
 #else
 #define FPH_ARG
 #define FPH_PARAM
 #endif
   template <int C>
-  __device__ __forceinline__ void panels(const BigLds& L, uint32_t& pivmask, bool& ok, int t, int wid, int lane FPH_PARAM) {
+  __device__ __forceinline__ void panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
+                                         int lane FPH_PARAM) {
     if constexpr (C < NB) {
 #pragma unroll 1
-      for (int wo = 0; wo < 4; ++wo) panel<C>(L, wo, (C * 4 + wo) & 1, pivmask, ok, t, wid, lane FPH_ARG);
-      panels<C + 1>(L, pivmask, ok, t, wid, lane FPH_ARG);
+      for (int wo = 0; wo < 4; ++wo)
+        if (16 * C + 4 * wo < n) panel<C>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
+      panels<C + 1>(L, n, dm, ok, t, wid, lane FPH_ARG);
     }
   }
 
-  __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane
+  __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane, int n
 #ifdef CKMI_PHASE_TIMERS
-                                         , unsigned long long (&fph)[3]
+                                         , unsigned long long (&fph)[6]
 #endif
   ) {
     (void)B;
     const int t = opaque_lane(tid);
-    uint32_t pivmask = 0u;
+    // steps of the skipped identity-padding panels pivot on their own row (published before the
+    // first panel's barrier; the solve reads perm / rank after the last one)
+    const int kpad = (n + 3) & ~3;
+    if (t >= kpad && t < NC) {
+      lds_at<int>(L.perm)[t] = t;
+      lds_at<int>(L.rank)[t] = t;
+    }
+    uint64_t dm[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) dm[j] = 0ull;
     bool ok = true;
-    panels<0>(L, pivmask, ok, t, wid, lane FPH_ARG);
+    panels<0>(L, n, dm, ok, t, wid, lane FPH_ARG);
     return ok;
   }
 
@@ -1057,7 +1200,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
   int st = ST_NEXT;
 #ifdef CKMI_PHASE_TIMERS
   unsigned long long bph[6] = {0, 0, 0, 0, 0, 0};
-  unsigned long long fph[3] = {0, 0, 0};
+  unsigned long long fph[6] = {0, 0, 0, 0, 0, 0};
   unsigned long long t_r0 = 0;
 #endif
 
@@ -1098,7 +1241,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
 #pragma unroll
           for (int k = 0; k < 6; ++k) bph[k] = 0;
 #pragma unroll
-          for (int k = 0; k < 3; ++k) fph[k] = 0;
+          for (int k = 0; k < 6; ++k) fph[k] = 0;
           t_r0 = __builtin_amdgcn_s_memtime();
 #endif
           const int prob = io.problem[r];
@@ -1362,9 +1505,9 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           {
             BPH_T0();
 #ifdef CKMI_PHASE_TIMERS
-            ok = M.factor(L, B, tid, wid, lane, fph);
+            ok = M.factor(L, B, tid, wid, lane, n, fph);
 #else
-            ok = M.factor(L, B, tid, wid, lane);
+            ok = M.factor(L, B, tid, wid, lane, n);
 #endif
             BPH_ADD(3);
           }
@@ -1596,6 +1739,11 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             if (tid == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
             c.rc = bmax(B, v, wid, lane) > dcfg->guard_y ? CKMI_RUN_RUNAWAY : 0;
           }
+          if (R.pfr && R.npv == 0 && c.rc == 0) {  // plug flow past the choke point (pfr_pressure)
+            double Tz = b.zn[0];
+            const double sYW = bsum_bcast(B, isp ? Tz * V.rwt()[tid - 1] : 0.0, Tz, 0, tid, wid, lane);
+            if (R.Pm * R.Pm - 4.0 * R.G * R.G * RU * Tz * sYW < 0.0) c.rc = CKMI_RUN_CHOKED;
+          }
           st = ST_STEP_END;
           break;
         }
@@ -1716,12 +1864,14 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           }
           if (isp) io.Y[(size_t)r * KK + tid - 1] = yf;
 #ifdef CKMI_PHASE_TIMERS
-          if (g_big_phase_buf && tid < 8) {
+          if (g_big_phase_buf && tid < 16) {  // [rhs, rhs+J, build, factor, solve, total, 6 x factor split, -]
             const unsigned long long tot = __builtin_amdgcn_s_memtime() - t_r0;
-            unsigned long long v = tid == 5 ? tot : (tid == 6 ? fph[0] : (tid == 7 ? fph[1] : 0));
+            unsigned long long v = tid == 5 ? tot : 0;
 #pragma unroll
             for (int k = 0; k < 5; ++k) v = tid == k ? bph[k] : v;
-            g_big_phase_buf[(size_t)r * 8 + tid] = v;
+#pragma unroll
+            for (int k = 0; k < 6; ++k) v = tid == 6 + k ? fph[k] : v;
+            g_big_phase_buf[(size_t)r * 16 + tid] = v;
           }
 #endif
           st = ST_NEXT;
@@ -1865,7 +2015,7 @@ int launch_big_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const React
 }  // namespace ckmi
 
 #ifdef CKMI_PHASE_TIMERS
-// diagnostic build only: buf = device u64 [n][8] per-reactor phase cycles of the workgroup kernel
+// diagnostic build only: buf = device u64 [n][16] per-reactor phase cycles of the workgroup kernel
 extern "C" int ckmi_debug_big_phase_buffer(void* buf) {
   if (hipMemcpyToSymbol(HIP_SYMBOL(ckmi::g_big_phase_buf), &buf, sizeof(buf)) != hipSuccess) return CKMI_ERR_HIP;
   return CKMI_OK;

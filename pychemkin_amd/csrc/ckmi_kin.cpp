@@ -78,6 +78,7 @@ struct Reactor0D {
   bool done = false;
   double tau = -1.0;
   std::vector<double> t, T, P, V, Y;  // Y [npts][KK]
+  ckmi_reactor_cfg cfg{};             // the configuration the last run was integrated with
 };
 Reactor0D g_r;
 
@@ -476,9 +477,11 @@ int run_reactor(ChemSet* s) {
       V = engine_volume_host(c.eng, t);  // c.eng: with the POLEN keyword
       P = (rho0 * engine_volume_host(c.eng, 0.0) / V) * RU * T * sw;
     } else if (pfr) {  // momentum (ckmi.h problem 3) or PPRO; V = the velocity
-      const double Pin = pp ? pp->y.front() : g_r.P0;
-      const double G = Pin / (RU * g_r.T0 * sw0) * g_r.V0, Pm = Pin + G * g_r.V0;
-      P = pp ? pwl(pp->x, pp->y, t) : 0.5 * (Pm + std::sqrt(Pm * Pm - 4.0 * G * G * RU * T * sw));
+      // as the kernels (ckmi.hip reactor_kernel, PFR.py:609-612): the mass flux from the inlet state, the
+      // PPRO profile in absolute positions (t is relative to the start position x0)
+      const double G = g_r.P0 / (RU * g_r.T0 * sw0) * g_r.V0, Pm = g_r.P0 + G * g_r.V0;
+      P = pp ? pwl(pp->x, pp->y, t + g_r.x0)
+             : 0.5 * (Pm + std::sqrt(std::max(Pm * Pm - 4.0 * G * G * RU * T * sw, 0.0)));  // choked: status 5
       V = G / (P / (RU * T * sw));
     } else if (g_r.problem == 1) {
       P = pp ? pwl(pp->x, pp->y, t) : g_r.P0;
@@ -493,6 +496,7 @@ int run_reactor(ChemSet* s) {
     g_r.V.push_back(V);
     g_r.Y.insert(g_r.Y.end(), pt.second.begin() + 1, pt.second.end());
   }
+  g_r.cfg = c;
   g_r.done = true;
   if (status != CKMI_RUN_OK)
     return fail(100 + status, "reactor integration failed (status " + std::to_string(status) + ")");
@@ -871,10 +875,16 @@ int KINAll0D_SetupHCCIInputs(int* chemset, double* ivc, double* evo, double* rpm
   return CKMI_OK;
 }
 
-// KINAll0D_GetEngineHeatRelease (chemkin_wrapper.py:769-777, engine.py:953-988): crank angles of 10 / 50
-// / 90 % of the cumulative chemical heat release of the last engine run, -sum_k h_k(298.15 K) W_k
-// (n_k(t) - n_k(0)) on its solution points (linear interpolation of the crossing).  The heat-loss and
-// apparent-heat-release rates per CA are not produced (0).
+// KINAll0D_GetEngineHeatRelease (chemkin_wrapper.py:769-777, engine.py:953-988) on the last engine run.
+//   hr10 / hr50 / hr90: crank angles of 10 / 50 / 90 % of the cumulative chemical heat release,
+//     -sum_k h_k(298.15 K) W_k (n_k(t) - n_k(0)), on the solution points (linear interpolation);
+//   ahrr: the peak apparent heat-release rate per CA [erg/degree], m c_v dT/dCA + P dV/dCA from the
+//     integrator's right-hand side at the solution points (ckmi_engine_heat_rates on the device);
+//   ahrrp: the peak of the same from the pressure trace with the charge's constant gamma,
+//     gamma/(gamma-1) P dV/dCA + 1/(gamma-1) V dP/dCA (central differences on the solution points);
+//   qloss_ca[0]: the peak wall heat-loss rate per CA [erg/degree], hA (T - T_wall) (ICHX; 0 adiabatic).
+// The reference reads these as scalars; which instant its library reports is not documented in the
+// reference, so the peaks over the cycle are returned (the full profiles: ckmi_engine_heat_rates).
 int KINAll0D_GetEngineHeatRelease(double* qloss_ca, double* ahrr, double* ahrrp, double* hr10, double* hr50,
                                   double* hr90) {
   std::lock_guard<std::recursive_mutex> lk(g_mu);
@@ -884,18 +894,65 @@ int KINAll0D_GetEngineHeatRelease(double* qloss_ca, double* ahrr, double* ahrrp,
   std::vector<double> cpR, hRT, sR;
   int rc = species_thermo(s, 298.15, cpR, hRT, sR);
   if (rc) return rc;
-  const int KK = s->KK;
+  const int KK = s->KK, n1 = KK + 1;
   const size_t np = g_r.t.size();
   std::vector<double> q(np, 0.0);
   for (size_t i = 0; i < np; ++i)
     for (int k = 0; k < KK; ++k)
       q[i] -= (g_r.Y[i * KK + k] - g_r.Y[k]) * hRT[k] * RU * 298.15 / s->wt[k];
-  if (qloss_ca) *qloss_ca = 0.0;
-  if (ahrr) *ahrr = 0.0;
-  if (ahrrp) *ahrrp = 0.0;
+  const double rate = 6.0 * g_r.eng[CKMI_ENG_RPM];  // degrees per second
+  // heat rates on the device, at the solution points
+  std::vector<double> ah(np, 0.0), ql(np, 0.0);
+  if (np > 0) {
+    (void)hipSetDevice(s->device);
+    std::vector<double> hin(KK + np + np * n1);
+    std::copy(g_r.Y0.begin(), g_r.Y0.end(), hin.begin());
+    std::copy(g_r.t.begin(), g_r.t.end(), hin.begin() + KK);
+    for (size_t i = 0; i < np; ++i) {
+      hin[KK + np + i * n1] = g_r.T[i];
+      std::copy(g_r.Y.begin() + i * KK, g_r.Y.begin() + (i + 1) * KK, hin.begin() + KK + np + i * n1 + 1);
+    }
+    double* d = nullptr;
+    if ((rc = hip_ok(hipMalloc((void**)&d, (hin.size() + 2 * np) * sizeof(double)), "hipMalloc"))) return rc;
+    double *dY0 = d, *dt = d + KK, *dy = dt + np, *dah = dy + np * n1, *dql = dah + np;
+    rc = hip_ok(hipMemcpy(d, hin.data(), hin.size() * sizeof(double), hipMemcpyHostToDevice), "H2D");
+    if (!rc) {
+      rc = ckmi_engine_heat_rates(s->mech, &g_r.cfg, g_r.T0, g_r.P0, dY0, (int32_t)np, dt, dy, dah, dql, nullptr);
+      if (rc) rc = fail(rc, ckmi_last_error());
+    }
+    if (!rc) rc = hip_ok(hipDeviceSynchronize(), "engine heat rates");
+    if (!rc) rc = hip_ok(hipMemcpy(ah.data(), dah, np * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    if (!rc) rc = hip_ok(hipMemcpy(ql.data(), dql, np * sizeof(double), hipMemcpyDeviceToHost), "D2H");
+    (void)hipFree(d);
+    if (rc) return rc;
+  }
+  double gamma = 1.4;
+  {  // gamma of the charge at IVC
+    std::vector<double> c0, h0, s0;
+    if ((rc = species_thermo(s, g_r.T0, c0, h0, s0))) return rc;
+    double cpm = 0.0, sw = 0.0;
+    for (int k = 0; k < KK; ++k) {
+      cpm += g_r.Y0[k] * c0[k] / s->wt[k];
+      sw += g_r.Y0[k] / s->wt[k];
+    }
+    gamma = cpm / (cpm - sw);
+  }
+  double pk_ah = 0.0, pk_ap = 0.0, pk_ql = 0.0;
+  for (size_t i = 0; i < np; ++i) {
+    pk_ah = std::max(pk_ah, ah[i] / rate);
+    pk_ql = std::max(pk_ql, ql[i] / rate);
+    if (np > 1) {  // central differences in CA (one-sided at the ends), as numpy.gradient
+      const size_t a = i == 0 ? 0 : i - 1, b = i + 1 == np ? np - 1 : i + 1;
+      const double dca = (g_r.t[b] - g_r.t[a]) * rate;
+      const double dP = (g_r.P[b] - g_r.P[a]) / dca, dV = (g_r.V[b] - g_r.V[a]) / dca;
+      pk_ap = std::max(pk_ap, gamma / (gamma - 1.0) * g_r.P[i] * dV + g_r.V[i] * dP / (gamma - 1.0));
+    }
+  }
+  if (qloss_ca) *qloss_ca = pk_ql;
+  if (ahrr) *ahrr = pk_ah;
+  if (ahrrp) *ahrrp = pk_ap;
   double* out[3] = {hr10, hr50, hr90};
   const double lev[3] = {0.1, 0.5, 0.9};
-  const double rate = 6.0 * g_r.eng[CKMI_ENG_RPM];
   for (int j = 0; j < 3; ++j) {
     if (!out[j]) continue;
     double ca = g_r.eng[CKMI_ENG_CA0];

@@ -93,7 +93,9 @@ __device__ __forceinline__ double pfr_pressure(const ckmi_reactor_cfg* c, int np
   }
   dPdx = 0.0;
   const double q = G * G * RU * T / Wbar;
-  return 0.5 * (Pm + sqrt(Pm * Pm - 4.0 * q));
+  // past the choke point there is no subsonic root: clamped at the sonic one, and the step that
+  // accepts such a state ends the run with CKMI_RUN_CHOKED
+  return 0.5 * (Pm + sqrt(fmax(Pm * Pm - 4.0 * q, 0.0)));
 }
 // Single-zone IC engine (problem 4, oracle/ckoracle.c engine_volume): slider-crank with piston-pin
 // offset e = -POLEN, the crank angle counted from the offset engine's top dead centre, clearance

@@ -18,6 +18,7 @@ from typing import List, Optional
 import numpy as np
 
 from ..batchreactor import BatchReactors
+from ..constants import R_GAS
 from ..logger import logger
 from ..reactormodel import ReactorError
 
@@ -288,6 +289,30 @@ class Engine(BatchReactors):
         if ca[-1] < self.EVOCA * (1.0 - 1e-15) - 1e-12:
             ca = np.append(ca, self.EVOCA)
         return (ca - self.IVCCA) / self.degpersec
+
+    def get_engine_heat_release_rates(self) -> dict:
+        """Heat rates per crank-angle degree on the saved solution points (extension: the profiles behind
+        the scalars of KINAll0D_GetEngineHeatRelease, engine.py:953-988).
+
+        Returns a dict of arrays over the solution points: ``CA`` [degree]; ``AHRR`` the apparent heat-
+        release rate m c_v dT/dCA + P dV/dCA [erg/degree] from the integrator's own right-hand side on the
+        device (chemical heat release net of the wall loss); ``AHRRP`` the same from the pressure trace
+        with a constant gamma (that of the charge at IVC), gamma/(gamma-1) P dV/dCA + 1/(gamma-1) V dP/dCA
+        (central differences on the saved points); ``QLossRateCA`` the wall heat-loss rate hA (T - T_wall)
+        [erg/degree] (0 for an adiabatic cylinder)."""
+        if self.runstatus != 0:
+            raise ReactorError("no successful engine run")
+        ts, ys = self._raw
+        mix0 = self.reactormixture
+        dm = self._chem.device_mechanism()
+        ahrr, qloss = dm.engine_heat_rates(self.reactor_cfg(), mix0.temperature, mix0.pressure, mix0.Y, ts, ys)
+        ca = self.IVCCA + ts * self.degpersec
+        P, V = self._PV_of(ts, ys[:, 0], ys[:, 1:])
+        gamma = mix0.CPBL() / (mix0.CPBL() - R_GAS)  # cp / cv of the charge (molar cp)
+        dP, dV = np.gradient(P, ca), np.gradient(V, ca)
+        ahrrp = gamma / (gamma - 1.0) * P * dV + 1.0 / (gamma - 1.0) * V * dP
+        return {"CA": ca, "AHRR": ahrr.cpu().numpy() / self.degpersec, "AHRRP": ahrrp,
+                "QLossRateCA": qloss.cpu().numpy() / self.degpersec}
 
     def get_engine_heat_release_CAs(self):
         """Crank angles of 10 / 50 / 90 % of the cumulative chemical heat release (engine.py:953-988).

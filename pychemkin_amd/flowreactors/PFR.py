@@ -200,7 +200,7 @@ class PlugFlowReactor(BatchReactors):
             P = np.interp(x + self._startposition, pp.x, pp.y)  # x from the start position; pp.x absolute
         else:
             Pm = mix0.pressure + G * self._u0
-            P = 0.5 * (Pm + np.sqrt(Pm * Pm - 4.0 * G * G * R_GAS * T / Wbar))
+            P = 0.5 * (Pm + np.sqrt(np.maximum(Pm * Pm - 4.0 * G * G * R_GAS * T / Wbar, 0.0)))  # choked: status 5
         u = G / (P * Wbar / (R_GAS * T))
         return P, u
 

@@ -292,6 +292,72 @@ class Mixture:
         qf, qr = dm.reaction_rates(T, P, Y)
         return qf[:, 0].cpu().numpy(), qr[:, 0].cpu().numpy()
 
+    # ------------------------------------------------------------------ static forms (chemistry set id)
+    @staticmethod
+    def _static_state(chemID: int, p: float, t: float, frac, wt, mode: str):
+        """Chemistry set and normalised mass fractions of the static rate calls (mixture.py:1386-1430):
+        the same argument checks, raised instead of exit()."""
+        from .chemistry import _chemistry_sets
+
+        if chemID < 0 or chemID not in _chemistry_sets:
+            raise MixtureError("invalid chemistry.")
+        if p <= 0.0 or (p * t) <= 0.0:
+            raise MixtureError("invalid pressure and/or temperature value(s).")
+        frac = np.asarray(frac, dtype=np.float64)
+        wt = np.asarray(wt, dtype=np.float64)
+        if len(frac) != len(wt):
+            raise MixtureError(f"{mode} fraction and molar mass arrays must have the same size = {len(frac)}")
+        if mode.lower() == "mole":
+            y = Mixture.mole_fraction_to_mass_fraction(molefrac=frac, wt=wt)
+        elif mode.lower() == "mass":
+            y = Mixture.normalize(frac=frac)[1]
+        else:
+            raise MixtureError('must specify "mole" or "mass" fractions given.')
+        chem = _chemistry_sets[chemID]
+        if len(y) != chem.KK:
+            raise MixtureError(f"composition has {len(y)} entries, the chemistry set {chem.KK} species")
+        return chem, y
+
+    @staticmethod
+    def rate_of_production(chemID: int, p: float, t: float, frac, wt, mode: str) -> np.ndarray:
+        """Species molar rates of production [mol/cm3-s] of the state (p, t, frac) (mixture.py:1353-1454):
+        KINGetGasROP with the normalised mass fractions, on the GPU (the same kernel as ROP())."""
+        import torch
+
+        chem, y = Mixture._static_state(chemID, p, t, frac, wt, mode)
+        dm = chem.device_mechanism()
+        T = torch.tensor([float(t)], dtype=torch.float64, device=dm.device)
+        P = torch.tensor([float(p)], dtype=torch.float64, device=dm.device)
+        Y = torch.as_tensor(y.reshape(-1, 1).copy(), dtype=torch.float64, device=dm.device)
+        return dm.rop_thermo(T, P, Y)[0][:, 0].cpu().numpy()
+
+    @staticmethod
+    def reaction_rates(chemID: int, numbreaction: int, p: float, t: float, frac, wt,
+                       mode: str) -> Tuple[np.ndarray, np.ndarray]:
+        """Forward and reverse rates of the gas reactions [mol/cm3-s] (mixture.py:1456-1567).
+
+        The reference hands the normalised mass fractions to KINGetGasReactionRates (mixture.py:1540),
+        which reads its composition argument as mole fractions (Chemkin's CKKFKR convention; the
+        reactionrates golden decides): the rates returned are those of the state whose mole
+        fractions equal these mass fractions, exactly as RxnRates() (reference_compat=True) returns them."""
+        import torch
+
+        chem, y = Mixture._static_state(chemID, p, t, frac, wt, mode)
+        if int(numbreaction) != chem.IIGas:
+            raise MixtureError(f"numbreaction = {numbreaction}, the chemistry set has {chem.IIGas} reactions")
+        dm = chem.device_mechanism()
+        yy = y * chem.WT  # y read as mole fractions -> the mass fractions of that state, for the kernel
+        T = torch.tensor([float(t)], dtype=torch.float64, device=dm.device)
+        P = torch.tensor([float(p)], dtype=torch.float64, device=dm.device)
+        Y = torch.as_tensor((yy / yy.sum()).reshape(-1, 1), dtype=torch.float64, device=dm.device)
+        qf, qr = dm.reaction_rates(T, P, Y)
+        return qf[:, 0].cpu().numpy(), qr[:, 0].cpu().numpy()
+
+    def use_idealgas_law(self) -> None:
+        """Ideal-gas law for the mixture properties (mixture.py:2706-2740).  The device path is ideal-gas
+        only (real-gas cubic EOS is out of scope), so this is the state every mixture is already in."""
+        self.userealgas = False
+
     def CPBL(self) -> float:
         """Mixture cp [erg/mol-K] (KINGetGasMixtureSpecificHeat x WTM, mixture.py:1646)."""
         return self._rop_thermo()[1] * self.WTM

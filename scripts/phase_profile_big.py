@@ -27,7 +27,7 @@ def main():
     dm = _native.DeviceMechanism(m.to_tables(), device=0)
     T0, P0, Y0, prob = bench.sweep_c5(m, 1, 0)
     idx = np.arange(0, len(T0), max(1, len(T0) // n))[:n]
-    buf = torch.zeros((len(idx), 8), dtype=torch.int64, device="cuda")
+    buf = torch.zeros((len(idx), 16), dtype=torch.int64, device="cuda")
     L = _native.lib()
     L.ckmi_debug_big_phase_buffer.argtypes = [ct.c_void_p]
     assert L.ckmi_debug_big_phase_buffer(buf.data_ptr()) == 0
@@ -48,11 +48,12 @@ def main():
             d["calls_per_step"] = calls[nm].sum() / st[:, 0].sum()
         out["phases"][nm] = d
     fac = ph[:, 3].sum()
-    # wave 0's view of the factorisation.  MFMA panels: [owner panel work, barrier wait, rest =
-    # pivot-row gather + MFMA update]; VALU build (CKMI_BIG_VALU): [pivot search, publish, update]
-    out["factor_split"] = {"part0": ph[:, 6].sum() / fac, "part1_barrier": ph[:, 7].sum() / fac,
-                           "rest_update": 1.0 - (ph[:, 6].sum() + ph[:, 7].sum()) / fac,
-                           "cycles_per_gj_step": fac / max(calls["factor"].sum(), 1) / (16 * ((m.KK + 16) // 16))}
+    # wave 0's view of the factorisation (MFMA panels): own panel work, barrier wait, pivot-row gather,
+    # B loads + MFMA update, owner column restore (VALU build CKMI_BIG_VALU: search, publish, update)
+    names_f = ["own_panels", "barrier", "-", "pivot_row_gather", "mfma_update", "restore"]
+    out["factor_split"] = {nm: ph[:, 6 + k].sum() / fac for k, nm in enumerate(names_f) if nm != "-"}
+    npan = max(calls["factor"].sum(), 1) * ((m.KK + 1 + 3) // 4)
+    out["factor_split"]["cycles_per_panel"] = {nm: ph[:, 6 + k].sum() / npan for k, nm in enumerate(names_f) if nm != "-"}
     other = tot - ph[:, :5].sum()
     out["phases"]["control"] = {"frac_of_total": other / tot, "cycles_per_step": other / st[:, 0].sum()}
     print(json.dumps(out, indent=1))

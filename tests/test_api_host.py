@@ -192,3 +192,28 @@ def test_afactor_get_set(chem):
 def test_make_cfg_rejects_long_profiles():
     with pytest.raises(ValueError):
         _native.make_cfg(profile=(np.arange(70.0), np.ones(70)))
+
+
+def test_static_rate_calls_check_arguments(chem):
+    """Mixture.rate_of_production / reaction_rates (mixture.py:1353-1567) take the reference's signature and
+    its argument checks (raised here instead of exit()); use_idealgas_law is the ideal-gas state."""
+    import inspect
+
+    M = ck.Mixture
+    assert list(inspect.signature(M.rate_of_production).parameters) == ["chemID", "p", "t", "frac", "wt", "mode"]
+    assert list(inspect.signature(M.reaction_rates).parameters) == ["chemID", "numbreaction", "p", "t", "frac",
+                                                                    "wt", "mode"]
+    x = np.full(chem.KK, 1.0 / chem.KK)
+    with pytest.raises(ck.mixture.MixtureError, match="invalid chemistry"):
+        M.rate_of_production(-1, P_ATM, 1000.0, x, chem.WT, "mole")
+    with pytest.raises(ck.mixture.MixtureError, match="pressure"):
+        M.rate_of_production(chem.chemID, 0.0, 1000.0, x, chem.WT, "mole")
+    with pytest.raises(ck.mixture.MixtureError, match="same size"):
+        M.rate_of_production(chem.chemID, P_ATM, 1000.0, x[:-1], chem.WT, "mole")
+    with pytest.raises(ck.mixture.MixtureError, match='"mole" or "mass"'):
+        M.reaction_rates(chem.chemID, chem.IIGas, P_ATM, 1000.0, x, chem.WT, "volume")
+    with pytest.raises(ck.mixture.MixtureError, match="numbreaction"):
+        M.reaction_rates(chem.chemID, chem.IIGas - 1, P_ATM, 1000.0, x, chem.WT, "mole")
+    air = ck.Mixture(chem)
+    air.use_idealgas_law()
+    assert air.userealgas is False

@@ -131,3 +131,36 @@ def test_adiabatic_mixing_golden_on_gpu(chem):
     T = np.array([premixed.temperature, ar.temperature, diluted.temperature])
     assert np.all(within(T, g["state-temperature"], *g["tolerance-var"]))
     assert np.all(within(diluted.X, g["species-diluted_mole_fraction"], *g["tolerance-frac"]))
+
+
+def test_static_rate_calls_match_mixture_methods(chem, mech):
+    """Mixture.rate_of_production / reaction_rates (mixture.py:1353-1567) with the reference's signature give
+    the numbers of the instance methods ROP() / RxnRates() on the same state (same kernels; the static forms
+    renormalise the given fractions, so they agree to that rounding), for mole and mass input; the
+    reactionrates golden through the static call."""
+    import pychemkin_amd as ck
+
+    M = ck.Mixture
+    m = M(chem)
+    m.temperature, m.pressure = 1500.0, 2 * P_ATM
+    m.X = [("CH4", 0.05), ("O2", 0.2), ("N2", 0.7), ("OH", 0.01), ("H", 0.01), ("CO", 0.03)]
+    w = m.ROP()
+    for frac, mode in ((m.X, "mole"), (m.Y, "mass")):
+        ws = M.rate_of_production(chem.chemID, m.pressure, m.temperature, frac, chem.WT, mode)
+        assert np.allclose(ws, w, rtol=1e-13, atol=1e-13 * np.max(np.abs(w)))
+    qf, qr = m.RxnRates()
+    qfs, qrs = M.reaction_rates(chem.chemID, chem.IIGas, m.pressure, m.temperature, m.Y, chem.WT, "mass")
+    assert np.allclose(qfs, qf, rtol=1e-13, atol=1e-13 * np.max(np.abs(qf)))
+    assert np.allclose(qrs, qr, rtol=1e-13, atol=1e-13 * np.max(np.abs(qr)))
+    # a state whose fractions are already normalised in floating point: bitwise the instance results
+    y = np.asarray(m.Y)
+    if y.sum() == 1.0:
+        assert np.array_equal(M.rate_of_production(chem.chemID, m.pressure, m.temperature, y, chem.WT, "mass"),
+                              m.ROP())
+    # the reactionrates golden (1800 K, 5 atm, CH4/air phi = 1 as mass fractions): net rates of the top 5
+    g = golden("reactionrates")
+    y0 = ch4_air_Y(mech, 1.0)[0]
+    qf, qr = M.reaction_rates(chem.chemID, chem.IIGas, 5 * P_ATM, 1800.0, y0, chem.WT, "mass")
+    order, net = M._sorted_nonzero(qf - qr, 0.0)
+    assert order.tolist() == g["state-order_1800"]
+    assert np.all(within(net, g["rate-net_reaction_rate_1800"], *g["tolerance-ROP"]))

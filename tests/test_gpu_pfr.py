@@ -171,3 +171,27 @@ def test_start_position_with_pressure_profile(chem):
     rho_out = a._final["P"] / (ck.constants.R_GAS * a._final["T"]) / np.sum(a._final["Y"] / chem.WT)
     rho_in = P_IN / (ck.constants.R_GAS * T_IN) / np.sum(a.reactormixture.Y / chem.WT)
     assert abs(a._final["V"] / (rho_in * U_IN / rho_out) - 1) < 1e-10
+
+
+@pytest.mark.parametrize("path", [0, 1])  # 0: wave kernel; 1: workgroup kernel forced
+def test_choked_tube_ends_with_status_5(dm_gri, oracle, mech, path):
+    """A tube driven past the choke point of the momentum equation ends with CKMI_RUN_CHOKED (5) in both
+    kernels, at the oracle's stop position and state; a slower tube in the same launch runs to the end."""
+    from pychemkin_amd import _native
+    from test_pfr import choked_tube
+
+    T0, P0, u0, Y0, W0 = choked_tube(mech)
+    run = dict(energy=1, t_end=300.0, atol=1e-12, rtol=1e-8)
+    _native.set_reactor_path(path)
+    try:
+        res = {k: v.cpu().numpy() for k, v in dm_gri.reactor_run(
+            _native.make_cfg(**run), np.array([3, 3], np.int32), np.array([T0, T0]), np.array([P0, P0]),
+            np.array([u0, 0.5 * u0]), np.stack([Y0, Y0])).items()}
+    finally:
+        _native.set_reactor_path(0)
+    assert list(res["stats"][:, 6]) == [5, 0]
+    r, Ye = oracle.reactor(T0, P0, u0, Y0, problem=3, **run)
+    assert r.status == 5
+    assert abs(res["t_stop"][0] / r.t_end - 1) < 1e-3
+    assert abs(res["T"][0] / r.T - 1) < 1e-3
+    assert np.all(np.isfinite(res["P"])) and np.all(np.isfinite(res["V"]))

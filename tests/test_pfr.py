@@ -142,3 +142,35 @@ def test_pfr_inputs_validated(chem):
     r.timestep_for_saving_solution = 0.0005
     xs = r._save_grid(LENGTH, U_IN)
     assert len(xs) == 373 and np.allclose(xs, golden("plugflow")["state-distance"], rtol=0, atol=1e-12)
+
+
+def choked_tube(mech):
+    """CH4/air at 1500 K, 1 atm entering at half the isothermal sound speed: subsonic at the inlet, but
+    the momentum equation's subsonic root vanishes once T W0 / (T0 W) exceeds (1 + M^2)^2 / (4 M^2) =
+    1.5625, well before the burned state (round-4 verdict: a choking guard instead of a NaN)."""
+    from conftest import ch4_air_Y
+    from pychemkin_amd.constants import R_GAS
+
+    T0, P0 = 1500.0, P_ATM
+    Y0 = ch4_air_Y(mech, 1.0)[0]
+    W0 = 1.0 / np.sum(Y0 / mech.wt)
+    u0 = 0.5 * np.sqrt(R_GAS * T0 / W0)
+    return T0, P0, u0, Y0, W0
+
+
+def choke_theta(M2):
+    return (1.0 + M2) ** 2 / (4.0 * M2)
+
+
+def test_oracle_choked_tube_ends_with_status_5(oracle, mech):
+    T0, P0, u0, Y0, W0 = choked_tube(mech)
+    res, Ye = oracle.reactor(T0, P0, u0, Y0, problem=3, energy=1, t_end=300.0, atol=1e-12, rtol=1e-8)
+    assert res.status == 5  # CKMI_RUN_CHOKED
+    assert 0.0 < res.t_end < 300.0
+    W = 1.0 / np.sum(Ye / mech.wt)
+    theta = res.T * W0 / (T0 * W)
+    assert theta > choke_theta(0.25)  # the first accepted state past the choke point
+    assert theta < 1.1 * choke_theta(0.25)
+    # the same tube at half the speed (M = 0.25: choke at 4.5) stays subsonic to the burned state
+    r2, _ = oracle.reactor(T0, P0, 0.5 * u0, Y0, problem=3, energy=1, t_end=300.0, atol=1e-12, rtol=1e-8)
+    assert r2.status == 0
