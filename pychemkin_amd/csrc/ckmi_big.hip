@@ -562,7 +562,7 @@ struct BigMatrixM {
     const int ti = lane & 15, q = lane >> 4;
     const int k0 = 16 * C + 4 * wo;
     double* Pb = lds_at<double>(L.xpart) + par * 4 * NC;             // [4 s][NC] P of the panel
-    double* Rb = lds_at<double>(L.xpart) + 8 * NC + wid * 16 * NB;  // [4 s][NB c][4 q] pivot rows, per wave
+    double* Rb = lds_at<double>(L.xpart) + 8 * NC + wid * 16 * NB;  // [4 s][4 q][NB c] pivot rows, per wave
     PanHdr* hdr = lds_at<PanHdr>(L.phdr) + par;
 #ifndef CKMI_BIG_PANEL_COLS
     if (wid == wo) {
@@ -715,19 +715,38 @@ struct BigMatrixM {
 #pragma unroll
     for (int s = 0; s < 4; ++s) pr[s] = __builtin_amdgcn_readfirstlane(hdr->p[s]);
     if (!__builtin_amdgcn_readfirstlane(hdr->ok)) ok = false;
-    // the 4 pivot rows' entries of this wave's columns (values before the panel), wave-locally
+    // the 4 pivot rows' entries of this wave's columns (values before the panel), wave-locally, into
+    // Rb[s][q][c] (one base address per lane, compile-time offsets).  The row's register block rp is
+    // wave-uniform: the diagonal block C (natural pivots, the common case: 90-97 % of the steps of the
+    // stand-in's Newton matrices at small gamma) is a static register index, any other block goes
+    // through a scalar branch tree
+    // (64-bit inline-asm stores from one address register: the compiler otherwise materialises an
+    // address per column and parks them in AGPRs; one wave's LDS operations complete in issue order,
+    // so the reads after wave_lds_sync see them)
+    const uint32_t rbq = (uint32_t)(uintptr_t)(Rb + q * NB);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int tip = pr[s] & 15, rp = pr[s] >> 4;
       mark_done(dm, pr[s]);
+      if (rp == C) {
+        if (ti == tip) {
 #pragma unroll
-      for (int r = 0; r < NB; ++r) {
-        if (r == rp) {  // uniform: one scalar branch selects the register row
-          if (ti == tip) {
+          for (int c = 0; c < NB; ++c)
+            asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[C][c >> 2][c & 3]),
+                         "i"(8 * (s * 4 * NB + c)) : "memory");
+        }
+      } else {
 #pragma unroll
-            for (int c = 0; c < NB; ++c) Rb[(s * NB + c) * 4 + q] = a[r][c >> 2][c & 3];
+        for (int r = 0; r < NB; ++r) {
+          if (r != C && r == rp) {  // uniform: one scalar branch selects the register row
+            if (ti == tip) {
+#pragma unroll
+              for (int c = 0; c < NB; ++c)
+                asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[r][c >> 2][c & 3]),
+                             "i"(8 * (s * 4 * NB + c)) : "memory");
+            }
+            asm volatile("" ::: "memory");
           }
-          asm volatile("" ::: "memory");
         }
       }
     }
@@ -735,10 +754,11 @@ struct BigMatrixM {
     PPH(3);
     // A = U^T (lane: column j = lane & 15 of the group, panel step lane >> 4), B = P'^T
     double A[NG];
+    {
+      const int j = lane & 15;
+      const double* ra = Rb + ((lane >> 4) * 4 + (j & 3)) * NB + (j >> 2);
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      const int j = lane & 15, c = 4 * g + (j >> 2);
-      A[g] = c < NB ? Rb[((lane >> 4) * NB + c) * 4 + (j & 3)] : 0.0;
+      for (int g = 0; g < NG; ++g) A[g] = 4 * g + (j >> 2) < NB ? ra[4 * g] : 0.0;
     }
     const int sl = lane >> 4;
     const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));  // pivot row of step sl
@@ -785,7 +805,11 @@ struct BigMatrixM {
   __device__ __forceinline__ void panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                          int lane FPH_PARAM) {
     if constexpr (C < NB) {
+#ifdef CKMI_BIG_UNROLL_WO  // A/B: the four owners' panels as straight-line code (4x the factorisation code)
+#pragma unroll
+#else
 #pragma unroll 1
+#endif
       for (int wo = 0; wo < 4; ++wo)
         if (16 * C + 4 * wo < n) panel<C>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
       panels<C + 1>(L, n, dm, ok, t, wid, lane FPH_ARG);

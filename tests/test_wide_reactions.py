@@ -165,9 +165,15 @@ def test_gpu_wide_reactors(wmech, worc, wdm, path):
     for i in range(len(cases)):
         r, Ye = worc.reactor(T0[i], P0[i], 1.0, Y0[i], problem=int(prob[i]), **run)
         assert r.status == 0 and res["stats"][i, 6] == 0
-        # tau: 1e-4 in round 3; 1.5e-4 on one case after the round-4 lane order of the reaction strips (the
-        # wdot summation order moved at rounding level; the north_star bar is 5e-3)
-        assert abs(res["tau"][i] / r.tau - 1) < 3e-4 and abs(res["T"][i] / r.T - 1) < 1e-4
+        # tau within 1e-4 of the oracle's own envelope under a +-1 % perturbation of rtol (11 runs): the
+        # step sequence of an adaptive BDF is chaotic at rounding level, so the device (another summation
+        # order of wdot) lands anywhere the oracle itself lands.  Measured envelopes (rel. to rtol = 1e-8):
+        # 1e-6 wide for three cases; -1.7e-4 / +3.8e-4 for the 5.3 us ignition at 1600 K, 40 atm, phi 1.5,
+        # whose device tau is 1.5e-4 off the unperturbed oracle run
+        env = [worc.reactor(T0[i], P0[i], 1.0, Y0[i], problem=int(prob[i]), **dict(run, rtol=run["rtol"] * f))[0].tau
+               for f in np.linspace(0.99, 1.01, 11)]
+        assert min(env) * (1 - 1e-4) <= res["tau"][i] <= max(env) * (1 + 1e-4)
+        assert abs(res["T"][i] / r.T - 1) < 1e-4
         for sp in ("CH4", "O2", "H2O", "CO2", "CO", "C2H6"):
             k = wmech.species.index(sp)
             assert abs(res["Y"][i, k] - Ye[k]) <= 1e-4 * max(abs(Ye[k]), 1e-3)
