@@ -228,11 +228,13 @@ def reactor_roofline(ops, stats, kern_s, kernel, traffic_key, n):
             "flops_per_launch": flops, "flops_per_reactor": flops / n, "kernel_ms": kern_s * 1e3}
 
 
-def cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau_gpu, seconds, max_sample, single=True):
+def cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau_gpu, seconds, max_sample, single=True, run=None):
     """Oracle C restatement (OpenMP over reactors) on a random subset of a strided sample of the same
-    sweep, in chunks until ~seconds of CPU work; plus the same oracle on one core."""
+    sweep, in chunks until ~seconds of CPU work; plus the same oracle on one core.  run: the oracle's
+    configuration when it is not the bench's RUN (plug-flow tubes, engine cylinders)."""
     from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
 
+    run = RUN if run is None else run
     orc = Oracle(mech)
     n = len(T0)
     stride = max(1, n // max_sample)
@@ -244,10 +246,12 @@ def cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau_gpu, seconds, max_sample, s
         idx = order[done: done + chunk]
         tc = time.perf_counter()
         _, cres, _ = orc.reactor_batch(T0[idx], P0[idx], Y0[idx], problem=prob[idx], V0=np.ones(len(idx)),
-                                       nthreads=threads, **RUN)
+                                       nthreads=threads, **run)
         tcpu += time.perf_counter() - tc
         ctau = np.array([r.tau for r in cres])
-        dmax = max(dmax, float(np.max(np.abs(tau_gpu[idx] / ctau - 1))))
+        ok = ctau > 0
+        if ok.any():
+            dmax = max(dmax, float(np.max(np.abs(tau_gpu[idx][ok] / ctau[ok] - 1))))
         done += len(idx)
     out = {"value": done / tcpu, "unit": "reactors/s", "cores": threads, "kind": "port", "host": host_info(),
            "sample": f"{done} reactors (random subset of every {stride}th reactor of this GPU's sweep), "
@@ -256,7 +260,7 @@ def cpu_reactor_baseline(mech, T0, P0, Y0, prob, tau_gpu, seconds, max_sample, s
     if single:
         idx1 = order[: max(4, min(32, order.size))]
         tc = time.perf_counter()
-        orc.reactor_batch(T0[idx1], P0[idx1], Y0[idx1], problem=prob[idx1], V0=np.ones(len(idx1)), nthreads=1, **RUN)
+        orc.reactor_batch(T0[idx1], P0[idx1], Y0[idx1], problem=prob[idx1], V0=np.ones(len(idx1)), nthreads=1, **run)
         out["single_core_value"] = len(idx1) / (time.perf_counter() - tc)
         out["single_core_sample"] = f"{len(idx1)} reactors of the same sample, 1 thread"
     return out
@@ -415,6 +419,7 @@ def model_line(kind, dm, dev, mech, ops, world, rank, args):
     if kind == "pfr":  # configs[2]-like tubes: 1 cm at 1 cm/s inlet velocity = 1 s of residence
         T0, P0, Y0 = model_sweep(mech, world, rank, total, 1100.0, 1700.0, P_ATM, 100 * P_ATM, 0.5, 2.0)
         cfg = _native.make_cfg(**RUN)
+        orc_run = RUN
         workload = (f"plug-flow tubes: GRI-3.0 CH4/air, {total} tubes in total (16 T0 1100-1700 K x 16 phi x 16 P "
                     "1-100 atm), 1 cm at 1 cm/s, momentum equation on, TIFP")
     else:
@@ -428,6 +433,7 @@ def model_line(kind, dm, dev, mech, ops, world, rank, args):
         # cylinders stall in the expansion stroke on the GPU
         run = dict(RUN, t_end=258.0 / 6000.0, nneg=True)
         cfg = _native.make_cfg(engine=hcci_block(), tran=tran, **run)
+        orc_run = dict(run, engine=hcci_block(), tran=fits)
         workload = (f"HCCI cylinders: GRI-3.0 CH4/air, {round(total ** (1 / 3)) ** 3} in total (T_IVC 420-520 K x "
                     "phi 0.3-1 x P_IVC 1-2 atm), the hcciengine golden's engine, ICHX/Woschni wall heat, -142..116 CA, NNEG")
     code = 3 if kind == "pfr" else 4
@@ -446,13 +452,18 @@ def model_line(kind, dm, dev, mech, ops, world, rank, args):
     tot = int(tot.item())
     unit = "tubes/s" if kind == "pfr" else "cylinders/s"
     del sh, res
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_reactor_baseline(mech, np.asarray(T0), np.asarray(P0), np.asarray(Y0), np.full(len(T0), code, np.int32),
+                                   tau, args.cpu_seconds_secondary, args.cpu_sample, single=True, run=orc_run)
+        cpu["unit"] = unit
     return {"metric": f"{'plug-flow reactor' if kind == 'pfr' else 'engine cycle'} integrations/sec ({workload})",
             "value": tot / tmax, "unit": unit, "total": tot, "per_gpu": len(T0), "seconds": tmax, "scaling": "strong",
             "failed": int((stats[:, 6] != 0).sum()), "runaway": int((stats[:, 6] == 4).sum()), "not_ignited": not_ign,
             "solver": solver_summary(stats),
             "roofline": reactor_roofline(ops, stats, float(np.mean(kern_ms)) / 1e3, "reactor_kernel<54, false, true>",
-                                         None, len(T0)),
-            "cpu_baseline": None}
+                                         f"reactor_{kind}", len(T0)),
+            "cpu_baseline": cpu}
 
 
 def _free_port():
@@ -604,7 +615,7 @@ def main():
         bops = count_ops(bm.to_tables())
         bdm = _native.DeviceMechanism(bm.to_tables(), device=dev)
         c5 = secondary_sweep("c5", bdm, dev, bm, bops, sweep_c5, world, rank, args, "big_reactor_kernel<11>",
-                             "big_reactor",
+                             "big_reactor_c5",
                              "configs[4] stand-in: 161-species GRI-3.0 + 108-tracer mechanism (no n-heptane mechanism "
                              "offline; parity with Chemkin unpinned), 64 T0 x 64 phi x 64 P = 262,144 CONP reactors in "
                              "total", "strong")

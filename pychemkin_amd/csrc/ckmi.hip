@@ -1264,7 +1264,10 @@ void assign_lanes(const ckmi_mech_desc* d, std::vector<int>& slots, const std::v
     return st;
   };
   double temp = 2.0;
-  const int iters = 400 * n;
+  // 400 proposals per slot, capped at 1024 slots' worth: mechanisms of thousands of reactions would
+  // otherwise spend seconds of host time per ckmi_mech_create (round-4 advice); the GRI-3.0 (384 slots)
+  // and 161-species (512) images are annealed exactly as before
+  const int iters = 400 * std::min(n, 1024);
   for (int it = 0; it < iters; ++it, temp = std::max(0.05, temp * (1.0 - 6.0 / iters))) {
     const int a = (int)(rnd() % n);
     if (slots[a] < 0) continue;

@@ -177,12 +177,17 @@ __device__ __forceinline__ double bwrms(Blk& B, double v, double ewt, int n, int
 // over b.  After factor(), a[][] holds the explicit inverse of the row-permuted matrix: with p_k
 // the pivot row of step k, x_k = sum_j B[p_k][j] b[p_j].
 //
-// J slot layout (written by rhs_big, read by build): element (i, j) at
-// ((i / 16) NB + j / 16) NT + 64 ((j % 16) / 4) + i % 16 + 16 (j % 4) -- a build loads it coalesced.
+// J slot layout (written by rhs_big, read by build): thread t = 64 w + ti + 16 q holds element
+// (i, j) = (ti + 16 r, 16 c + 4 w + q) of the matrix as its k-th value, k = r NB + c; the slot stores
+// the values in float4 chunks [k / 4][t][k % 4], so a build loads its 121 values with 31 coalesced
+// 16-byte loads (one 4-byte load per value before round 5).
+__device__ __forceinline__ int jidx(int k, int t) { return (((k >> 2) * NT + t) << 2) + (k & 3); }
 __device__ __forceinline__ int jslot(int i, int j, int NB) {
   const int s = j & 15;
-  return ((i >> 4) * NB + (j >> 4)) * NT + ((s >> 2) << 6) + (i & 15) + ((s & 3) << 4);
+  const int t = ((s >> 2) << 6) + (i & 15) + ((s & 3) << 4);
+  return jidx((i >> 4) * NB + (j >> 4), t);
 }
+__host__ __device__ constexpr int jslot_floats(int NB) { return (NB * NB + 3) / 4 * 4 * NT; }
 
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp_mov_u64(uint64_t v) {
@@ -248,7 +253,7 @@ struct BigMatrix {
 #pragma unroll
       for (int c = 0; c < NB; ++c) {
         const int i = ti + 16 * r, j = 16 * c + 4 * w + q;
-        const double jv = (i < n && j < n) ? (double)J[(r * NB + c) * NT + t] : 0.0;
+        const double jv = (i < n && j < n) ? (double)J[jidx(r * NB + c, t)] : 0.0;
         a[r][c] = (i == j ? 1.0 : 0.0) - gamma * jv;
       }
     }
@@ -520,6 +525,17 @@ struct BigMatrixM {
     const int t = opaque_lane(tid);
     const int lane = t & 63, w = t >> 6;
     const int ti = lane & 15, q = lane >> 4;
+    constexpr int NK = (NB * NB + 3) / 4;  // float4 chunks of this thread's values (jidx)
+    float jv[4 * NK];
+    const float4* J4 = reinterpret_cast<const float4*>(J);
+#pragma unroll
+    for (int kk = 0; kk < NK; ++kk) {
+      const float4 v = J4[kk * NT + t];
+      jv[4 * kk] = v.x;
+      jv[4 * kk + 1] = v.y;
+      jv[4 * kk + 2] = v.z;
+      jv[4 * kk + 3] = v.w;
+    }
 #pragma unroll
     for (int r = 0; r < NB; ++r) {
 #pragma unroll
@@ -527,8 +543,8 @@ struct BigMatrixM {
         const int i = ti + 16 * r, j = 16 * c + 4 * w + q;
         double v = 0.0;
         if (c < NB) {
-          const double jv = (i < n && j < n) ? (double)J[(r * NB + c) * NT + t] : 0.0;
-          v = (i == j ? 1.0 : 0.0) - gamma * jv;
+          const double jvv = (i < n && j < n) ? (double)jv[r * NB + c] : 0.0;
+          v = (i == j ? 1.0 : 0.0) - gamma * jvv;
         }
         a[r][c >> 2][c & 3] = v;
       }
@@ -579,6 +595,15 @@ struct BigMatrixM {
 #pragma unroll
         for (int s = 0; s < 4; ++s) y[j][s] = row < NC ? Pb[s * NC + row] : 0.0;
       }
+#ifdef CKMI_PHASE_TIMERS
+      {  // the transposed columns have landed before the stamp
+        double chk = 0.0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) chk += y[j][0];
+        if (chk == 12345.678) fph[2] += 1;
+      }
+#endif
+      PPH(2);
       int ps[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -762,6 +787,29 @@ struct BigMatrixM {
     }
     const int sl = lane >> 4;
     const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));  // pivot row of step sl
+    // Issue order (A/B, CKMI_BIG_MFMA_GROUP_FIRST): accumulator group G (tiles 4G .. 4G + 3, among them
+    // tile C, the next panel's) for every row block first, then the other groups, so that the next
+    // panel's owner would wait for 11 MFMAs only and the other 22 would run beside its pivot steps.
+    // Measured 1.3 % slower (509 vs 503 ms on 2,048 configs[4] reactors, bitwise the same results): at the
+    // wo loop's back-edge the compiler moves ~40 accumulator registers between AGPRs and VGPRs, which
+    // waits for every MFMA anyway.  Row-block-major order stays.
+#ifdef CKMI_BIG_MFMA_GROUP_FIRST
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+      const int i = 16 * rb + (lane & 15);
+      const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
+      a[rb][G] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[G], Bv, a[rb][G], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);  // keep the issue order: the scheduler may not mix the two loops
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+      const int i = 16 * rb + (lane & 15);
+      const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+        if (g != G) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
+    }
+#else  // A/B reference: row-block-major issue order
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
       const int i = 16 * rb + (lane & 15);
@@ -769,6 +817,7 @@ struct BigMatrixM {
 #pragma unroll
       for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
     }
+#endif
 #ifdef CKMI_PHASE_TIMERS
     {  // the MFMA results have landed before the stamp
       double chk = 0.0;
@@ -805,11 +854,7 @@ struct BigMatrixM {
   __device__ __forceinline__ void panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                          int lane FPH_PARAM) {
     if constexpr (C < NB) {
-#ifdef CKMI_BIG_UNROLL_WO  // A/B: the four owners' panels as straight-line code (4x the factorisation code)
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
+#pragma unroll 1  // (fully unrolled: 4x the code, and the ROCm 7.2 backend crashes in AMDGPU Rewrite AGPR-Copy-MFMA)
       for (int wo = 0; wo < 4; ++wo)
         if (16 * C + 4 * wo < n) panel<C>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
       panels<C + 1>(L, n, dm, ok, t, wid, lane FPH_ARG);
@@ -1205,7 +1250,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
   Ign& g = *lds_at<Ign>(oc + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)));
   RunCtx& R = *lds_at<RunCtx>(oc + align16((int)sizeof(BdfS)) + align16((int)sizeof(Ctl)) + align16((int)sizeof(Ign)));
   R.cfg = cfg;
-  float* Jg = jws + (size_t)blockIdx.x * NB * NB * NT;
+  float* Jg = jws + (size_t)blockIdx.x * jslot_floats(NB);
   double* Dg = dws + (size_t)blockIdx.x * NDQ * img.IIp;
   const int KK = V.KK;
   const int n = KK + 1;
@@ -1978,7 +2023,7 @@ int launch_big_nc(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO& 
   BIG_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, big_reactor_kernel<NB, PL>, NT, L.bytes));
   if (per_cu < 1) return set_error(CKMI_ERR_SIZE, "workgroup-per-reactor kernel does not fit on a CU");
   const int grid = std::max(1, std::min(ncu * per_cu, n));
-  const size_t jbytes = ((size_t)grid * NB * NB * NT * sizeof(float) + 255) & ~(size_t)255;
+  const size_t jbytes = ((size_t)grid * jslot_floats(NB) * sizeof(float) + 255) & ~(size_t)255;
   const size_t dbytes = ((size_t)grid * NDQ * m->img.IIp * sizeof(double) + 255) & ~(size_t)255;
   const size_t cbytes = (sizeof(DevCfg) + 255) & ~(size_t)255;
   void* ws = nullptr;
@@ -2012,9 +2057,13 @@ int launch_big_reactors(const ckmi_mech* m, int n, const DevCfg& dc, const React
   if (m->has_plog) {
     // PLOG, chemically activated and general (FORD / RORD / fractional) reactions: the extended
     // variant, compiled for three matrix sizes (a mechanism runs in the smallest that holds it)
+#ifdef CKMI_BIG_ONLY_NB
+    return set_error(CKMI_ERR_UNSUPPORTED, "diagnostic build: no extended variants");
+#else
     if (nvar <= 128) return launch_big_nc<8, true>(m, n, dc, io, stream);
     if (nvar <= 176) return launch_big_nc<11, true>(m, n, dc, io, stream);
     return launch_big_nc<12, true>(m, n, dc, io, stream);
+#endif
   }
   switch ((nvar + 15) / 16) {  // NB: register blocks per dimension (NC = 16 NB >= n)
     case 1:

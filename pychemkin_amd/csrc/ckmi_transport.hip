@@ -120,8 +120,10 @@ __global__ void mixture_viscosity_kernel(int KK, int n, const double* __restrict
   const double x = log(T[ii]);
   // x_k = Y_k / W_k: the Wilke ratio is homogeneous of degree 0 in X, so the normalisation
   // sum_j x_j cancels between each numerator and its denominator
+  // negative trace mass fractions (integrator output) count as 0, as in the engine's wall-heat path
+  // (ckmi_reactor.hpp engine_hA)
   for (int k = 0; k < KK; ++k) {
-    const double xk = Y[(size_t)k * n + ii] / wt[k];
+    const double xk = fmax(Y[(size_t)k * n + ii], 0.0) / wt[k];
     Xs[k * bs] = xk;
     const double* a = fits + 4 * k;
     Rs[k * bs] = exp(-0.5 * fma(x, fma(x, fma(x, a[3], a[2]), a[1]), a[0]));
@@ -144,7 +146,7 @@ __global__ void mixture_viscosity_kernel(int KK, int n, const double* __restrict
   if (live) visc[i] = mix;
 }
 
-// one state per lane: X_k = (Y_k / W_k) / sum_j Y_j / W_j, lambda_k = exp(poly_k(ln T)),
+// one state per lane: X_k = (Y_k^+ / W_k) / sum_j Y_j^+ / W_j (Y^+ = max(Y, 0)), lambda_k = exp(poly_k(ln T)),
 // lambda = (sum_k X_k lambda_k + 1 / sum_k X_k / lambda_k) / 2 (Chemkin's mixture-averaged rule, the
 // form the engine's wall heat transfer evaluates in ckmi_reactor.hpp).  Species with X_k = 0 add
 // nothing to either sum.  KK x (2 FLOP + exp) per state: FP64 VALU / transcendental bound.
@@ -156,7 +158,7 @@ __global__ void mixture_conductivity_kernel(int KK, int n, const double* __restr
   const double x = log(T[i]);
   double sx = 0.0, sxl = 0.0, sxr = 0.0;
   for (int k = 0; k < KK; ++k) {
-    const double xk = Y[(size_t)k * n + i] / wt[k];
+    const double xk = fmax(Y[(size_t)k * n + i], 0.0) / wt[k];  // negative traces count as 0 (engine_hA)
     if (xk == 0.0) continue;
     const double* a = cfits + 4 * k;
     const double lk = exp(fma(x, fma(x, fma(x, a[3], a[2]), a[1]), a[0]));

@@ -70,10 +70,29 @@ vf = trf.viscosity_fits(wt, pl, 3500.0)
 cf = trf.conductivity_fits(wt, pl, mech.to_tables()["thermo"], 3500.0)
 
 
-def props(Tv):
-    mu = trf.mixture_viscosity(Tv, np.tile(X, (len(Tv), 1)), wt, vf)
-    lam = trf.mixture_conductivity(Tv, np.tile(X, (len(Tv), 1)), cf)
+def props(Tv, Xp=None):
+    Xp = X if Xp is None else Xp
+    mu = trf.mixture_viscosity(Tv, np.tile(Xp, (len(Tv), 1)), wt, vf)
+    lam = trf.mixture_conductivity(Tv, np.tile(Xp, (len(Tv), 1)), cf)
     return mu, lam
+
+
+def comp(pairs):
+    x = np.zeros(mech.KK)
+    for sname, v in pairs:
+        x[mech.species.index(sname)] = v
+    return x / x.sum()
+
+
+# property compositions tried for the uniform residual (round-4 verdict item 4): the charge (baseline),
+# air, and the fresh fuel-air charge without EGR (phi = 0.8 of the reference's fuel blend)
+_fuel = comp([("CH4", 0.9), ("C3H8", 0.05), ("C2H6", 0.05)])
+_A = mech.ncf.astype(float)
+_o2 = (_A[mech.elements.index("C")] @ _fuel + _A[mech.elements.index("H")] @ _fuel / 4
+       - _A[mech.elements.index("O")] @ _fuel / 2) / 0.21
+COMPS = {"charge": X, "air": comp([("O2", 0.21), ("N2", 0.79)]),
+         "fresh_no_egr": (0.8 * _fuel + _o2 * comp([("O2", 0.21), ("N2", 0.79)])) / (0.8 + _o2),
+         "N2": comp([("N2", 1.0)])}
 
 
 gam0 = cp_mol[0] / (cp_mol[0] - R_GAS)
@@ -90,6 +109,22 @@ for name, Tp in (("bulk", T), ("film", 0.5 * (T + e[11]))):
     h = e[8] * Re ** e[9] * Pr ** e[10] * lam / B
     out["hA_" + name] = (h * area).tolist()
     out["ratio_" + name] = (Q / (h * area * (T - e[11]))).tolist()
+# the uniform residual per property composition (film temperature), over the frozen-charge window
+# -132 .. -82 CA: mean ratio and its relative spread
+win = (ca >= -132.0) & (ca <= -82.0)
+summary = {}
+for name, Xp in COMPS.items():
+    mu, lam = props(0.5 * (T + e[11]), Xp)
+    Re = rho * w * B / mu
+    h = e[8] * Re ** e[9] * lam / B
+    r = (Q / (h * area * (T - e[11])))[win]
+    summary[name] = {"mean_ratio": float(r.mean()), "rel_spread": float(r.std() / r.mean()),
+                     "mu_rel_to_charge": float(np.mean(mu / props(0.5 * (T + e[11]))[0])),
+                     "lambda_rel_to_charge": float(np.mean(lam / props(0.5 * (T + e[11]))[1]))}
+out["composition_variants"] = summary
 out.update(T=T.tolist(), cp_rel_err=(cp_mol / cp_g - 1).tolist(), Q=Q.tolist(), area=area.tolist(), w=w.tolist(),
            V=V.tolist())
-json.dump(out, sys.stdout)
+if "--summary" in sys.argv:
+    json.dump(summary, sys.stdout, indent=1)
+else:
+    json.dump(out, sys.stdout)

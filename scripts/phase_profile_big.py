@@ -48,12 +48,13 @@ def main():
             d["calls_per_step"] = calls[nm].sum() / st[:, 0].sum()
         out["phases"][nm] = d
     fac = ph[:, 3].sum()
-    # wave 0's view of the factorisation (MFMA panels): own panel work, barrier wait, pivot-row gather,
-    # B loads + MFMA update, owner column restore (VALU build CKMI_BIG_VALU: search, publish, update)
-    names_f = ["own_panels", "barrier", "-", "pivot_row_gather", "mfma_update", "restore"]
-    out["factor_split"] = {nm: ph[:, 6 + k].sum() / fac for k, nm in enumerate(names_f) if nm != "-"}
+    # wave 0's view of the factorisation (MFMA panels): own panels (pivot steps + publication), barrier
+    # wait, own panels' entry + column transposition, pivot-row gather, B loads + MFMA update, owner column
+    # restore (VALU build CKMI_BIG_VALU: search, publish, update)
+    names_f = ["own_panel_steps", "barrier", "own_panel_entry", "pivot_row_gather", "mfma_update", "restore"]
+    out["factor_split"] = {nm: ph[:, 6 + k].sum() / fac for k, nm in enumerate(names_f) }
     npan = max(calls["factor"].sum(), 1) * ((m.KK + 1 + 3) // 4)
-    out["factor_split"]["cycles_per_panel"] = {nm: ph[:, 6 + k].sum() / npan for k, nm in enumerate(names_f) if nm != "-"}
+    out["factor_split"]["cycles_per_panel"] = {nm: ph[:, 6 + k].sum() / npan for k, nm in enumerate(names_f) }
     other = tot - ph[:, :5].sum()
     out["phases"]["control"] = {"frac_of_total": other / tot, "cycles_per_step": other / st[:, 0].sum()}
     print(json.dumps(out, indent=1))

@@ -1,6 +1,8 @@
 """Per-launch HBM bytes of the reactor and ROP kernels from scripts/pmc_traffic.sh output.
 
-    python scripts/traffic_summary.py gpurun_out/traffic_TAG [--c4]   (--c4: a run of the c4 line only)
+    python scripts/traffic_summary.py gpurun_out/traffic_TAG [--line c4|c5|pfr|hcci]
+      (a run of that bench line only: its kernel's largest dispatch is the line's launch -- the smaller
+      ones are the line's warm-up and the tiny headline run that always precedes it)
 
 FETCH_SIZE (KiB) is doubled per the gfx950 calibration (MI355X_MICROARCH.md, HBM section: it
 tallies 128-B requests at 64 B); WRITE_SIZE (KiB) is taken as is.  Output: profiles/traffic.json
@@ -17,8 +19,9 @@ import sys
 
 def main():
     root = sys.argv[1]
-    # reactor_kernel dispatches of a run belong to one line: c3 (default) or c4 (--c4)
-    reactor_key = "reactor_c4" if "--c4" in sys.argv else "reactor"
+    line = sys.argv[sys.argv.index("--line") + 1] if "--line" in sys.argv else ("c4" if "--c4" in sys.argv else "c3")
+    # reactor_kernel dispatches of a run belong to one line: c3 (default) or c4
+    reactor_key = "reactor_c4" if line == "c4" else "reactor"
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     grid = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
@@ -40,6 +43,18 @@ def main():
         for (kind, _, cname), v in per.items():
             acc[kind][cname].append(v)
     out = {}
+    # the line's own kernel and its key in profiles/traffic.json (largest dispatch only)
+    single = {"c4": ("reactor_c4", "reactor_c4"), "c5": ("big_reactor", "big_reactor_c5"),
+              "pfr": ("reactor_pfr_launch", "reactor_pfr"), "hcci": ("reactor_pfr_launch", "reactor_hcci")}.get(line)
+    if single is not None:
+        c = acc[single[0]]
+        fetch = 2.0 * 1024 * max(c["FETCH_SIZE"])
+        write = 1024 * max(c["WRITE_SIZE"])
+        units = {"c4": 2 ** 20, "c5": 262144, "pfr": 16 ** 3, "hcci": 25 ** 3}[line]  # bench.py model_line totals
+        out[single[1]] = {"bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+                          "dispatches": 1, "units": units}
+        print(json.dumps(out, indent=1))
+        return
     for kind, c in acc.items():
         if kind.startswith("reactor_c4"):  # the c4 run's tiny headline dispatches are dropped: largest dispatch only
             fetch = 2.0 * 1024 * max(c["FETCH_SIZE"])

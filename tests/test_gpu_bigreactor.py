@@ -158,3 +158,20 @@ def test_workgroup_kernel_deterministic(big):
           dm.reactor_run(cfg, prob[perm], T0[perm], P0[perm], np.ones(n), Y0[perm]).items() if not k.startswith("_")}
     for k in ("tau", "T", "P", "Y", "stats"):
         assert np.array_equal(r1[k][perm], r2[k]), k
+
+
+def test_mechanism_creation_time(big_mech, tables):
+    """Round-4 advice: ckmi_mech_create anneals the reaction-strip lane assignment on the host (400 proposals
+    per slot, capped at 1024 slots' worth).  Creation of the GRI-3.0 and 161-species device tables, the
+    annealing included, is timed and bounded."""
+    import time
+
+    from pychemkin_amd import _native
+
+    for name, t in (("gri30", tables), ("tracer161", big_mech.to_tables())):
+        t0 = time.perf_counter()
+        dm = _native.DeviceMechanism(t)
+        dt = time.perf_counter() - t0
+        dm.close()
+        print(f"ckmi_mech_create {name}: {dt * 1e3:.1f} ms")
+        assert dt < 2.0

@@ -196,7 +196,8 @@ def test_conductivity_golden_through_drop_in(chem_tr, mech, tr):
     assert np.max(np.abs(lam / (tr.species_viscosity(Ts, chem_tr.conductivity_fits)[:, k] * 1e-7) - 1)) < 1e-13
     gl = np.asarray(g["state-conductivity"])
     # measured: 79 of 100 within the golden's tolerance, <= 2.2e-3 (Conductivity)
-    assert within(lam, gl, *g["tolerance-var"]).sum() == 79
+    # (a lower bound on the match count and a bound on the error: a fit that improves parity must not fail)
+    assert within(lam, gl, *g["tolerance-var"]).sum() >= 79
     assert np.max(np.abs(lam / gl - 1)) < 2.5e-3
     m = ck.Mixture(chem_tr)
     m.temperature, m.pressure = 1500.0, P_ATM
@@ -238,3 +239,21 @@ def test_kin_conductivity(mech, chem_tr, tr):
         assert b"transport" in L.ckmi_kin_last_error()
     finally:
         kin.release(cs.value)
+
+
+def test_negative_trace_fractions_count_as_zero(chem_tr, mech):
+    """Round-4 advice: integrator output carries slightly negative trace mass fractions; the mixture viscosity
+    and conductivity kernels read them as 0, as the engine's wall-heat path does (engine_hA), so the result
+    is bitwise that of the clipped composition, positive and finite."""
+    dt = chem_tr.device_transport()
+    rng = np.random.default_rng(5)
+    Y = rng.dirichlet(np.ones(mech.KK), 8).T.copy()
+    Y[5, :] = -1e-12
+    Y[11, :] = -3e-9
+    Yc = np.maximum(Y, 0.0)
+    T = np.linspace(500.0, 2500.0, 8)
+    for fn in (dt.mixture_viscosity, dt.mixture_conductivity):
+        a = fn(T, Y).cpu().numpy()
+        b = fn(T, Yc).cpu().numpy()
+        assert np.all(np.isfinite(a)) and np.all(a > 0)
+        assert np.array_equal(a, b)
