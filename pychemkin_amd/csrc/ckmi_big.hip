@@ -748,11 +748,29 @@ struct BigMatrixM {
     // (64-bit inline-asm stores from one address register: the compiler otherwise materialises an
     // address per column and parks them in AGPRs; one wave's LDS operations complete in issue order,
     // so the reads after wave_lds_sync see them)
+    // All four pivot rows in the diagonal register block (the common case): every lane writes its row of
+    // that block (11 full-wave stores instead of 44 with 4 lanes each and 4 branches), and the A operand
+    // reads the pivot rows out of it.
+    double* Bk = lds_at<double>(L.xpart) + 8 * NC + BW * 16 * NB + wid * 64 * NB;  // [16 ti][4 q][NB c]
+    bool allc = true;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      mark_done(dm, pr[s]);
+      allc = allc && (pr[s] >> 4) == C;
+    }
+#ifdef CKMI_BIG_GATHER_ROWS
+    allc = false;  // A/B: the per-row gather only
+#endif
     const uint32_t rbq = (uint32_t)(uintptr_t)(Rb + q * NB);
+    if (allc) {
+      const uint32_t bkq = (uint32_t)(uintptr_t)(Bk + (ti * 4 + q) * NB);
+#pragma unroll
+      for (int c = 0; c < NB; ++c)
+        asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(bkq), "v"(a[C][c >> 2][c & 3]), "i"(8 * c) : "memory");
+    } else {
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int tip = pr[s] & 15, rp = pr[s] >> 4;
-      mark_done(dm, pr[s]);
       if (rp == C) {
         if (ti == tip) {
 #pragma unroll
@@ -775,18 +793,20 @@ struct BigMatrixM {
         }
       }
     }
+    }
     wave_lds_sync();
     PPH(3);
     // A = U^T (lane: column j = lane & 15 of the group, panel step lane >> 4), B = P'^T
+    const int sl = lane >> 4;
+    const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));  // pivot row of step sl
     double A[NG];
     {
       const int j = lane & 15;
-      const double* ra = Rb + ((lane >> 4) * 4 + (j & 3)) * NB + (j >> 2);
+      const double* ra = allc ? Bk + ((pl & 15) * 4 + (j & 3)) * NB + (j >> 2)
+                              : Rb + ((lane >> 4) * 4 + (j & 3)) * NB + (j >> 2);
 #pragma unroll
       for (int g = 0; g < NG; ++g) A[g] = 4 * g + (j >> 2) < NB ? ra[4 * g] : 0.0;
     }
-    const int sl = lane >> 4;
-    const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));  // pivot row of step sl
     // Issue order (A/B, CKMI_BIG_MFMA_GROUP_FIRST): accumulator group G (tiles 4G .. 4G + 3, among them
     // tile C, the next panel's) for every row block first, then the other groups, so that the next
     // panel's owner would wait for 11 MFMAs only and the other 22 would run beside its pivot steps.
@@ -1995,11 +2015,14 @@ BigLds big_layout(const ckmi_mech* m, int NC, int lds_max) {
   // the Jacobian column block takes what is left (multiple of BW columns, at most the matrix)
   const int LDJ = NT + 1;
   int jcb = (lds_max - align16(o) - 16) / (8 * LDJ);
-  if (8 * LDJ * jcb < 8 * NT * NBP && lds_max - align16(o) - 16 < 8 * NT * NBP) jcb = 0;  // xpart must fit
+  // xpart: the solve's partial sums [NT][NBP], or the factorisation's panel buffers [2][4][NC], per-wave
+  // pivot rows [BW][16 NB] and per-wave diagonal block rows [BW][64 NB] (BigMatrixM::panel)
+  const int xneed = 8 * std::max(NT * NBP, 8 * NC + BW * 16 * (NC / 16) + BW * 64 * (NC / 16));
+  if (8 * LDJ * jcb < xneed && lds_max - align16(o) - 16 < xneed) jcb = 0;  // xpart must fit
   jcb = std::min(jcb, (NC + BW - 1) / BW * BW);
   jcb = jcb / BW * BW;
   L.jcb = jcb;
-  L.jblk = take(std::max(8 * LDJ * std::max(jcb, 0), 8 * NT * NBP));
+  L.jblk = take(std::max(8 * LDJ * std::max(jcb, 0), xneed));
   L.xpart = L.jblk;  // solves never overlap a Jacobian assembly
   L.bytes = o;
   return L;
