@@ -4,11 +4,11 @@
 # kernel's dispatches belong to one line: c3 + rop + lu + rop161, then c4, c5, pfr and hcci alone;
 # then the per-line summaries are merged with profiles/traffic.json (the file bench.py reads) into
 # gpurun_out/traffic_merged.json, to be copied into profiles/ with the run's other results.
-# Usage: pmc_traffic.sh TAG [GROUPS]   (GROUPS: comma list of c3,c4,c5,pfr,hcci; default all)
+# Usage: pmc_traffic.sh TAG [GROUPS]   (GROUPS: comma list of c3,c4,c5,pfr,hcci,ropext; default all)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-dev}
-GROUPS_=${2:-c3,c4,c5,pfr,hcci}
+GROUPS_=${2:-c3,c4,c5,pfr,hcci,ropext}
 export TMPDIR=/tmp
 run() {  # run NAME LINES SUMMARY-FLAGS BENCH-FLAGS
   for c in FETCH_SIZE WRITE_SIZE; do
@@ -28,6 +28,7 @@ for g in ${GROUPS_//,/ }; do
     c5) run ${TAG}_c5 c5 "--line c5" "--reactors 64" || exit $?; files+=(gpurun_out/traffic_${TAG}_c5.json) ;;
     pfr) run ${TAG}_pfr pfr "--line pfr" "--reactors 64" || exit $?; files+=(gpurun_out/traffic_${TAG}_pfr.json) ;;
     hcci) run ${TAG}_hcci hcci "--line hcci" "--reactors 64" || exit $?; files+=(gpurun_out/traffic_${TAG}_hcci.json) ;;
+    ropext) run ${TAG}_ropext ropext "--line ropext" "--reactors 64" || exit $?; files+=(gpurun_out/traffic_${TAG}_ropext.json) ;;
   esac
 done
 python3 - "${files[@]}" <<'PY'

@@ -1,8 +1,9 @@
 """Per-launch HBM bytes of the reactor and ROP kernels from scripts/pmc_traffic.sh output.
 
-    python scripts/traffic_summary.py gpurun_out/traffic_TAG [--line c4|c5|pfr|hcci]
+    python scripts/traffic_summary.py gpurun_out/traffic_TAG [--line c4|c5|pfr|hcci|ropext]
       (a run of that bench line only: its kernel's largest dispatch is the line's launch -- the smaller
-      ones are the line's warm-up and the tiny headline run that always precedes it)
+      ones are the line's warm-up and the tiny headline run that always precedes it; ropext: the
+      161-species ROP dispatches of that run are the extended-mechanism line's, keyed rop_ext[_jit])
 
 FETCH_SIZE (KiB) is doubled per the gfx950 calibration (MI355X_MICROARCH.md, HBM section: it
 tallies 128-B requests at 64 B); WRITE_SIZE (KiB) is taken as is.  Output: profiles/traffic.json
@@ -41,6 +42,10 @@ def main():
                 continue
             per[(kind, row["Dispatch_Id"], row["Counter_Name"])] += float(row["Counter_Value"])
         for (kind, _, cname), v in per.items():
+            if line == "ropext":  # that run's other kernels are its tiny headline run: not the lines' launches
+                if not kind.startswith("rop_161sp"):
+                    continue
+                kind = "rop_ext" + kind[len("rop_161sp"):]
             acc[kind][cname].append(v)
     out = {}
     # the line's own kernel and its key in profiles/traffic.json (largest dispatch only)
@@ -67,7 +72,7 @@ def main():
                      "dispatches": len(c["FETCH_SIZE"])}
     # units per launch of the bench workload (bench.py defaults)
     units = {"reactor": 65536, "reactor_c4": 2 ** 20, "big_reactor": 262144, "rop": 10_000_000, "rop_jit": 10_000_000,
-             "rop_161sp": 1_000_000, "rop_161sp_jit": 1_000_000}
+             "rop_161sp": 1_000_000, "rop_161sp_jit": 1_000_000, "rop_ext": 1_000_000, "rop_ext_jit": 1_000_000}
     for k, u in units.items():
         if k in out:
             out[k]["units"] = u
