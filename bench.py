@@ -307,12 +307,13 @@ def rop_line(dev, mech, ops, ns, rank, world, cpu_sample, kernel_name="rop_kerne
 
         orc_r = Oracle(mech)
         threads = cpu_threads()
-        m = min(ns, 200_000)
+        small = mech.KK <= 63  # bounded sample: ~0.1-5 s of CPU work per leg
+        m = min(ns, 200_000 if small else 100_000)
         Th, Ph, Yh = Ts[:m].cpu().numpy(), Ps[:m].cpu().numpy(), Ys[:, :m].cpu().numpy()
         tc = time.perf_counter()
         wc, _, _ = orc_r.rop_batch(Th, Ph, Yh, nthreads=threads)
         t_all = time.perf_counter() - tc
-        m1 = min(m, 20_000)
+        m1 = min(m, 20_000 if small else 4_000)
         tc = time.perf_counter()
         orc_r.rop_batch(Th[:m1], Ph[:m1], np.ascontiguousarray(Yh[:, :m1]), nthreads=1)
         t_one = time.perf_counter() - tc
@@ -328,9 +329,10 @@ def rop_line(dev, mech, ops, ns, rank, world, cpu_sample, kernel_name="rop_kerne
     return out
 
 
-def lu_line(dev, nsys, n):
+def lu_line(dev, nsys, n, cpu_sample=0):
     """Batched LU (ckmi_lu_factor_batched) on nsys Newton-like matrices I - gamma J of size n, timed with HIP
-    events on the stream it is launched on; algorithmic work (2/3) n^3 per matrix."""
+    events on the stream it is launched on; algorithmic work (2/3) n^3 per matrix.  cpu_baseline: the
+    oracle's dense LU (the C integrator's own factorisation) over the first matrices, OpenMP over systems."""
     g = torch.Generator(device=dev).manual_seed(0)
     A0 = torch.eye(n, dtype=torch.float64, device=dev) - 1e-6 * torch.randn(
         (nsys, n, n), dtype=torch.float64, device=dev, generator=g) * 10.0 ** (6.0 * torch.rand(
@@ -342,7 +344,7 @@ def lu_line(dev, nsys, n):
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        _, _, info = _native.lu_factor_batched(A)
+        _, ipiv, info = _native.lu_factor_batched(A)
         e1.record()
         torch.cuda.synchronize()
         if it:
@@ -350,12 +352,34 @@ def lu_line(dev, nsys, n):
     sec = float(np.median(times))
     flops = nsys * 2.0 / 3.0 * n ** 3
     nbytes = nsys * 2.0 * n * n * 8
+    cpu = None
+    if cpu_sample > 0:
+        from oracle.oracle import lu_factor_batch  # noqa: E402  (cpu_baseline leg only)
+
+        m = min(nsys, 4096)
+        Ah = A0[:m].cpu().numpy()
+        threads = cpu_threads()
+        tc = time.perf_counter()
+        LUc, pc, _ = lu_factor_batch(Ah, threads)
+        t_all = time.perf_counter() - tc
+        m1 = min(m, 256)
+        tc = time.perf_counter()
+        lu_factor_batch(Ah[:m1], 1)
+        t_one = time.perf_counter() - tc
+        LUg, pg = A[:m].cpu().numpy(), ipiv[:m].cpu().numpy()
+        cpu = {"value": m / t_all, "unit": "systems/s", "cores": threads, "kind": "port", "host": host_info(),
+               "single_core_value": m1 / t_one,
+               "sample": f"first {m} of the same {nsys} matrices ({m1} on one core), oracle C dense LU "
+                         "(partial pivoting), OpenMP over systems",
+               "pivots_identical_frac": float(np.mean(np.all(pc == pg, axis=1))),
+               "factor_max_abs_diff_vs_gpu": float(np.max(np.abs(LUc - LUg)))}
     del A, A0
     return {"kernel": "lu_factor_kernel<11>", "systems": nsys, "n": n, "ms_per_launch": sec * 1e3,
             "systems_per_s": nsys / sec, "singular": int((info != 0).sum().item()),
             "roofline": {"bound": "mfma", "pipe": "fp64-mfma", "achieved": flops / sec / 1e12,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": flops / sec / 1e12 / FP64_PEAK_TFLOPS,
-                         "hbm_GBs": nbytes / sec / 1e9, "traffic": load_traffic("lu", nsys)}}
+                         "hbm_GBs": nbytes / sec / 1e9, "traffic": load_traffic("lu", nsys)},
+            "cpu_baseline": cpu}
 
 
 def secondary_sweep(name, dm, dev, mech, ops, sweep_fn, world, rank, args, kernel, traffic_key, workload, scaling):
@@ -624,10 +648,10 @@ def main():
     if "rop" in lines and args.rop_states > 0:
         rop = rop_line(dev, mech, ops, args.rop_states, rank, world, args.cpu_sample)
     if "lu" in lines and rank == 0 and args.lu_systems > 0:
-        lu = lu_line(dev, args.lu_systems, 161)
+        lu = lu_line(dev, args.lu_systems, 161, args.cpu_sample if world == 1 else 0)
     if "rop161" in lines and rank == 0 and args.big_states > 0:
         bm = big_mechanism()
-        rop_big = rop_line(dev, bm, count_ops(bm.to_tables()), args.big_states, rank, world, 0,
+        rop_big = rop_line(dev, bm, count_ops(bm.to_tables()), args.big_states, rank, world, args.cpu_sample,
                            kernel_name="rop_kernel<0,3>", traffic_key="rop_161sp",
                            label=f"synthetic GRI-3.0 + tracers, KK = {bm.KK}, II = {bm.II}")
     rop_ext = None
@@ -636,7 +660,7 @@ def main():
         # reactions (count_ops prices a PLOG / general reaction like an Arrhenius one: a lower bound)
         em = Mechanism.from_files(os.path.join(ROOT, "data", "gri30_tracer161_ext_chem.inp"),
                                   os.path.join(ROOT, "data", "gri30_tracer161_thermo.dat"))
-        rop_ext = rop_line(dev, em, count_ops(em.to_tables()), args.big_states, rank, world, 0,
+        rop_ext = rop_line(dev, em, count_ops(em.to_tables()), args.big_states, rank, world, args.cpu_sample,
                            kernel_name="rop_kernel<0,3,true>", traffic_key="rop_ext",
                            label=f"data/gri30_tracer161_ext (PLOG, HIGH, FORD/RORD, fractional, wide), KK = {em.KK}, "
                                  f"II = {em.II}")

@@ -632,6 +632,17 @@ static void lu_solve(int n, const double* A, const int* piv, double* b) {
   }
 }
 
+/* Batched dense LU, the integrator's own lu_factor above over nsys row-major n x n matrices in place,
+ * OpenMP over systems: the CPU baseline of bench.py's batched-LU line (test infrastructure). */
+void cko_lu_factor_batch(int n, int nsys, double* A, int* piv, int* info, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+  for (int s = 0; s < nsys; ++s)
+    info[s] = lu_factor(n, A + (size_t)s * n * n, piv + (size_t)s * n);
+}
+
 /* ------------------------------------------------------ BDF integrator */
 #define QMAX 5
 #define L_MAX (QMAX + 1)

@@ -39,6 +39,19 @@ def lib():
 _P = ct.c_void_p
 
 
+def lu_factor_batch(A: np.ndarray, nthreads: int = 0):
+    """Batched partial-pivoting LU of (nsys, n, n) row-major matrices (ckoracle.c cko_lu_factor_batch: the
+    integrator's own dense LU): returns (LU, piv, info), info[s] = 1 + the first zero pivot column or 0."""
+    L = lib()
+    L.cko_lu_factor_batch.argtypes = [ct.c_int, ct.c_int, _P, _P, _P, ct.c_int]
+    A = np.array(A, dtype=np.float64, order="C", copy=True)
+    nsys, n = A.shape[0], A.shape[1]
+    piv = np.zeros((nsys, n), dtype=np.int32)
+    info = np.zeros(nsys, dtype=np.int32)
+    L.cko_lu_factor_batch(n, nsys, A.ctypes.data, piv.ctypes.data, info.ctypes.data, int(nthreads))
+    return A, piv, info
+
+
 class _Mech(ct.Structure):
     _fields_ = [("KK", ct.c_int), ("II", ct.c_int)] + [
         (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
