@@ -607,29 +607,63 @@ struct BigMatrixM {
       int ps[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        uint64_t key = 0;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
-          const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
-          if (cand && kr > key) key = kr;
-        }
-        key = wave_max_u64_all(key);
-        const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)key);
-        const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
-        if (khi == 0u) ok = false;
-        const int p = (int)(0xffffffffu - klo);
-        ps[s] = p;
-        const int pl = p & 63, pj = p >> 6;
         // the pivot row's entries of the 4 panel columns (wave-uniform, from lane pl)
         double pv[4];
+        int p;
+#ifndef CKMI_BIG_PIVOT_MAX
+        // Natural pivot first: the diagonal row k0 + s is the pivot whenever it is still free and no
+        // free row's key exceeds its key (keys are unique: the row is in the low word).  That check is
+        // one readlane of the row and a ballot of 3 compares per lane; the whole-wave u64 max (6
+        // dependent DPP / row-swap stages) runs only when it fails.  Same pivot, same arithmetic.
+        {
+          const int pn = k0 + s, pnl = pn & 63, pnj = pn >> 6;  // wave-uniform
+          uint64_t dmn = dm[0];
 #pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          double v = y[0][s2];
+          for (int j = 1; j < NJ; ++j) dmn = pnj == j ? dm[j] : dmn;
 #pragma unroll
-          for (int j = 1; j < NJ; ++j) v = pj == j ? y[j][s2] : v;
-          pv[s2] = bcast(v, pl);
+          for (int s2 = 0; s2 < 4; ++s2) {
+            double v = y[0][s2];
+#pragma unroll
+            for (int j = 1; j < NJ; ++j) v = pnj == j ? y[j][s2] : v;
+            pv[s2] = bcast(v, pnl);
+          }
+          const uint64_t kn = ((uint64_t)__float_as_uint((float)fabs(pv[s])) << 32) | (0xffffffffu - (uint32_t)pn);
+          bool above = false;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
+            const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
+            above = above || (cand && kr > kn);
+          }
+          p = pn;
+          if (((dmn >> pnl) & 1ull) || __builtin_amdgcn_ballot_w64(above) != 0ull) p = -1;
+          else if ((uint32_t)(kn >> 32) == 0u) ok = false;
         }
+        if (p < 0)
+#endif
+        {
+          uint64_t key = 0;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
+            const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
+            if (cand && kr > key) key = kr;
+          }
+          key = wave_max_u64_all(key);
+          const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)key);
+          const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
+          if (khi == 0u) ok = false;
+          p = (int)(0xffffffffu - klo);
+          const int pl = p & 63, pj = p >> 6;
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) {
+            double v = y[0][s2];
+#pragma unroll
+            for (int j = 1; j < NJ; ++j) v = pj == j ? y[j][s2] : v;
+            pv[s2] = bcast(v, pl);
+          }
+        }
+        ps[s] = p;
         const double piv = pv[s];
         const double rcp = rcp_nr(piv);
 #pragma unroll
