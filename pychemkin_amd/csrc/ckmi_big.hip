@@ -786,6 +786,14 @@ struct BigMatrixM {
     // that block (11 full-wave stores instead of 44 with 4 lanes each and 4 branches), and the A operand
     // reads the pivot rows out of it.
     double* Bk = lds_at<double>(L.xpart) + 8 * NC + BW * 16 * NB + wid * 64 * NB;  // [16 ti][4 q][NB c]
+#ifndef CKMI_BIG_B_LATE
+    // The B operands (P rows of this lane's step) are loaded here, before the gather: in the MFMA loop
+    // each load had been followed by a wait for it (6 LDS round trips on the critical path).  The gather's
+    // asm stores (memory clobbers) keep the compiler from sinking them.
+    double Bl[NB];
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) Bl[rb] = Pb[(lane >> 4) * NC + 16 * rb + (lane & 15)];
+#endif
     bool allc = true;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -867,7 +875,11 @@ struct BigMatrixM {
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
       const int i = 16 * rb + (lane & 15);
+#ifndef CKMI_BIG_B_LATE
+      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
+#else
       const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
+#endif
 #pragma unroll
       for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
     }
