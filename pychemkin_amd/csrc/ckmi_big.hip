@@ -859,14 +859,14 @@ struct BigMatrixM {
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
       const int i = 16 * rb + (lane & 15);
-      const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
+      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
       a[rb][G] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[G], Bv, a[rb][G], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);  // keep the issue order: the scheduler may not mix the two loops
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
       const int i = 16 * rb + (lane & 15);
-      const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
+      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
 #pragma unroll
       for (int g = 0; g < NG; ++g)
         if (g != G) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
