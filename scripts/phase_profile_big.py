@@ -57,6 +57,14 @@ def main():
     out["factor_split"]["cycles_per_panel"] = {nm: ph[:, 6 + k].sum() / npan for k, nm in enumerate(names_f) }
     other = tot - ph[:, :5].sum()
     out["phases"]["control"] = {"frac_of_total": other / tot, "cycles_per_step": other / st[:, 0].sum()}
+    # the control states' own time (state-machine passes; the Newton iteration's solve and the setup's
+    # build + factorisation are subtracted / excluded)
+    nst = st[:, 0].sum()
+    newton = ph[:, 12].sum() - ph[:, 4].sum()
+    out["control_split_cycles_per_step"] = {
+        "newton_iter_excl_solve": newton / nst, "step_complete": ph[:, 13].sum() / nst,
+        "step_begin_end": ph[:, 14].sum() / nst, "other_states": ph[:, 15].sum() / nst,
+        "unattributed": (other - newton - ph[:, 13:16].sum()) / nst}
     print(json.dumps(out, indent=1))
 
 
