@@ -513,7 +513,11 @@ struct PanHdr {
   int pad[3];
 };
 
-template <int NB>
+// LA: the look-ahead factorisation (else the barrier form), an A/B form built with CKMI_BIG_LOOKAHEAD for the
+// NB = 11 kernel without pressure-dependent rates only: in the PLOG kernels and at NB = 9 it crashes the ROCm
+// 7.2 backend (AMDGPU Rewrite AGPR-Copy-MFMA, eliminateSpillsOfReassignedVGPRs), and it quadruples the
+// compile time of this file.  Measured: bitwise the same results, no faster.
+template <int NB, bool LA = true>
 struct BigMatrixM {
   static constexpr int NC = 16 * NB;
   static constexpr int NG = (NB + 3) / 4;    // accumulator groups of 4 register tiles
@@ -553,11 +557,108 @@ struct BigMatrixM {
 
   static constexpr int NJ = (NC + 63) / 64;  // rows per lane in the transposed panel
 
+  // xpart during a factorisation: panel buffers [3][4 s][NC], per-wave pivot rows [BW][4 s][4 q][NB c],
+  // per-wave diagonal-block rows [BW][16 ti][4 q][NB c]; after the 3 panel headers in phdr, the look-ahead's
+  // sync words: [0] panels published, [4 + w] last panel wave w has finished with
+  static constexpr int NPB = 3;
+  __device__ __forceinline__ static double* pan_buf(const BigLds& L, int i) {
+    return lds_at<double>(L.xpart) + i * 4 * NC;
+  }
+  __device__ __forceinline__ static double* row_buf(const BigLds& L, int wid) {
+    return lds_at<double>(L.xpart) + NPB * 4 * NC + wid * 16 * NB;
+  }
+  __device__ __forceinline__ static double* blk_buf(const BigLds& L, int wid) {
+    return lds_at<double>(L.xpart) + NPB * 4 * NC + BW * 16 * NB + wid * 64 * NB;
+  }
+  // write-only scratch: the look-ahead's column staging of the waves that do not own the next panel
+  __device__ __forceinline__ static double* junk_buf(const BigLds& L) {
+    return lds_at<double>(L.xpart) + NPB * 4 * NC + BW * 16 * NB + BW * 64 * NB;
+  }
+  __device__ __forceinline__ static int* sync_words(const BigLds& L) {
+    return lds_at<int>(L.phdr + NPB * (int)sizeof(PanHdr));
+  }
+
   // row r of the matrix has been a pivot row: bit (r & 63) of dm[r >> 6] (wave-uniform masks)
   __device__ __forceinline__ static void mark_done(uint64_t (&dm)[NJ], int p) {
     const uint64_t bit = 1ull << (p & 63);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) dm[j] |= (p >> 6) == j ? bit : 0ull;  // selects, not a dynamic index
+  }
+
+  // the 4 pivot steps of the panel k0 .. k0 + 3 on its columns in the row-per-lane layout (lane l: rows
+  // l, l + 64, l + 128), pivots into ps
+  __device__ __forceinline__ static void pivot_steps(double (&y)[NJ][4], const uint64_t (&rid)[NJ], int k0,
+                                                     uint64_t (&dm)[NJ], bool& ok, int lane, int (&ps)[4]) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      // the pivot row's entries of the 4 panel columns (wave-uniform, from lane pl)
+      double pv[4];
+      int p;
+#ifndef CKMI_BIG_PIVOT_MAX
+      // Natural pivot first: the diagonal row k0 + s is the pivot whenever it is still free and no
+      // free row's key exceeds its key (keys are unique: the row is in the low word).  That check is
+      // one readlane of the row and a ballot of 3 compares per lane; the whole-wave u64 max (6
+      // dependent DPP / row-swap stages) runs only when it fails.  Same pivot, same arithmetic.
+      {
+        const int pn = k0 + s, pnl = pn & 63, pnj = pn >> 6;  // wave-uniform
+        uint64_t dmn = dm[0];
+#pragma unroll
+        for (int j = 1; j < NJ; ++j) dmn = pnj == j ? dm[j] : dmn;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          double v = y[0][s2];
+#pragma unroll
+          for (int j = 1; j < NJ; ++j) v = pnj == j ? y[j][s2] : v;
+          pv[s2] = bcast(v, pnl);
+        }
+        const uint64_t kn = ((uint64_t)__float_as_uint((float)fabs(pv[s])) << 32) | (0xffffffffu - (uint32_t)pn);
+        bool above = false;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
+          const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
+          above = above || (cand && kr > kn);
+        }
+        p = pn;
+        if (((dmn >> pnl) & 1ull) || __builtin_amdgcn_ballot_w64(above) != 0ull) p = -1;
+        else if ((uint32_t)(kn >> 32) == 0u) ok = false;
+      }
+      if (p < 0)
+#endif
+      {
+        uint64_t key = 0;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
+          const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
+          if (cand && kr > key) key = kr;
+        }
+        key = wave_max_u64_all(key);
+        const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)key);
+        const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
+        if (khi == 0u) ok = false;
+        p = (int)(0xffffffffu - klo);
+        const int pl = p & 63, pj = p >> 6;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          double v = y[0][s2];
+#pragma unroll
+          for (int j = 1; j < NJ; ++j) v = pj == j ? y[j][s2] : v;
+          pv[s2] = bcast(v, pl);
+        }
+      }
+      ps[s] = p;
+      const double piv = pv[s];
+      const double rcp = rcp_nr(piv);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const bool isp = lane + 64 * j == p;
+        const double g = isp ? (piv - 1.0) * rcp : y[j][s] * rcp;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) y[j][s2] = s2 == s ? (isp ? rcp : -g) : fma(-g, pv[s2], y[j][s2]);
+      }
+      mark_done(dm, p);
+    }
   }
 
   // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo
@@ -577,8 +678,8 @@ struct BigMatrixM {
     constexpr int G = C >> 2, E = C & 3;
     const int ti = lane & 15, q = lane >> 4;
     const int k0 = 16 * C + 4 * wo;
-    double* Pb = lds_at<double>(L.xpart) + par * 4 * NC;             // [4 s][NC] P of the panel
-    double* Rb = lds_at<double>(L.xpart) + 8 * NC + wid * 16 * NB;  // [4 s][4 q][NB c] pivot rows, per wave
+    double* Pb = pan_buf(L, par);   // [4 s][NC] P of the panel
+    double* Rb = row_buf(L, wid);   // [4 s][4 q][NB c] pivot rows, per wave
     PanHdr* hdr = lds_at<PanHdr>(L.phdr) + par;
 #ifndef CKMI_BIG_PANEL_COLS
     if (wid == wo) {
@@ -605,76 +706,7 @@ struct BigMatrixM {
 #endif
       PPH(2);
       int ps[4];
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        // the pivot row's entries of the 4 panel columns (wave-uniform, from lane pl)
-        double pv[4];
-        int p;
-#ifndef CKMI_BIG_PIVOT_MAX
-        // Natural pivot first: the diagonal row k0 + s is the pivot whenever it is still free and no
-        // free row's key exceeds its key (keys are unique: the row is in the low word).  That check is
-        // one readlane of the row and a ballot of 3 compares per lane; the whole-wave u64 max (6
-        // dependent DPP / row-swap stages) runs only when it fails.  Same pivot, same arithmetic.
-        {
-          const int pn = k0 + s, pnl = pn & 63, pnj = pn >> 6;  // wave-uniform
-          uint64_t dmn = dm[0];
-#pragma unroll
-          for (int j = 1; j < NJ; ++j) dmn = pnj == j ? dm[j] : dmn;
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) {
-            double v = y[0][s2];
-#pragma unroll
-            for (int j = 1; j < NJ; ++j) v = pnj == j ? y[j][s2] : v;
-            pv[s2] = bcast(v, pnl);
-          }
-          const uint64_t kn = ((uint64_t)__float_as_uint((float)fabs(pv[s])) << 32) | (0xffffffffu - (uint32_t)pn);
-          bool above = false;
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
-            const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
-            above = above || (cand && kr > kn);
-          }
-          p = pn;
-          if (((dmn >> pnl) & 1ull) || __builtin_amdgcn_ballot_w64(above) != 0ull) p = -1;
-          else if ((uint32_t)(kn >> 32) == 0u) ok = false;
-        }
-        if (p < 0)
-#endif
-        {
-          uint64_t key = 0;
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            const uint64_t kr = ((uint64_t)__float_as_uint((float)fabs(y[j][s])) << 32) | rid[j];
-            const bool cand = lane + 64 * j < NC && !((dm[j] >> lane) & 1ull);
-            if (cand && kr > key) key = kr;
-          }
-          key = wave_max_u64_all(key);
-          const uint32_t klo = __builtin_amdgcn_readfirstlane((uint32_t)key);
-          const uint32_t khi = __builtin_amdgcn_readfirstlane((uint32_t)(key >> 32));
-          if (khi == 0u) ok = false;
-          p = (int)(0xffffffffu - klo);
-          const int pl = p & 63, pj = p >> 6;
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) {
-            double v = y[0][s2];
-#pragma unroll
-            for (int j = 1; j < NJ; ++j) v = pj == j ? y[j][s2] : v;
-            pv[s2] = bcast(v, pl);
-          }
-        }
-        ps[s] = p;
-        const double piv = pv[s];
-        const double rcp = rcp_nr(piv);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const bool isp = lane + 64 * j == p;
-          const double g = isp ? (piv - 1.0) * rcp : y[j][s] * rcp;
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) y[j][s2] = s2 == s ? (isp ? rcp : -g) : fma(-g, pv[s2], y[j][s2]);
-        }
-        mark_done(dm, p);
-      }
+      pivot_steps(y, rid, k0, dm, ok, lane, ps);
       // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -785,7 +817,7 @@ struct BigMatrixM {
     // All four pivot rows in the diagonal register block (the common case): every lane writes its row of
     // that block (11 full-wave stores instead of 44 with 4 lanes each and 4 branches), and the A operand
     // reads the pivot rows out of it.
-    double* Bk = lds_at<double>(L.xpart) + 8 * NC + BW * 16 * NB + wid * 64 * NB;  // [16 ti][4 q][NB c]
+    double* Bk = blk_buf(L, wid);  // [16 ti][4 q][NB c]
 #ifndef CKMI_BIG_B_LATE
     // The B operands (P rows of this lane's step) are loaded here, before the gather: in the MFMA loop
     // each load had been followed by a wait for it (6 LDS round trips on the critical path).  The gather's
@@ -927,6 +959,244 @@ struct BigMatrixM {
     }
   }
 
+  // ---------------------------------------------------------------- look-ahead form (default)
+  // The barrier form above serialises, per panel: the owner's 4 pivot steps -> barrier -> every wave's
+  // pivot-row gather and rank-4 MFMA update -> the next owner's pivot steps (it needs its columns
+  // updated).  Here the owner of panel t + 1 updates just its 4 panel columns with panel t's transforms
+  // on the VALU, in the row-per-lane layout of the pivot steps (from the same P' and pivot rows the MFMA
+  // uses), factors panel t + 1 and publishes it before issuing its own MFMAs for panel t; the other waves
+  // run their panel-t MFMAs meanwhile.  Waves synchronise through LDS words instead of workgroup
+  // barriers (a barrier would make every wave wait for the owner's MFMAs too): "panels published" and,
+  // per wave, "last panel finished"; the panel buffers rotate over 3 so that panel t + 1 is written only
+  // once every wave is done with panel t - 2.  The pivots and the arithmetic of every transform are those
+  // of the barrier form; only the 4 look-ahead columns are updated by FMAs instead of the MFMA (measured:
+  // bitwise the same results).  A/B form (CKMI_BIG_LOOKAHEAD): it did not shorten the factorisation
+  // (200 vs 211 ms per extra factorisation of 2,048 configs[4] reactors, CKMI_BIG_FACTOR_TWICE).
+  __device__ __forceinline__ static void la_wait(const int* f, int v, bool& live) {
+    if (!live) return;
+    for (int it = 0; it < (1 << 22); ++it) {  // bounded: a broken protocol fails the factorisation, not the GPU
+      const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (x >= v) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    live = false;
+  }
+  __device__ __forceinline__ static void la_wait_all(const int* g, int v, bool& live) {
+    if (!live) return;
+    for (int it = 0; it < (1 << 22); ++it) {
+      int m = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+      for (int w = 1; w < BW; ++w) m = min(m, __hip_atomic_load(g + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      if (__builtin_amdgcn_readfirstlane(m) >= v) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    live = false;
+  }
+  __device__ __forceinline__ static void la_signal(int* f, int v, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's LDS writes have landed
+    if (lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+
+  // owner of panel tn (columns in register tile CN of this wave): the columns into the row-per-lane layout
+  // through panel buffer tn % 3; with `upd`, panel tp's transforms applied to them (P' from panel buffer
+  // tp % 3, the pivot rows' entries from this wave's gather of panel tp); the 4 pivot steps; P, perm /
+  // rank and the header published, then "panels published" = tn + 1
+  // every wave: its column group q of register tile CN into panel buffer tn % 3 if it owns panel tn, else
+  // into the write-only scratch (the accumulators are read unconditionally: reading them under a branch
+  // makes the backend spill the matrix)
+  template <int CN>
+  __device__ __forceinline__ void la_stage(const BigLds& L, int tn, bool own, int lane) const {
+    constexpr int GN = CN >> 2, EN = CN & 3;
+    const int ti = lane & 15, q = lane >> 4;
+    const uint32_t dst = (uint32_t)(uintptr_t)((own ? pan_buf(L, tn % NPB) : junk_buf(L)) + q * NC + ti);
+#pragma unroll
+    for (int r = 0; r < NB; ++r)
+      asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(dst), "v"(a[r][GN][EN]), "i"(8 * 16 * r) : "memory");
+  }
+
+  template <int CN>
+  __device__ __forceinline__ static void la_own(const BigLds& L, int tn, bool upd, int tp, const int (&pr)[4], bool allc,
+                                                uint64_t (&dm)[NJ], bool& ok, int wid, int lane) {
+    const int k0 = 4 * tn;
+    double* Pn = pan_buf(L, tn % NPB);
+    wave_lds_sync();
+    double y[NJ][4];
+    uint64_t rid[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int row = lane + 64 * j;
+      rid[j] = 0xffffffffu - (uint32_t)row;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) y[j][s] = row < NC ? Pn[s * NC + row] : 0.0;
+    }
+    if (upd) {
+      const double* Pt = pan_buf(L, tp % NPB);
+      const double* Rb = row_buf(L, wid);
+      const double* Bk = blk_buf(L, wid);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        double u[4];  // pivot row s of panel tp, columns k0 .. k0 + 3 (lane group q = s2 of tile CN)
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) u[s2] = allc ? Bk[((pr[s] & 15) * 4 + s2) * NB + CN] : Rb[(s * 4 + s2) * NB + CN];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const int row = lane + 64 * j;
+          const double pv = row < NC ? Pt[s * NC + row] - (row == pr[s] ? 1.0 : 0.0) : 0.0;
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) y[j][s2] = fma(pv, u[s2], y[j][s2]);
+        }
+      }
+    }
+    int ps[4];
+    pivot_steps(y, rid, k0, dm, ok, lane, ps);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int row = lane + 64 * j;
+      if (row < NC) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) Pn[s * NC + row] = y[j][s];
+      }
+    }
+    PanHdr* hdr = lds_at<PanHdr>(L.phdr) + tn % NPB;
+    if (lane < 4) {
+      const int pl = lane == 0 ? ps[0] : (lane == 1 ? ps[1] : (lane == 2 ? ps[2] : ps[3]));
+      lds_at<int>(L.perm)[k0 + lane] = pl;
+      lds_at<int>(L.rank)[pl] = k0 + lane;
+      hdr->p[lane] = pl;
+    }
+    if (lane == 0) hdr->ok = ok ? 1 : 0;
+    la_signal(sync_words(L), tn + 1, lane);
+  }
+
+  // panel t = 4 C + wo (columns in register tile C of wave wo), every wave
+  // LAST: wo = 3, the next panel is in register tile C + 1 (wave 0)
+  template <int C, bool LAST>
+  __device__ __forceinline__ void la_panel(const BigLds& L, int wo, int n, uint64_t (&dm)[NJ], bool& ok, bool& live,
+                                           int wid, int lane FPH_PARAM) {
+#ifdef CKMI_PHASE_TIMERS
+    unsigned long long ft = __builtin_amdgcn_s_memtime();
+#define PPH(i) do { const unsigned long long f2 = __builtin_amdgcn_s_memtime(); fph[i] += f2 - ft; ft = f2; } while (0)
+#else
+#define PPH(i) (void)0
+#endif
+    constexpr int G = C >> 2, E = C & 3;
+    const int ti = lane & 15, q = lane >> 4;
+    const int t = 4 * C + wo;
+    int* sw = sync_words(L);
+    la_wait(sw, t + 1, live);  // panel t published
+    if (!live) ok = false;
+    PPH(1);
+    const PanHdr* hdr = lds_at<const PanHdr>(L.phdr) + t % NPB;
+    const double* Pb = pan_buf(L, t % NPB);
+    double* Rb = row_buf(L, wid);
+    double* Bk = blk_buf(L, wid);
+    int pr[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) pr[s] = __builtin_amdgcn_readfirstlane(hdr->p[s]);
+    if (!__builtin_amdgcn_readfirstlane(hdr->ok)) ok = false;
+    bool allc = true;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      mark_done(dm, pr[s]);
+      allc = allc && (pr[s] >> 4) == C;
+    }
+    // the pivot rows' entries of this wave's columns (values before the panel), as in panel<C>
+    const uint32_t rbq = (uint32_t)(uintptr_t)(Rb + q * NB);
+    if (allc) {
+      const uint32_t bkq = (uint32_t)(uintptr_t)(Bk + (ti * 4 + q) * NB);
+#pragma unroll
+      for (int c = 0; c < NB; ++c)
+        asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(bkq), "v"(a[C][c >> 2][c & 3]), "i"(8 * c) : "memory");
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int tip = pr[s] & 15, rp = pr[s] >> 4;
+        if (rp == C) {
+          if (ti == tip) {
+#pragma unroll
+            for (int c = 0; c < NB; ++c)
+              asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[C][c >> 2][c & 3]),
+                           "i"(8 * (s * 4 * NB + c)) : "memory");
+          }
+        } else {
+#pragma unroll
+          for (int r = 0; r < NB; ++r) {
+            if (r != C && r == rp) {
+              if (ti == tip) {
+#pragma unroll
+                for (int c = 0; c < NB; ++c)
+                  asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[r][c >> 2][c & 3]),
+                               "i"(8 * (s * 4 * NB + c)) : "memory");
+              }
+              asm volatile("" ::: "memory");
+            }
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+    PPH(3);
+    // look-ahead: the owner of panel t + 1 factors it now (its columns brought up to date by panel t here)
+    constexpr int CN = LAST ? C + 1 : C;
+    if constexpr (CN < NB) {
+      const int tn = t + 1;
+      const int won = LAST ? 0 : wo + 1;
+      if (4 * tn < n) {
+        if (wid == won) la_wait_all(sw + 4, tn - NPB, live);  // every wave is done with panel buffer tn % 3
+        la_stage<CN>(L, tn, wid == won, lane);
+        if (wid == won) la_own<CN>(L, tn, true, t, pr, allc, dm, ok, wid, lane);
+      }
+    }
+    PPH(0);
+    // the MFMA operands (loaded after the look-ahead block: live across it they overflow the register file)
+    const int sl = lane >> 4;
+    const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));
+    double A[NG];
+    {
+      const int j = lane & 15;
+      const double* ra = allc ? Bk + ((pl & 15) * 4 + (j & 3)) * NB + (j >> 2)
+                              : Rb + ((lane >> 4) * 4 + (j & 3)) * NB + (j >> 2);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) A[g] = 4 * g + (j >> 2) < NB ? ra[4 * g] : 0.0;
+    }
+    double Bl[NB];
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) Bl[rb] = Pb[(lane >> 4) * NC + 16 * rb + (lane & 15)];
+#pragma unroll
+    for (int rb = 0; rb < NB; ++rb) {
+      const int i = 16 * rb + (lane & 15);
+      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
+    }
+    PPH(4);
+    if (wid == wo) {  // the panel columns keep their processed values
+#pragma unroll
+      for (int r = 0; r < NB; ++r) a[r][G][E] = Pb[q * NC + ti + 16 * r];
+    }
+    la_signal(sw + 4 + wid, t, lane);  // this wave is done with panel buffer t % 3
+    PPH(5);
+#undef PPH
+  }
+
+  template <int C>
+  __device__ __forceinline__ void la_panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, bool& live, int wid,
+                                            int lane FPH_PARAM) {
+    if constexpr (C < NB) {
+#pragma unroll 1
+      for (int wo = 0; wo < 3; ++wo)
+        if (16 * C + 4 * wo < n) la_panel<C, false>(L, wo, n, dm, ok, live, wid, lane FPH_ARG);
+      if (16 * C + 12 < n) la_panel<C, true>(L, 3, n, dm, ok, live, wid, lane FPH_ARG);
+      la_panels<C + 1>(L, n, dm, ok, live, wid, lane FPH_ARG);
+    }
+  }
+
   __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane, int n
 #ifdef CKMI_PHASE_TIMERS
                                          , unsigned long long (&fph)[6]
@@ -945,7 +1215,25 @@ struct BigMatrixM {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) dm[j] = 0ull;
     bool ok = true;
-    panels<0>(L, n, dm, ok, t, wid, lane FPH_ARG);
+#ifndef CKMI_BIG_SYNC_BARRIER
+    if constexpr (!LA)
+#endif
+      panels<0>(L, n, dm, ok, t, wid, lane FPH_ARG);
+#ifndef CKMI_BIG_SYNC_BARRIER
+    else {
+      int* sw = sync_words(L);
+      if (t < 4 + BW) sw[t] = t < 4 ? 0 : -1;  // nothing published, no panel finished
+      __syncthreads();
+      bool live = true;
+      if (n > 0) {
+        const int pr0[4] = {0, 0, 0, 0};
+        la_stage<0>(L, 0, wid == 0, lane);
+        if (wid == 0) la_own<0>(L, 0, false, 0, pr0, false, dm, ok, wid, lane);
+      }
+      la_panels<0>(L, n, dm, ok, live, wid, lane FPH_ARG);
+      __syncthreads();  // perm / rank complete, every wave's updates done
+    }
+#endif
     return ok;
   }
 
@@ -990,13 +1278,19 @@ struct BigMatrixM {
 };
 
 #ifdef CKMI_BIG_VALU
-template <int NB>
+template <int NB, bool PL>
 using BigMat = BigMatrix<NB>;  // one workgroup barrier per column (VALU rank-1 updates)
 #else
 // NB = 12 (177..192 variables) keeps the per-column VALU factorisation: its MFMA form overflows
 // the register file (and crashes the ROCm 7.2 backend with the VGPR-form MFMA option)
-template <int NB>
-using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB>, BigMatrix<NB>>;
+// The look-ahead factorisation (BigMatrixM::la_panels) is an A/B form: measured no faster (CKMI_BIG_LOOKAHEAD)
+#ifdef CKMI_BIG_LOOKAHEAD
+template <int NB, bool PL>
+using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB, (NB == 11 && !PL)>, BigMatrix<NB>>;
+#else
+template <int NB, bool PL>
+using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB, false>, BigMatrix<NB>>;
+#endif
 #endif
 
 // ------------------------------------------------------------------ general reactions
@@ -1325,7 +1619,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
   Blk B;
   B.ored = L.red;
   B.phase = 0;
-  BigMat<NB> M;
+  BigMat<NB, PL> M;
   BdfT<NT> b;
   b.zn.base = L.zn + tid * 8;
   BdfT<NT> b0;  // component 0 (T): its Nordsieck history, read by every thread
@@ -1642,6 +1936,12 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
 #ifdef CKMI_PHASE_TIMERS
             ok = M.factor(L, B, tid, wid, lane, n, fph);
 #else
+#ifdef CKMI_BIG_FACTOR_TWICE  // timing experiment: the factorisation's share of the run time
+            (void)M.factor(L, B, tid, wid, lane, n);
+            __syncthreads();
+            M.build(Jg, S.gamma, tid, n);
+            __syncthreads();
+#endif
             ok = M.factor(L, B, tid, wid, lane, n);
 #endif
             BPH_ADD(3);
@@ -2052,7 +2352,7 @@ BigLds big_layout(const ckmi_mech* m, int NC, int lds_max) {
   const int NBP = (NC / 16 + 1) & ~1;
   L.prow = take(8 * BW * 4 * NBP);
   L.gcol = take(8 * 2 * 16 * NBP);
-  L.phdr = take(2 * 32);  // [2] PivHdr (VALU factor) or PanHdr (MFMA factor)
+  L.phdr = take(3 * 32 + 32);  // [2] PivHdr (VALU factor) or [3] PanHdr + sync words (MFMA factor)
   L.perm = take(4 * NT);
   L.rank = take(4 * NT);
   L.bp = take(8 * 16 * NBP);
@@ -2061,9 +2361,10 @@ BigLds big_layout(const ckmi_mech* m, int NC, int lds_max) {
   // the Jacobian column block takes what is left (multiple of BW columns, at most the matrix)
   const int LDJ = NT + 1;
   int jcb = (lds_max - align16(o) - 16) / (8 * LDJ);
-  // xpart: the solve's partial sums [NT][NBP], or the factorisation's panel buffers [2][4][NC], per-wave
-  // pivot rows [BW][16 NB] and per-wave diagonal block rows [BW][64 NB] (BigMatrixM::panel)
-  const int xneed = 8 * std::max(NT * NBP, 8 * NC + BW * 16 * (NC / 16) + BW * 64 * (NC / 16));
+  // xpart: the solve's partial sums [NT][NBP], or the factorisation's panel buffers [3][4][NC], per-wave
+  // pivot rows [BW][16 NB], per-wave diagonal block rows [BW][64 NB] and a [4][NC] staging scratch
+  // (BigMatrixM::pan_buf etc.)
+  const int xneed = 8 * std::max(NT * NBP, 16 * NC + BW * 16 * (NC / 16) + BW * 64 * (NC / 16));
   if (8 * LDJ * jcb < xneed && lds_max - align16(o) - 16 < xneed) jcb = 0;  // xpart must fit
   jcb = std::min(jcb, (NC + BW - 1) / BW * BW);
   jcb = jcb / BW * BW;

@@ -302,3 +302,40 @@ def test_oracle_runaway_guard(mech, oracle):
     assert r.status == 4 and r.nst < 1000 and -0.01 < Y.min() < -1e-3 and r.T < 1000.0
     r, Y = oracle.reactor(T0[378], P0[378], 1.0, Y0[378], **run)
     assert r.status == 0 and Y.min() > -1e-3
+
+
+class _CappedFits:
+    """A mechanism whose NASA-7 fits all end at `thi` (the upper fit extrapolated beyond it)."""
+
+    def __init__(self, mech, thi):
+        self._m, self._thi = mech, thi
+
+    def __getattr__(self, k):
+        return getattr(self._m, k)
+
+    def to_tables(self):
+        t = dict(self._m.to_tables())
+        th = t["thermo"].copy()
+        th[:, 2] = np.minimum(th[:, 2], self._thi)
+        t["thermo"] = th
+        return t
+
+
+def hot_h2_o2(mech):
+    """Stoichiometric H2/O2 at constant volume from 1500 K and 10 atm: its end state is ~3,900 K."""
+    Y0 = np.zeros(mech.KK)
+    Y0[mech.species.index("H2")] = 2 * 2.016
+    Y0[mech.species.index("O2")] = 31.998
+    return 1500.0, 10 * P_ATM, Y0 / Y0.sum()
+
+
+def test_oracle_hot_run_above_the_fit_range_is_not_a_runaway(mech):
+    """Round-4 advice: the runaway guard's upper bound is 2 max_k T_high (ckoracle.c, ckmi.hip), so a run that
+    legitimately ends above every fit's upper limit (here all fits capped at 3,000 K, the end state ~3,900 K)
+    keeps status 0; only a real runaway (8-10k K) trips it."""
+    from oracle.oracle import Oracle
+
+    orc = Oracle(_CappedFits(mech, 3000.0))
+    T0, P0, Y0 = hot_h2_o2(mech)
+    r, Y = orc.reactor(T0, P0, 1.0, Y0, problem=2, energy=1, t_end=1e-3, atol=1e-12, rtol=1e-8)
+    assert r.status == 0 and 3000.0 < r.T < 6000.0

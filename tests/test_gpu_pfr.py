@@ -72,6 +72,48 @@ def test_plugflow_golden_through_kin_calls(mech):
         kin.release(cs.value)
 
 
+def test_kin_tube_from_x0_with_pressure_profile(mech):
+    """Round-4 advice: the KIN path's P and V columns of a tube that starts at x0 > 0 under a PPRO profile
+    are the profile at the absolute positions and the inlet mass flux over the local density (what the kernel
+    integrated, ckmi_kin.cpp Reactor0D post-processing)."""
+    from pychemkin_amd import kin
+    from pychemkin_amd.constants import R_GAS
+
+    x0, xend = 1.0, 4.0
+    px = np.array([0.0, 1.0, 2.0, 4.0])
+    pv = P_IN * np.array([1.0, 0.9, 0.8, 0.7])
+    L = kin.bind()
+    cs = ct.c_int(kin.register(mech))
+    try:
+        i = lambda v: ct.byref(ct.c_int(v))  # noqa: E731
+        d = lambda v: ct.byref(ct.c_double(v))  # noqa: E731
+        assert L.KINAll0D_Setup(ct.byref(cs), i(3), i(1), i(2), i(1), i(1), np.zeros(1, np.int32), i(0)) == 0
+        Y0 = feed_Y(mech)
+        rho_in = P_IN / (R_GAS * T_IN) / np.sum(Y0 / mech.wt)
+        mdot = rho_in * np.pi * DIAM ** 2 / 4 * U_IN
+        assert L.KINAll0D_SetupPFRInputs(ct.byref(cs), d(x0), d(xend), d(T_IN), d(P_IN), d(0.0), d(DIAM),
+                                         np.zeros(1), np.zeros(1), d(mdot), Y0) == 0, kin.last_error()
+        assert L.KINAll0D_SetProfileParameter(b"PPRO", i(len(px)), px, pv) == 0, kin.last_error()
+        for line in ("DTSV    0.01", "ATOL    1e-12", "RTOL    1e-08"):
+            assert L.KINAll0D_SetUserKeyword(line.encode()) == 0, line
+        assert L.KINAll0D_Calculate(ct.byref(cs)) == 0, kin.last_error()
+        nr, npts = ct.c_int(0), ct.c_int(0)
+        assert L.KINAll0D_GetSolnResponseSize(ct.byref(nr), ct.byref(npts)) == 0
+        n = npts.value
+        x, T, P, V = (np.zeros(n) for _ in range(4))
+        Y = np.zeros((mech.KK, n), order="F")
+        assert L.KINAll0D_GetGasSolnResponse(ct.byref(nr), ct.byref(npts), i(mech.KK), x, T, P, V, Y) == 0
+    finally:
+        kin.release(cs.value)
+    # output positions are absolute (x0 + the integration variable), increasing, up to about the tube's end
+    assert abs(x[0] - x0) < 1e-12 and np.all(np.diff(x) > 0) and xend - 0.1 < x[-1] < xend + 0.1
+    np.testing.assert_allclose(P, np.interp(x, px, pv), rtol=1e-12)  # the profile at absolute positions
+    rho = P / (R_GAS * T) / np.sum(Y / mech.wt[:, None], axis=0)
+    np.testing.assert_allclose(V, rho_in * U_IN / rho, rtol=1e-10)  # inlet mass flux / local density
+    assert abs(T[-1] / T_IN - 1) < 1e-12  # fixed-temperature tube
+    assert np.all(np.isfinite(Y)) and abs(np.sum(Y[:, -1]) - 1) < 1e-8
+
+
 @pytest.mark.parametrize("path", [0, 1])  # 0: wave kernel; 1: workgroup kernel forced
 def test_tube_batches_match_oracle(dm_gri, oracle, mech, path):
     """CH4/air tubes, fixed T and adiabatic, different inlet velocities and pressures in one launch."""

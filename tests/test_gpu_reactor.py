@@ -314,3 +314,27 @@ def test_tp_equilibrium_golden_by_long_given_temperature_runs(dm, mech):
         gold = gold_all[sel]
         assert np.all(within(no, gold, *g["tolerance-frac"])), (T0, no / gold - 1)
         assert np.max(np.abs(no / gold - 1)) < 1e-6
+
+
+@pytest.mark.parametrize("path", [0, 1])  # 0: wave kernel; 1: workgroup kernel forced
+def test_hot_run_above_the_fit_range_is_not_a_runaway(mech, path):
+    """Round-4 advice: with every NASA-7 fit capped at 3,000 K, stoichiometric H2/O2 at constant volume ends
+    near 3,900 K with status 0 in both kernels (guard at 2 max_k T_high), at the oracle's end state."""
+    from oracle.oracle import Oracle
+    from pychemkin_amd import _native
+    from test_engine import _CappedFits, hot_h2_o2
+
+    m = _CappedFits(mech, 3000.0)
+    dm = _native.DeviceMechanism(m.to_tables())
+    T0, P0, Y0 = hot_h2_o2(mech)
+    run = dict(energy=1, t_end=1e-3, atol=1e-12, rtol=1e-8)
+    _native.set_reactor_path(path)
+    try:
+        res = {k: v.cpu().numpy() for k, v in dm.reactor_run(_native.make_cfg(**run), np.array([2], np.int32),
+                                                             np.array([T0]), np.array([P0]), np.array([1.0]),
+                                                             Y0[None]).items()}
+    finally:
+        _native.set_reactor_path(0)
+    r, _ = Oracle(m).reactor(T0, P0, 1.0, Y0, problem=2, **run)
+    assert res["stats"][0, 6] == 0 and r.status == 0
+    assert res["T"][0] > 3000.0 and abs(res["T"][0] / r.T - 1) < 1e-6
