@@ -661,8 +661,10 @@ struct BigMatrixM {
     }
   }
 
-  // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo
-  template <int C>
+  // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo.  SKIP (timing
+  // experiments with CKMI_BIG_FACTOR_TWICE_SKIP, on a discarded factorisation only): 1 no MFMA update, 2 no
+  // pivot steps, 4 no pivot-row gather stores, 8 no workgroup barrier
+  template <int C, int SKIP = 0>
   __device__ __forceinline__ void panel(const BigLds& L, int wo, int par, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                         int lane
 #ifdef CKMI_PHASE_TIMERS
@@ -706,7 +708,12 @@ struct BigMatrixM {
 #endif
       PPH(2);
       int ps[4];
-      pivot_steps(y, rid, k0, dm, ok, lane, ps);
+      if constexpr ((SKIP & 2) != 0) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ps[s] = k0 + s;
+      } else {
+        pivot_steps(y, rid, k0, dm, ok, lane, ps);
+      }
       // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -800,7 +807,8 @@ struct BigMatrixM {
     }
 #endif
     PPH(0);
-    __syncthreads();  // the panel's P' and pivots are published
+    if constexpr ((SKIP & 8) == 0) __syncthreads();  // the panel's P' and pivots are published
+    else wave_lds_sync();
     PPH(1);
     int pr[4];
 #pragma unroll
@@ -836,6 +844,7 @@ struct BigMatrixM {
     allc = false;  // A/B: the per-row gather only
 #endif
     const uint32_t rbq = (uint32_t)(uintptr_t)(Rb + q * NB);
+    if constexpr ((SKIP & 4) == 0) {
     if (allc) {
       const uint32_t bkq = (uint32_t)(uintptr_t)(Bk + (ti * 4 + q) * NB);
 #pragma unroll
@@ -866,6 +875,7 @@ struct BigMatrixM {
           }
         }
       }
+    }
     }
     }
     wave_lds_sync();
@@ -905,7 +915,7 @@ struct BigMatrixM {
     }
 #else  // A/B reference: row-block-major issue order
 #pragma unroll
-    for (int rb = 0; rb < NB; ++rb) {
+    for (int rb = 0; rb < ((SKIP & 1) ? 0 : NB); ++rb) {
       const int i = 16 * rb + (lane & 15);
 #ifndef CKMI_BIG_B_LATE
       const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
@@ -948,14 +958,14 @@ struct BigMatrixM {
 #define FPH_ARG
 #define FPH_PARAM
 #endif
-  template <int C>
+  template <int C, int SKIP = 0>
   __device__ __forceinline__ void panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                          int lane FPH_PARAM) {
     if constexpr (C < NB) {
 #pragma unroll 1  // (fully unrolled: 4x the code, and the ROCm 7.2 backend crashes in AMDGPU Rewrite AGPR-Copy-MFMA)
       for (int wo = 0; wo < 4; ++wo)
-        if (16 * C + 4 * wo < n) panel<C>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
-      panels<C + 1>(L, n, dm, ok, t, wid, lane FPH_ARG);
+        if (16 * C + 4 * wo < n) panel<C, SKIP>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
+      panels<C + 1, SKIP>(L, n, dm, ok, t, wid, lane FPH_ARG);
     }
   }
 
@@ -1197,6 +1207,7 @@ struct BigMatrixM {
     }
   }
 
+  template <int SKIP = 0>
   __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane, int n
 #ifdef CKMI_PHASE_TIMERS
                                          , unsigned long long (&fph)[6]
@@ -1218,7 +1229,7 @@ struct BigMatrixM {
 #ifndef CKMI_BIG_SYNC_BARRIER
     if constexpr (!LA)
 #endif
-      panels<0>(L, n, dm, ok, t, wid, lane FPH_ARG);
+      panels<0, SKIP>(L, n, dm, ok, t, wid, lane FPH_ARG);
 #ifndef CKMI_BIG_SYNC_BARRIER
     else {
       int* sw = sync_words(L);
@@ -1937,7 +1948,13 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             ok = M.factor(L, B, tid, wid, lane, n, fph);
 #else
 #ifdef CKMI_BIG_FACTOR_TWICE  // timing experiment: the factorisation's share of the run time
-            (void)M.factor(L, B, tid, wid, lane, n);
+#ifndef CKMI_BIG_FACTOR_TWICE_SKIP
+#define CKMI_BIG_FACTOR_TWICE_SKIP 0
+#endif
+            if constexpr (NB <= 11 && CKMI_BIG_FACTOR_TWICE_SKIP != 0)
+              (void)M.template factor<CKMI_BIG_FACTOR_TWICE_SKIP>(L, B, tid, wid, lane, n);
+            else
+              (void)M.factor(L, B, tid, wid, lane, n);
             __syncthreads();
             M.build(Jg, S.gamma, tid, n);
             __syncthreads();
