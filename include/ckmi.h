@@ -197,8 +197,8 @@ typedef struct {
 #define CKMI_RUN_ERRTEST 2
 #define CKMI_RUN_CONVFAIL 3
 /* the state left the physical domain after an accepted step and the run was ended there: a mass
- * fraction below -max(1e-3, 1e3 atol), or (energy runs) T outside [min_k T_low,k / 2, max_k T_high,k]
- * of the NASA-7 fits.  Without NNEG a loose tolerance can let trace concentrations go negative and
+ * fraction below -max(1e-3, 1e3 atol), or (energy runs) T outside [min_k T_low,k / 2, 2 max_k T_high,k]
+ * of the NASA-7 fits (the margin lets legitimately hot runs extrapolate the fits).  Without NNEG a loose tolerance can let trace concentrations go negative and
  * drive bimolecular rates of the wrong sign until the temperature runs away; the guard ends such a
  * reactor at once instead of letting it burn max_steps. */
 #define CKMI_RUN_RUNAWAY 4

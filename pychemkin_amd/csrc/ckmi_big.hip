@@ -915,7 +915,13 @@ struct BigMatrixM {
     }
 #else  // A/B reference: row-block-major issue order
 #pragma unroll
-    for (int rb = 0; rb < ((SKIP & 1) ? 0 : NB); ++rb) {
+    for (int rbi = 0; rbi < ((SKIP & 1) ? 0 : NB); ++rbi) {
+#ifdef CKMI_BIG_MFMA_ROT
+      // row block C first: the next panel's pivot-row gather (3 of 4 panels) reads it first
+      const int rb = (rbi + C) % NB;
+#else
+      const int rb = rbi;
+#endif
       const int i = 16 * rb + (lane & 15);
 #ifndef CKMI_BIG_B_LATE
       const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
