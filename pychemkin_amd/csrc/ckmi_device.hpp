@@ -83,19 +83,50 @@ constexpr int DPP_QUAD_2301 = 0x4E;  // quad_perm [2,3,0,1]
 constexpr int DPP_ROW_HALF_MIRROR = 0x141;
 constexpr int DPP_ROW_MIRROR = 0x140;
 
+// Across the four rows: the gfx950 row swaps (v_permlane16_swap pairs rows 0-1 and 2-3,
+// v_permlane32_swap the two halves) hand every lane its partner row's value, so each lane forms
+// (s0 + s1) + (s2 + s3) itself -- the association of the readlane form, bitwise, without the 8
+// readlanes and their SGPR round trip.  A/B form (CKMI_REDUCE_SWAP): bitwise the same results, no faster
+// (c3 244.7 vs 243.1 ms, c5 438.7 vs 439.5 ms on the A/B samples, profiles/r05_ab_reduce_swap_*.log).
+template <bool HALVES>
+__device__ __forceinline__ void row_swap(double v, double& own, double& other) {
+  const uint32_t lo = (uint32_t)__double2loint(v), hi = (uint32_t)__double2hiint(v);
+  const auto l = HALVES ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
+                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h = HALVES ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
+                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  own = __hiloint2double((int)h[0], (int)l[0]);  // {own, partner} in a row-dependent order:
+  other = __hiloint2double((int)h[1], (int)l[1]);  // only commutative combinations of the two
+}
 __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_mov<DPP_QUAD_1032>(v);
   v += dpp_mov<DPP_QUAD_2301>(v);
   v += dpp_mov<DPP_ROW_HALF_MIRROR>(v);
   v += dpp_mov<DPP_ROW_MIRROR>(v);
+#ifndef CKMI_REDUCE_SWAP
   return uni((bcast(v, 0) + bcast(v, 16)) + (bcast(v, 32) + bcast(v, 48)));
+#else
+  double a, b;
+  row_swap<false>(v, a, b);
+  v = a + b;
+  row_swap<true>(v, a, b);
+  return uni(a + b);
+#endif
 }
 __device__ __forceinline__ double wave_max(double v) {
   v = fmax(v, dpp_mov<DPP_QUAD_1032>(v));
   v = fmax(v, dpp_mov<DPP_QUAD_2301>(v));
   v = fmax(v, dpp_mov<DPP_ROW_HALF_MIRROR>(v));
   v = fmax(v, dpp_mov<DPP_ROW_MIRROR>(v));
+#ifndef CKMI_REDUCE_SWAP
   return uni(fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48))));
+#else
+  double a, b;
+  row_swap<false>(v, a, b);
+  v = fmax(a, b);
+  row_swap<true>(v, a, b);
+  return uni(fmax(a, b));
+#endif
 }
 
 // max of a u32 over the wave (DPP inside rows, readlanes across them); the pivot search
