@@ -587,6 +587,10 @@ struct BigMatrixM {
 
   // the 4 pivot steps of the panel k0 .. k0 + 3 on its columns in the row-per-lane layout (lane l: rows
   // l, l + 64, l + 128), pivots into ps
+  // JN: the row group (row >> 6) of the panel's diagonal rows, a compile-time constant (k0 .. k0 + 3 lie
+  // in one 16-row block, which never straddles a multiple of 64), so the natural pivot's row needs no
+  // select chain
+  template <int JN>
   __device__ __forceinline__ static void pivot_steps(double (&y)[NJ][4], const uint64_t (&rid)[NJ], int k0,
                                                      uint64_t (&dm)[NJ], bool& ok, int lane, int (&ps)[4]) {
 #pragma unroll
@@ -600,7 +604,9 @@ struct BigMatrixM {
       // one readlane of the row and a ballot of 3 compares per lane; the whole-wave u64 max (6
       // dependent DPP / row-swap stages) runs only when it fails.  Same pivot, same arithmetic.
       {
-        const int pn = k0 + s, pnl = pn & 63, pnj = pn >> 6;  // wave-uniform
+        const int pn = k0 + s, pnl = pn & 63;  // wave-uniform; pn >> 6 == JN
+#ifdef CKMI_BIG_PIVOT_SELECT
+        const int pnj = pn >> 6;
         uint64_t dmn = dm[0];
 #pragma unroll
         for (int j = 1; j < NJ; ++j) dmn = pnj == j ? dm[j] : dmn;
@@ -611,6 +617,11 @@ struct BigMatrixM {
           for (int j = 1; j < NJ; ++j) v = pnj == j ? y[j][s2] : v;
           pv[s2] = bcast(v, pnl);
         }
+#else
+        const uint64_t dmn = dm[JN];
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) pv[s2] = bcast(y[JN][s2], pnl);
+#endif
         const uint64_t kn = ((uint64_t)__float_as_uint((float)fabs(pv[s])) << 32) | (0xffffffffu - (uint32_t)pn);
         bool above = false;
 #pragma unroll
@@ -712,7 +723,7 @@ struct BigMatrixM {
 #pragma unroll
         for (int s = 0; s < 4; ++s) ps[s] = k0 + s;
       } else {
-        pivot_steps(y, rid, k0, dm, ok, lane, ps);
+        pivot_steps<(16 * C) / 64>(y, rid, k0, dm, ok, lane, ps);
       }
       // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
 #pragma unroll
@@ -1070,7 +1081,7 @@ struct BigMatrixM {
       }
     }
     int ps[4];
-    pivot_steps(y, rid, k0, dm, ok, lane, ps);
+    pivot_steps<(16 * CN) / 64>(y, rid, k0, dm, ok, lane, ps);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int row = lane + 64 * j;
