@@ -1494,6 +1494,36 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     if (upload(m, m->slot_of, &so) != CKMI_OK) return CKMI_ERR_HIP;
     I.slot_of = so;
   }
+  {
+    // Jacobian column lists of the workgroup kernel (ckmi_big.hip rhs_big): for species j the unit slots
+    // naming j, in device-slot order, so that a column block visits only its own slots instead of every
+    // slot of every reaction once per block
+    std::vector<std::vector<uint32_t>> lists(KK);
+    for (int i = 0; i < IIp; ++i) {
+      const uint32_t inf = uinfo[i];
+      if (inf & RX_GEN) continue;
+      const int nr = (inf >> 7) & 7, np = (inf >> 10) & 7;
+      for (int sl = 0; sl < 8; ++sl) {
+        const bool prod = sl >= 4;
+        const int u0 = sl & 3;
+        if (u0 >= (prod ? np : nr)) continue;
+        const int j = (int)(((prod ? ups[i] : urs[i]) >> (8 * u0)) & 0xffu);
+        if (j < KK) lists[j].push_back((uint32_t)i | ((uint32_t)sl << 16));
+      }
+    }
+    std::vector<int> ptr(KK + 1, 0);
+    std::vector<uint32_t> ent;
+    for (int j = 0; j < KK; ++j) {
+      ent.insert(ent.end(), lists[j].begin(), lists[j].end());
+      ptr[j + 1] = (int)ent.size();
+    }
+    if (ent.empty()) ent.push_back(0u);
+    const int* dp = nullptr;
+    const uint32_t* de = nullptr;
+    if (upload(m, ptr, &dp) != CKMI_OK || upload(m, ent, &de) != CKMI_OK) return CKMI_ERR_HIP;
+    I.jcol_ptr = dp;
+    I.jcol_ent = de;
+  }
   void* p = nullptr;
   HIP_CHECK(hipMalloc(&p, blob.size()));
   m->allocs.push_back(p);

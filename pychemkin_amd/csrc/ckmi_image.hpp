@@ -39,6 +39,10 @@ constexpr int KK_IMAGE_MAX = 255;  // species bytes: the dummy slot KKp - 1 must
 struct MechImage {
   const uint4* blob;  // device copy of the image
   const int* slot_of; // device: original reaction index -> device slot
+  // device: the workgroup kernel's Jacobian columns, CSR over species j: the (device slot i, unit slot sl)
+  // pairs whose slot species is j, packed i | sl << 16 (general reactions excluded)
+  const int* jcol_ptr;       // [KK + 1]
+  const uint32_t* jcol_ent;  // [jcol_ptr[KK]]
   int bytes;          // multiple of 16
   int KK, KKp, II, IIp, G, naux;
   int sp_one;         // dummy species slot (KKp - 1)
