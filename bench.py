@@ -10,6 +10,10 @@ wall time.  PCIe transfers are excluded from `value`; the PCIe-inclusive rate of
 reported beside it (`pcie_inclusive`).
 
 Secondary lines in the same JSON object (each sharded over the ranks, max-over-ranks timing):
+  c1   configs[0]: ONE GRI-3.0 CONP reactor (CH4/air phi 1, 1200 K, 1 atm, TIFP, 1e-10/1e-8) through the
+       drop-in GivenPressureBatchReactor_EnergyConservation.run(): per-call wall latency (median of 7),
+       solver counts, the oracle on one core; plus the reference's serial 20-condition loop
+       (ignitiondelay.py:127-144) against one BatchSweep launch of the same 20 (rank 0 only)
   c4   configs[3]: 2^20 GRI-3.0 reactors, CONP/CONV alternating, strong scaling (total fixed)
   c5   configs[4]: 262,144 reactors of the 161-species stand-in mechanism (no ~160-species
        n-heptane mechanism exists offline; parity with Chemkin unpinned), workgroup-per-reactor
@@ -26,7 +30,7 @@ over the kernel time measured with HIP events on the launch stream) and, on rank
 CPU baseline: the oracle C restatement (OpenMP) timed on a bounded sample of the same workload on
 this host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c3,c4,c5,rop,lu,rop161,ropext,pfr,hcci]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--lines c1,c3,c4,c5,rop,lu,rop161,ropext,pfr,hcci]
 
 Launch: under torch.distributed.run (RANK / WORLD_SIZE / LOCAL_RANK set) every process is one
 rank.  Run directly with --gpus N > 1, bench.py is its own launcher: it starts N child processes
@@ -490,6 +494,74 @@ def model_line(kind, dm, dev, mech, ops, world, rank, args):
             "cpu_baseline": cpu}
 
 
+def c1_line(args):
+    """configs[0] latency: one reactor through the drop-in API, the way a PyChemkin user runs it."""
+    import pychemkin_amd as ck
+    from pychemkin_amd.batch import BatchSweep
+
+    chem = ck.Chemistry(chem=os.path.join(ROOT, "data", "grimech30_chem.inp"),
+                        therm=os.path.join(ROOT, "data", "grimech30_thermo.dat"), label="GRI 3.0")
+    chem.preprocess()
+    fuel = ck.Mixture(chem)
+    fuel.X = [("CH4", 1.0)]
+    air = ck.Mixture(chem)
+    air.X = [("O2", 0.21), ("N2", 0.79)]
+    mix = ck.Mixture(chem)
+    mix.X_by_Equivalence_Ratio(chem, fuel.X, air.X, np.zeros(chem.KK), ["CO2", "H2O", "N2"], 1.0)
+    mix.temperature = 1200.0
+    mix.pressure = P_ATM
+    r = ck.GivenPressureBatchReactor_EnergyConservation(mix, label="c1")
+    r.volume = 1.0
+    r.time = RUN["t_end"]
+    r.tolerances = (RUN["atol"], RUN["rtol"])
+    r.set_ignition_delay(method="T_inflection")
+    assert r.run() == 0  # warm-up: device mechanism, code objects, JIT
+    lat = []
+    for _ in range(7):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rc = r.run()
+        tau = r.get_ignition_delay()
+        lat.append((time.perf_counter() - t0) * 1e3)
+        assert rc == 0
+    stats = r.solver_statistics
+    from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
+
+    orc = Oracle(chem.mechanism())
+    cl = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        ro, _ = orc.reactor(mix.temperature, mix.pressure, 1.0, mix.Y, problem=1, **RUN)
+        cl.append((time.perf_counter() - t0) * 1e3)
+    # the reference's serial loop (ignitiondelay.py:127-144): one run() per condition, T0 += 20 K
+    temps = 1200.0 + 20.0 * np.arange(20)
+    t0 = time.perf_counter()
+    taus = []
+    for T in temps:
+        r.temperature = T
+        assert r.run() == 0
+        taus.append(r.get_ignition_delay())
+    loop_s = time.perf_counter() - t0
+    sweep = BatchSweep(chem, problem="CONP", energy="ENERGY", t_end=RUN["t_end"], atol=RUN["atol"], rtol=RUN["rtol"],
+                       ignition="T_inflection", devices=[torch.cuda.current_device()])
+    sweep.run(temps[:2], P_ATM, Y0=mix.Y)  # warm-up
+    t0 = time.perf_counter()
+    br = sweep.run(temps, P_ATM, Y0=mix.Y)
+    batch_s = time.perf_counter() - t0
+    return {"metric": "single-reactor latency (configs[0]: GRI-3.0 CONP CH4/air phi 1, 1200 K, 1 atm, t_end 1 s, TIFP, "
+                      "1e-10/1e-8, drop-in run())",
+            "latency_ms": float(np.median(lat)), "latency_ms_all": lat, "tau_ms": tau, "unit": "ms",
+            "higher_is_better": False, "solver": {k: int(v) for k, v in stats.items()},
+            "cpu_baseline": {"value": float(np.median(cl)), "unit": "ms", "cores": 1, "kind": "port",
+                             "sample": "the same reactor, oracle C restatement, 1 thread, median of 3",
+                             "tau_rel_diff_vs_gpu": abs(ro.tau * 1e3 / tau - 1), "nst": ro.nst, "nfe": ro.nfe,
+                             "nlu": ro.nlu},
+            "serial_loop_20": {"seconds": loop_s, "per_run_ms": loop_s / 20 * 1e3,
+                               "pattern": "ignitiondelay.py:127-144: reactor.temperature = T; run(); get_ignition_delay()"},
+            "batch_20": {"seconds": batch_s, "speedup_vs_serial_loop": loop_s / batch_s,
+                         "tau_max_rel_diff_vs_loop": float(np.max(np.abs(br.tau * 1e3 / np.asarray(taus) - 1)))}}
+
+
 def _free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
         so.bind(("127.0.0.1", 0))
@@ -560,8 +632,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reactors", type=int, default=0, help="override the headline reactors per GPU (0 = full 65,536)")
     ap.add_argument("--sub-reactors", type=int, default=0, help="cap the c4 / c5 shards (0 = full sweeps)")
-    ap.add_argument("--lines", default="c3,c4,c5,rop,lu,rop161,ropext,pfr,hcci",
-                    help="comma list of: c3 (headline, always run), c4, c5, rop, lu, rop161, ropext, pfr, hcci")
+    ap.add_argument("--lines", default="c1,c3,c4,c5,rop,lu,rop161,ropext,pfr,hcci",
+                    help="comma list of: c1, c3 (headline, always run), c4, c5, rop, lu, rop161, ropext, pfr, hcci")
     ap.add_argument("--rop-states", type=int, default=10_000_000)
     ap.add_argument("--lu-systems", type=int, default=16384)
     ap.add_argument("--big-states", type=int, default=1_000_000)
@@ -665,6 +737,7 @@ def main():
                            label=f"data/gri30_tracer161_ext (PLOG, HIGH, FORD/RORD, fractional, wide), KK = {em.KK}, "
                                  f"II = {em.II}")
 
+    c1 = c1_line(args) if "c1" in lines and rank == 0 else None
     pfr = model_line("pfr", dm, dev, mech, ops, world, rank, args) if "pfr" in lines else None
     hcci = model_line("hcci", dm, dev, mech, ops, world, rank, args) if "hcci" in lines else None
 
@@ -693,6 +766,7 @@ def main():
             "roofline": reactor_roofline(ops, stats, kern_s, "reactor_kernel<54>", "reactor", n),
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "c1": c1,
             "c4": c4,
             "c5": c5,
             "rop": rop,

@@ -38,8 +38,13 @@ extern "C" {
 #endif
 
 /* ABI version returned by ckmi_version(): bumped whenever a struct layout or a table stride changes.
- * 1: round-1/2 layout (CKMI_SLOTS 4, ckmi_reactor_cfg up to prof3_v); 2: CKMI_SLOTS 8, cfg.eng[20], cfg.tran. */
-#define CKMI_ABI_VERSION 2
+ * 1: round-1/2 layout (CKMI_SLOTS 4, ckmi_reactor_cfg up to prof3_v); 2: CKMI_SLOTS 8, cfg.eng[20], cfg.tran;
+ * 3: desc.MM / desc.ncf (element counts) and cfg.no_elem_proj. */
+#define CKMI_ABI_VERSION 3
+
+/* the reactor kernels hold element conservation (ckmi_reactor_cfg.no_elem_proj) for mechanisms whose
+ * species contain at most this many distinct elements */
+#define CKMI_PROJ_MMAX 8
 
 #define CKMI_SLOTS 8 /* distinct species per reaction side in the flat tables ([II][CKMI_SLOTS] arrays) */
 
@@ -98,6 +103,8 @@ typedef struct {
   const double* plog_par;  /* [npl][4] ln P (dyn/cm2), ln A (cgs), b, E/R (K); ascending, distinct P */
   const double* ford;      /* [II][CKMI_SLOTS] forward order of each reactant slot (FORD; = rnu without it), or NULL */
   const double* rord;      /* [II][CKMI_SLOTS] reverse order of each product slot (RORD; = pnu without it), or NULL */
+  int32_t MM;              /* elements (0 with ncf NULL: the reactors do not hold element conservation) */
+  const int32_t* ncf;      /* [MM][KK] element counts of each species (KINGetGasSpeciesComposition), or NULL */
 } ckmi_mech_desc;
 
 typedef struct ckmi_mech ckmi_mech; /* opaque: tables resident in HBM of one device */
@@ -141,6 +148,11 @@ typedef struct {
   /* [KK][8] device: ln-T cubics of ln eta_k [g/(cm s)] (0..3, ckmi_transport_fit) and ln lambda_k
    * [erg/(cm s K)] (4..7, ckmi_conductivity_fit) for the engine's ICHX wall heat transfer (else NULL) */
   const double* tran;
+  /* 0 (default): element conservation is held to 0.1 rtol -- after an accepted step whose element content
+   * (sum_k a_mk Y_k / W_k) has drifted by more than 0.1 rtol of the largest element content from the
+   * initial mixture's, the corrector is projected back onto it (oracle/ckoracle.c elem_project);
+   * 1: no projection (diagnostics) */
+  int32_t no_elem_proj;
 } ckmi_reactor_cfg;
 
 /* engine parameter block (ckmi_reactor_cfg.eng; oracle/ckoracle.h CKO_ENG_* is the same layout) */
@@ -311,6 +323,12 @@ int ckmi_engine_heat_rates(const ckmi_mech* mech, const ckmi_reactor_cfg* cfg, d
  * integrators on the same GRI-3.0 reactors), 2 / 3 = the wave kernel with the FP64 / FP32-stored
  * Newton inverse whatever the tolerances.  Process-wide. */
 int ckmi_set_reactor_path(int32_t path);
+
+/* Host-only capacity query of the workgroup-per-reactor kernel (no GPU needed): the largest mechanism
+ * image in bytes (MechImage, staged in LDS) it accepts for nvar = KK + 1 state variables, KKp padded
+ * species and G third-body groups on a CU with lds_max bytes of LDS; -1 if none fits.  A mechanism
+ * whose image is larger gets CKMI_ERR_SIZE from ckmi_reactor_run. */
+int ckmi_big_max_image_bytes(int32_t nvar, int32_t KKp, int32_t G, int32_t lds_max);
 
 /* Batched dense LU of Newton iteration matrices too large for one wave (mechanisms with more
  * than 63 species).  Replaces the factorisation inside the reference's

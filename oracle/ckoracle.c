@@ -689,6 +689,11 @@ typedef struct {
   double rtol, atol;
   int nneg;
   rctx* ctx;
+  /* element projection of the accepted corrector: npe elements (0 = off), pc[m][k] = a_mk / W_k for
+   * state component k = 1 + species, eb0[m] = the reactor's initial element content [mol/g] */
+  int npe;
+  double pc[CKO_PROJ_MMAX][NMAX];
+  double eb0[CKO_PROJ_MMAX];
 } bdf;
 
 /* x^(1/p) for the step-size / order heuristics, in single precision as on the device
@@ -809,6 +814,82 @@ static void adjust_order(bdf* b, int deltaq) {
     for (int j = 2; j < q; ++j)
       for (int i = 0; i < b->n; ++i) b->zn[j][i] -= l[j] * b->zn[q][i];
   }
+}
+
+/* Element projection of an accepted step (CVODE's projection of the corrector, CVodeSetProjFn, restated for
+ * the linear element constraints).  A closed reactor conserves the element content e_m = sum_k a_mk Y_k / W_k
+ * exactly; the modified Newton iteration conserves it only to the accuracy of the linear solves (J is parked
+ * in FP32 and M^-1 is inexact: c M^-1 != c), so without this the element totals drift by up to a few 1e-7
+ * over a run.  Conservation is held to PROJ_TOL rtol: after the error test passes, when the residual of
+ * y = zn[0] + acor, max_m |C y - eb0|_m / max_m eb0_m, exceeds PROJ_TOL rtol, y is moved to the nearest state with
+ * C y = eb0 in the weighted norm sum_k dy_k^2 / w_k, w_k = Y_k W_k (moles: dY_k = Y_k sum_m a_mk lambda_m, the
+ * element-potential form of equilibrium solvers -- every species changes by a relative amount of the size of
+ * the drift, ~1e-10, so none changes sign; error weights (rtol |y| + atol)^2 put corrections of atol size on
+ * trace species and drove them negative under NNEG), by
+ *     (C W C^T + eps diag(C W C^T)) lambda = C y - eb0,   acor_k -= w_k sum_m C_mk lambda_m,
+ * before the history update, so the whole Nordsieck array moves with it.  eps = PROJ_RIDGE keeps element
+ * combinations carried only by trace species from amplifying the residual; an element with no weight at all
+ * (absent from the mixture) is left out; species at or below 0 get no weight.  Both device kernels do the same
+ * (ckmi_reactor.hpp elem_project_wave, ckmi_big.hip elem_project_big: one fused 8-value reduction of the
+ * residual per accepted step, the Gram matrix only past the threshold).  Below the threshold the step is left as it is (most runs are
+ * never projected: their drift stays far below rtol), which keeps the integrator's results those of the
+ * unconstrained BDF (e.g. the sensitivity golden's finite differences). */
+#define PROJ_RIDGE 1e-8
+#define PROJ_TOL 0.1
+static int elem_project(bdf* b) {
+  const int n = b->n, M = b->npe;
+  if (M <= 0) return 0;
+  double r[CKO_PROJ_MMAX], G[CKO_PROJ_MMAX][CKO_PROJ_MMAX], w[NMAX];
+  for (int m = 0; m < M; ++m) {
+    r[m] = 0.0;
+    for (int l = 0; l < M; ++l) G[m][l] = 0.0;
+  }
+  for (int k = 1; k < n; ++k) {
+    const double y = b->zn[0][k] + b->acor[k];
+    w[k] = y > 0.0 ? y * b->ctx->m->wt[k - 1] : 0.0;
+    for (int m = 0; m < M; ++m) {
+      const double cm = b->pc[m][k];
+      r[m] += cm * y;
+      const double cw = cm * w[k];
+      for (int l = 0; l <= m; ++l) G[m][l] += cw * b->pc[l][k];
+    }
+  }
+  double rmax = 0.0, bmax = 0.0;
+  for (int m = 0; m < M; ++m) {
+    rmax = fmax(rmax, fabs(r[m] - b->eb0[m]));
+    bmax = fmax(bmax, b->eb0[m]);
+  }
+  if (!(rmax > PROJ_TOL * b->rtol * bmax)) return 0;
+  /* LDL^T of the ridged Gram matrix (lower triangle), elements without weight dropped */
+  double L[CKO_PROJ_MMAX][CKO_PROJ_MMAX], dg[CKO_PROJ_MMAX], z[CKO_PROJ_MMAX], lam[CKO_PROJ_MMAX];
+  int live[CKO_PROJ_MMAX];
+  for (int j = 0; j < M; ++j) {
+    live[j] = G[j][j] > 0.0;
+    double dj = G[j][j] * (1.0 + PROJ_RIDGE);
+    for (int k = 0; k < j; ++k) dj -= L[j][k] * L[j][k] * dg[k];
+    dg[j] = live[j] ? dj : 1.0;
+    for (int i = j + 1; i < M; ++i) {
+      double v = G[i][j];
+      for (int k = 0; k < j; ++k) v -= L[i][k] * L[j][k] * dg[k];
+      L[i][j] = live[j] ? v / dg[j] : 0.0;
+    }
+  }
+  for (int j = 0; j < M; ++j) {
+    double v = r[j] - b->eb0[j];
+    for (int k = 0; k < j; ++k) v -= L[j][k] * z[k];
+    z[j] = live[j] ? v : 0.0;
+  }
+  for (int j = M - 1; j >= 0; --j) {
+    double v = z[j] / dg[j];
+    for (int i = j + 1; i < M; ++i) v -= L[i][j] * lam[i];
+    lam[j] = live[j] ? v : 0.0;
+  }
+  for (int k = 1; k < n; ++k) {
+    double s = 0.0;
+    for (int m = 0; m < M; ++m) s += b->pc[m][k] * lam[m];
+    b->acor[k] -= w[k] * s;
+  }
+  return 1;
 }
 
 enum { NF_FIRST = 0, NF_CONV_FAIL = 1, NF_ERR_FAIL = 2 };
@@ -1052,6 +1133,25 @@ static int bdf_step(bdf* b, int* nst_global) {
   for (int i = b->q; i >= 2; --i) b->tau[i] = b->tau[i - 1];
   if (b->q == 1 && b->nst > 1) b->tau[2] = b->tau[1];
   b->tau[1] = b->h;
+  /* the order-selection norms of a step that selects (qwait reaches 0 below), from the corrector before
+   * the element projection: the device kernels take them in the step's one fused reduction beside the
+   * element residual (ckmi_big.hip: one workgroup barrier per accepted step) */
+  double ddn = 0.0, dup = 0.0;
+  if (b->etamax != 1.0 && b->qwait == 1) {
+    if (b->q > 1) {
+      for (int i = 0; i < b->n; ++i) b->tempv[i] = b->zn[b->q][i] + b->l[b->q] * b->acor[i];
+      ddn = wrms(b, b->tempv) * b->tq[1];
+    }
+    if (b->q != QMAX && b->saved_tq5 != 0.0) {
+      const double hr = b->h / b->tau[2];
+      double hrL = hr;
+      for (int j = 1; j < b->L; ++j) hrL *= hr;
+      const double cquot = (b->tq[5] / b->saved_tq5) * hrL;
+      for (int i = 0; i < b->n; ++i) b->tempv[i] = b->acor[i] - cquot * b->zn[QMAX][i];
+      dup = wrms(b, b->tempv) * b->tq[3];
+    }
+  }
+  elem_project(b);
   for (int j = 0; j <= b->q; ++j)
     for (int i = 0; i < b->n; ++i) b->zn[j][i] += b->l[j] * b->acor[i];
   b->qwait--;
@@ -1073,19 +1173,8 @@ static int bdf_step(bdf* b, int* nst_global) {
     } else {
       b->qwait = 2;
       double etaqm1 = 0.0, etaqp1 = 0.0;
-      if (b->q > 1) {
-        const double ddn = wrms(b, b->zn[b->q]) * b->tq[1];
-        etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, b->q) + ADDON);
-      }
-      if (b->q != QMAX && b->saved_tq5 != 0.0) {
-        const double hr = b->h / b->tau[2];
-        double hrL = hr;
-        for (int j = 1; j < b->L; ++j) hrL *= hr;
-        const double cquot = (b->tq[5] / b->saved_tq5) * hrL;
-        for (int i = 0; i < b->n; ++i) b->tempv[i] = b->acor[i] - cquot * b->zn[QMAX][i];
-        const double dup = wrms(b, b->tempv) * b->tq[3];
-        etaqp1 = 1.0 / (eta_root(BIAS3 * dup, b->L + 1) + ADDON);
-      }
+      if (b->q > 1) etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, b->q) + ADDON);
+      if (b->q != QMAX && b->saved_tq5 != 0.0) etaqp1 = 1.0 / (eta_root(BIAS3 * dup, b->L + 1) + ADDON);
       const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
       if (etam < THRESH) {
         b->eta = 1.0;
@@ -1177,6 +1266,15 @@ int cko_reactor(const cko_mech* m, const cko_cfg* cfg, double T0, double P0, dou
   b->rtol = cfg->rtol;
   b->atol = cfg->atol;
   b->nneg = cfg->nneg;
+  b->npe = (!cfg->no_elem_proj && m->ncf && m->MM > 0 && m->MM <= CKO_PROJ_MMAX) ? m->MM : 0;
+  for (int e = 0; e < b->npe; ++e) {
+    b->pc[e][0] = 0.0;
+    b->eb0[e] = 0.0;
+    for (int k = 0; k < KK; ++k) {
+      b->pc[e][1 + k] = m->ncf[(size_t)e * KK + k] / m->wt[k];
+      b->eb0[e] += b->pc[e][1 + k] * Y0[k];
+    }
+  }
   const double Wbar0 = mean_wt(m, Y0);
   const double rho0 = P0 * Wbar0 / (RU * T0);
   double Vstart = V0;

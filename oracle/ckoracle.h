@@ -41,7 +41,11 @@ typedef struct {
   const double* plog_par;/* [npl][4]: ln P (dyn/cm2), ln A (cgs), b, E/R; ascending P per reaction */
   const double* ford;    /* [II][4] forward order of each reactant slot (FORD; = rnu without it), or NULL */
   const double* rord;    /* [II][4] reverse order of each product slot (RORD; = pnu without it), or NULL */
+  int MM;                /* elements (element projection of the corrector; 0 or > CKO_PROJ_MMAX: none) */
+  const int* ncf;        /* [MM][KK] element counts of each species, or NULL */
 } cko_mech;
+
+#define CKO_PROJ_MMAX 8 /* elements the corrector's element projection handles (= CKMI_PROJ_MMAX) */
 
 typedef struct {
   int problem;      /* 1 CONP, 2 CONV */
@@ -77,6 +81,7 @@ typedef struct {
   const double* eng;  /* problem 4 (single-zone IC engine): CKO_ENG_N parameters, CKO_ENG_* layout */
   const double* tran; /* [KK][8]: cubic ln-T fits of ln viscosity [g/cm-s] (0..3) and ln conductivity
                          [erg/cm-K-s] (4..7), for the engine's wall heat transfer (NULL: none) */
+  int no_elem_proj;   /* 1: no element projection of the accepted corrector (A/B and diagnostics only) */
 } cko_cfg;
 
 /* engine parameter block (problem 4; same layout as ckmi_reactor_cfg.eng, include/ckmi.h) */

@@ -57,7 +57,7 @@ class _Mech(ct.Structure):
         (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
                           "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val",
                           "plog_ptr", "plog_par", "ford", "rord")
-    ]
+    ] + [("MM", ct.c_int), ("ncf", _P)]
 
 
 class _Cfg(ct.Structure):
@@ -69,7 +69,7 @@ class _Cfg(ct.Structure):
         ("gfac", ct.c_double), ("qloss", ct.c_double), ("htc", ct.c_double), ("areaq", ct.c_double),
         ("tamb", ct.c_double), ("pert_rxn", ct.c_int), ("pert_fac", ct.c_double), ("nprof2", ct.c_int),
         ("prof2_kind", ct.c_int), ("prof2_t", _P), ("prof2_v", _P), ("nprof3", ct.c_int), ("prof3_t", _P),
-        ("prof3_v", _P), ("eng", _P), ("tran", _P),
+        ("prof3_v", _P), ("eng", _P), ("tran", _P), ("no_elem_proj", ct.c_int),
     ]
 
 
@@ -104,8 +104,13 @@ class Oracle:
         self.wt = t["wt"]
         s = _Mech()
         s.KK, s.II = self.KK, self.II
-        for name, _ in _Mech._fields_[2:]:
+        for name, _ in _Mech._fields_[2:-2]:
             setattr(s, name, _ptr(self._keep[name]))
+        # element counts: the corrector's element projection (ckoracle.c elem_project)
+        ncf = getattr(mech, "ncf", None)
+        if ncf is not None:
+            self._keep["ncf"] = np.ascontiguousarray(ncf, np.int32)
+            s.MM, s.ncf = int(self._keep["ncf"].shape[0]), _ptr(self._keep["ncf"])
         self._mech = s
         L = lib()
         L.cko_thermo.argtypes = [ct.POINTER(_Mech), ct.c_double, _P, _P, _P]
@@ -151,10 +156,12 @@ class Oracle:
                  ign_mode=None, ign_val=0.0, ign_species=0, ign_stop=False, max_steps=0, profile=None,
                  prof_kind=0, gfac=1.0, qloss=0.0, htc=0.0, areaq=0.0, tamb=300.0, asteps=0, pert_rxn=-1,
                  pert_fac=1.0, profile2=None, prof2_kind=0, avar=-1, avalue=0.0, profile3=None, engine=None,
-                 tran=None):
+                 tran=None, elem_proj=True):
         """asteps / avar / avalue (adaptive output points) do not change the integration and are
-        accepted for signature parity with pychemkin_amd._native.make_cfg."""
+        accepted for signature parity with pychemkin_amd._native.make_cfg.  elem_proj=False turns the
+        element projection of the corrector off (A/B and drift diagnostics)."""
         c = _Cfg()
+        c.no_elem_proj = 0 if elem_proj else 1
         c.prof_kind, c.gfac, c.qloss, c.htc, c.areaq, c.tamb = int(prof_kind), gfac, qloss, htc, areaq, tamb
         c.pert_rxn, c.pert_fac = int(pert_rxn), float(pert_fac)
         c.problem, c.energy, c.t_end, c.atol, c.rtol = problem, energy, t_end, atol, rtol

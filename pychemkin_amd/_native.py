@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # _lib/libckmi_prof.so, used by scripts/phase_profile.py); it is never a CPU path.
 LIB_PATH = os.environ.get("CKMI_LIB") or os.path.join(_HERE, "_lib", "libckmi.so")
 
-ABI_VERSION = 2  # CKMI_ABI_VERSION (include/ckmi.h): the layouts of MechDesc / ReactorCfg below
+ABI_VERSION = 3  # CKMI_ABI_VERSION (include/ckmi.h): the layouts of MechDesc / ReactorCfg below
 NSTAT = 8
 STAT_NAMES = ("nst", "nfe", "nje", "nlu", "ncf", "nef", "status", "nni")
 RUN_STATUS = {0: "ok", 1: "max_steps", 2: "error_test_failures", 3: "convergence_failures", 4: "runaway",
@@ -40,7 +40,22 @@ class MechDesc(ct.Structure):
         (n, _P) for n in ("wt", "thermo", "rtype", "rev", "nr", "np", "rsp", "psp", "rnu", "pnu", "arr", "low",
                           "revp", "has_rev", "ftype", "fpar", "tbsp", "eff_ptr", "eff_sp", "eff_val",
                           "plog_ptr", "plog_par", "ford", "rord")
-    ]
+    ] + [("MM", ct.c_int32), ("ncf", _P)]
+
+
+# the pointer fields of MechDesc (MM is a count, ncf optional: tables without element counts leave the
+# element projection off)
+_DESC_PTRS = [n for n, t in MechDesc._fields_[2:] if t is _P and n != "ncf"]
+
+
+def fill_desc(d: "MechDesc", tables: Dict[str, np.ndarray], keep: Dict[str, np.ndarray]) -> None:
+    d.KK, d.II = int(tables["KK"]), int(tables["II"])
+    for name in _DESC_PTRS:
+        setattr(d, name, keep[name].ctypes.data)
+    if "ncf" in keep and "MM" in tables:
+        d.MM, d.ncf = int(tables["MM"]), keep["ncf"].ctypes.data
+    else:
+        d.MM, d.ncf = 0, None
 
 
 class ReactorCfg(ct.Structure):
@@ -53,7 +68,7 @@ class ReactorCfg(ct.Structure):
         ("areaq", ct.c_double), ("tamb", ct.c_double), ("asteps", ct.c_int32), ("avar", ct.c_int32),
         ("avalue", ct.c_double), ("nprof2", ct.c_int32), ("prof2_kind", ct.c_int32), ("prof2_t", ct.c_double * 64),
         ("prof2_v", ct.c_double * 64), ("nprof3", ct.c_int32), ("prof3_t", ct.c_double * 64),
-        ("prof3_v", ct.c_double * 64), ("eng", ct.c_double * 20), ("tran", _P),
+        ("prof3_v", ct.c_double * 64), ("eng", ct.c_double * 20), ("tran", _P), ("no_elem_proj", ct.c_int32),
     ]
 
 
@@ -83,6 +98,7 @@ PROTOTYPES = {
     "ckmi_engine_heat_rates": (ct.c_int, [_P, ct.POINTER(ReactorCfg), ct.c_double, ct.c_double, _P, ct.c_int32, _P, _P,
                                           _P, _P, _P]),
     "ckmi_set_reactor_path": (ct.c_int, [ct.c_int32]),
+    "ckmi_big_max_image_bytes": (ct.c_int, [ct.c_int32, ct.c_int32, ct.c_int32, ct.c_int32]),
     "ckmi_set_rop_path": (ct.c_int, [ct.c_int32]),
     "ckmi_rop_jit_state": (ct.c_int, [_P, ct.POINTER(ct.c_int32)]),
     "ckmi_rop_jit_source": (ct.c_int, [ct.POINTER(MechDesc), ct.c_char_p, ct.c_int64, ct.POINTER(ct.c_int64)]),
@@ -181,6 +197,8 @@ def parse_mechanism(chem_text: str, therm_text: str = ""):
         t["eff_val"] = np.ctypeslib.as_array(ct.cast(d.eff_val, ct.POINTER(ct.c_double)), (max(ne, 1),))[:ne].copy()
         t["plog_par"] = np.ctypeslib.as_array(ct.cast(d.plog_par, ct.POINTER(ct.c_double)),
                                               (max(npl, 1), 4)).copy()
+        t["MM"] = np.int32(d.MM)
+        t["ncf"] = np.ctypeslib.as_array(ct.cast(d.ncf, ct.POINTER(ct.c_int32)), (MM, KK)).copy()
         sp = ct.create_string_buffer(16 * KK + 1)
         el = ct.create_string_buffer(16 * MM + 1)
         awt = np.zeros(MM)
@@ -220,14 +238,16 @@ def make_cfg(energy: int = 1, t_end: float = 1.0, atol: float = 1e-12, rtol: flo
              ign_stop: bool = False, max_steps: int = 0, profile=None, prof_kind: int = 0, gfac: float = 1.0,
              qloss: float = 0.0, htc: float = 0.0, areaq: float = 0.0, tamb: float = 300.0,
              asteps: int = 0, avar: int = -1, avalue: float = 0.0, profile2=None, prof2_kind: int = 0,
-             profile3=None, engine=None, tran=None) -> ReactorCfg:
+             profile3=None, engine=None, tran=None, elem_proj: bool = True) -> ReactorCfg:
     """Typed form of the reactor keywords (see include/ckmi.h ckmi_reactor_cfg).
 
     profile: (x, v) VPRO/PPRO (prof_kind 0) or TPRO (prof_kind 1); profile2: (x, v) QPRO
     (prof2_kind 1) or AEXT (prof2_kind 2); profile3: (x, v) AEXT beside a QPRO profile2; engine: the
     CKMI_ENG_* parameter block of problem 4 (<= 20 values); tran: device tensor [KK][8] of viscosity and
-    conductivity fits (the engine's ICHX heat transfer), kept alive by the returned struct."""
+    conductivity fits (the engine's ICHX heat transfer), kept alive by the returned struct; elem_proj=False
+    turns off the element projection of the corrector (diagnostics; include/ckmi.h no_elem_proj)."""
     c = ReactorCfg()
+    c.no_elem_proj = 0 if elem_proj else 1
     if engine is not None:
         e = np.asarray(engine, np.float64)
         if e.size > 20:
@@ -281,9 +301,7 @@ def mech_desc(tables: Dict[str, np.ndarray]):
     """ckmi_mech_desc view of flat mechanism tables; returns (desc, arrays kept alive)."""
     keep = {k: np.ascontiguousarray(v) for k, v in tables.items() if isinstance(v, np.ndarray) and v.ndim > 0}
     d = MechDesc()
-    d.KK, d.II = int(tables["KK"]), int(tables["II"])
-    for name, _ in MechDesc._fields_[2:]:
-        setattr(d, name, keep[name].ctypes.data)
+    fill_desc(d, tables, keep)
     return d, keep
 
 
@@ -323,9 +341,7 @@ class DeviceMechanism:
         self.II = int(tables["II"])
         keep = {k: np.ascontiguousarray(v) for k, v in tables.items() if isinstance(v, np.ndarray) and v.ndim > 0}
         d = MechDesc()
-        d.KK, d.II = self.KK, self.II
-        for name, _ in MechDesc._fields_[2:]:
-            setattr(d, name, keep[name].ctypes.data)
+        fill_desc(d, tables, keep)
         h = _P()
         with torch.cuda.device(self.device):
             _check(lib().ckmi_mech_create(ct.byref(d), ct.byref(h)), "ckmi_mech_create")

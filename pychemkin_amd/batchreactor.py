@@ -23,10 +23,10 @@ from __future__ import annotations
 import numpy as np
 
 from . import _native
-from .constants import R_GAS
+from .constants import P_ATM, R_GAS
 from .logger import logger
 from .mixture import Mixture, interpolate_mixtures
-from .reactormodel import Profile, ReactorError, ReactorModel
+from .reactormodel import Keyword, Profile, ReactorError, ReactorModel
 from .utilities import find_interpolate_parameters
 
 
@@ -89,6 +89,8 @@ class BatchReactors(ReactorModel):
         if value <= 0.0:
             raise ReactorError("simulation end time must be > 0")
         self._endtime = float(value)
+        if "TIME" not in self._inputcheck:
+            self._inputcheck.append("TIME")
 
     @property
     def area(self) -> float:
@@ -338,8 +340,90 @@ class BatchReactors(ReactorModel):
             **heat, **adap)
 
     # ------------------------------------------------------------------ run
+    def full_keyword_lines(self) -> list:
+        """The keyword block of the full-keyword mode, as the reference assembles it
+        (batchreactor.py:822-925): the keywords set so far, ATOL / RTOL, TRAN, CONP|CONV, ENRG|TGIV, PRES [atm],
+        TEMP, TIME, REAC species mole fraction (> 1e-12), the profile points (PPRO in atm), QRGEQ, END."""
+        lines = [kw.getvalue_as_string()[1] for kw in self._keyword_list if kw.keyphrase not in ("END", "QRGEQ")]
+        if "ATOL" not in self._keyword_index:
+            lines.append(f"ATOL    {self._absolute_tolerance!r}")
+        if "RTOL" not in self._keyword_index:
+            lines.append(f"RTOL    {self._relative_tolerance!r}")
+        lines.append("TRAN")
+        lines.append("CONP" if self._problemtype == self.ProblemTypes["CONP"] else "CONV")
+        lines.append("ENRG" if self._energytype == self.EnergyTypes["ENERGY"] else "TGIV")
+        mix = self.reactormixture
+        lines += [f"PRES    {mix.pressure / P_ATM!r}", f"TEMP    {mix.temperature!r}", f"TIME    {self._endtime!r}"]
+        X = mix.X
+        lines += [f"REAC    {sp}    {float(X[k])!r}" for k, sp in enumerate(self._specieslist) if X[k] > 1.0e-12]
+        for p in self._profiles_list:
+            scale = 1.0 / P_ATM if p.profilekey == "PPRO" else 1.0
+            lines += [f"{p.profilekey}    {float(x)!r}    {float(y) * scale!r}" for x, y in zip(p.x, p.y)]
+        if self._energytype == self.EnergyTypes["ENERGY"]:
+            lines.append("QRGEQ")
+        lines.append("END")
+        return lines
+
+    def _run_full_keywords(self) -> int:
+        """Full-keyword mode (usefullkeywords(True)): the keyword block goes through the KIN ABI's
+        full-keyword input parser, KINAll0D_CalculateInput (include/ckmi_kin.h; the reference's
+        __run_model_withFullInputs, batchreactor.py:944-978), on the same device kernels."""
+        import ctypes as ct
+
+        from . import kin
+
+        if self.validate_inputs() != 0:
+            raise ReactorError("missing required input keywords")
+        L = kin.bind()
+        mix = self.reactormixture
+        cs = ct.c_int(kin.register(self._chem.mechanism()))
+        try:
+            zero = np.zeros(1, np.int32)
+            rc = L.KINAll0D_Setup(ct.byref(cs), ct.byref(ct.c_int(self._reactortype)), ct.byref(ct.c_int(self._problemtype)),
+                                  ct.byref(ct.c_int(self._energytype)), ct.byref(ct.c_int(self._solvertype)),
+                                  ct.byref(ct.c_int(1)), zero, ct.byref(ct.c_int(0)))
+            rc = rc or L.KINAll0D_SetupWorkArrays(ct.byref(ct.c_int(154)), ct.byref(cs))
+            z = np.zeros(1)
+            V0 = self._volume if self._volume > 0.0 else 1.0
+            rc = rc or L.KINAll0D_SetupBatchInputs(
+                ct.byref(cs), ct.byref(ct.c_double(self._endtime)), ct.byref(ct.c_double(mix.temperature)),
+                ct.byref(ct.c_double(mix.pressure)), ct.byref(ct.c_double(V0)), ct.byref(ct.c_double(self._heat_loss_rate)),
+                ct.byref(ct.c_double(self._reactivearea)), np.ascontiguousarray(mix.Y), z, z)
+            if rc:
+                raise ReactorError(f"full-keyword setup failed: {kin.last_error()}")
+            lines = self.full_keyword_lines()
+            blob = "".join(lines).encode()
+            lens = np.array([len(x) for x in lines], np.int32)
+            status = L.KINAll0D_CalculateInput(ct.byref(ct.c_int(154)), ct.byref(cs), blob, ct.byref(ct.c_int(len(lines))),
+                                               lens)
+            if status != 0:
+                logger.critical("reactor %s failed in full-keyword mode: %s", self.label, kin.last_error())
+                self.setrunstatus(status)
+                return status
+            tau = ct.c_double(0.0)
+            L.KINAll0D_GetIgnitionDelay(ct.byref(tau))
+            nr, npt = ct.c_int(0), ct.c_int(0)
+            L.KINAll0D_GetSolnResponseSize(ct.byref(nr), ct.byref(npt))
+            n, KK = npt.value, self.numbspecies
+            t, T, P, V = (np.zeros(n) for _ in range(4))
+            Y = np.zeros((KK, n), order="F")
+            L.KINAll0D_GetGasSolnResponse(ct.byref(nr), ct.byref(npt), ct.byref(ct.c_int(KK)), t, T, P, V, Y)
+        finally:
+            kin.release(cs.value)
+        self._tau = tau.value
+        self._stats = None
+        self._final = dict(T=float(T[-1]), P=float(P[-1]), V=float(V[-1]), Y=Y[:, -1].copy())
+        self._raw = (t, np.column_stack([T, Y.T]))
+        self._solution_rawarray = {}
+        self._solution_mixturearray = []
+        self._numbsolutionpoints = 0
+        self.setrunstatus(0)
+        return 0
+
     def run(self) -> int:
         """Integrate the reactor on the GPU; returns 0 on success (batchreactor.py:1161-1261)."""
+        if not Keyword.noFullKeyword:
+            return self._run_full_keywords()
         cfg = self.reactor_cfg()
         mix = self.reactormixture
         if mix.validate() != 0:
@@ -423,7 +507,8 @@ class BatchReactors(ReactorModel):
         return P, V
 
     def process_solution(self) -> None:
-        """Raw solution arrays and solution mixtures (batchreactor.py:1335-1435)."""
+        """Raw solution arrays and solution mixtures (batchreactor.py:1335-1435).  The species profiles
+        are mass fractions, or mole fractions X_k = Y_k Wbar / W_k after setsolutionspeciesfracmode("mole")."""
         if self.runstatus != 0:
             raise ReactorError("please run the reactor successfully first")
         ts, ys = self._raw
@@ -432,16 +517,39 @@ class BatchReactors(ReactorModel):
         P, V = self._PV_of(ts, T, Y)
         self._numbsolutionpoints = len(ts)
         self._solution_rawarray = {"time": ts.copy(), "temperature": T.copy(), "pressure": P, "volume": V}
+        frac = Y
+        if self._speciesmode == "mole":
+            n = Y / self.reactormixture.WT
+            frac = n / n.sum(axis=1, keepdims=True)
         for k, sp in enumerate(self._specieslist):
-            self._solution_rawarray[sp] = Y[:, k].copy()
+            self._solution_rawarray[sp] = frac[:, k].copy()
         self._solution_mixturearray = []
-        for i in range(len(ts)):
+        self.create_solution_mixtures(np.asfortranarray(frac.T))
+
+    def create_solution_mixtures(self, specfrac: np.ndarray) -> int:
+        """One Mixture per solution point from the processed profiles and specfrac[KK][npts], species
+        fractions of the current mode (reference batchreactor.py:1487-1548); 0 on success."""
+        if not self.getrawsolutionstatus():
+            logger.info("please use 'process_solution' to post-process the raw solution data first.")
+            return 1
+        specfrac = np.asarray(specfrac, np.float64)
+        if specfrac.shape != (self.numbspecies, self._numbsolutionpoints):
+            raise ReactorError(f"species fractions must be [{self.numbspecies}][{self._numbsolutionpoints}]")
+        P = self.get_solution_variable_profile("pressure")
+        T = self.get_solution_variable_profile("temperature")
+        V = self.get_solution_variable_profile("volume")
+        self._solution_mixturearray = []
+        for i in range(self._numbsolutionpoints):
             m = Mixture(self._chem)
             m.temperature = T[i]
             m.pressure = P[i]
             m.volume = V[i]
-            m.Y = np.maximum(Y[i], 0.0)
+            if self._speciesmode == "mass":
+                m.Y = np.maximum(specfrac[:, i], 0.0)
+            else:
+                m.X = np.maximum(specfrac[:, i], 0.0)
             self._solution_mixturearray.append(m)
+        return 0
 
     def get_solution_variable_profile(self, varname: str) -> np.ndarray:
         if not self._solution_rawarray:

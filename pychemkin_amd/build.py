@@ -97,9 +97,11 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
         jobs.append((TRAN_SRC, tran_obj, LU_FLAGS))
     # a variant that only names the workgroup kernel shares the default build's ckmi.hip object
     main_extra = [f for f in extra if "CKMI_BIG" not in f]
-    tag = "main" if (default or (extra and not main_extra)) else os.path.splitext(os.path.basename(out))[0]
+    # (a phase-timer build never shares the production object, and vice versa)
+    tag = "prof" if prof else ("main" if (default or not main_extra)
+                               else os.path.splitext(os.path.basename(out))[0])
     main_obj = os.path.join(OBJ_DIR, f"ckmi_{tag}.o")
-    if force or (tag != "main" and not prof) or _stale(main_obj, [SRC] + DEPS):
+    if force or (tag not in ("main", "prof")) or (prof and main_extra) or _stale(main_obj, [SRC] + DEPS):
         jobs.append((SRC, main_obj, FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + list(main_extra)))
     with ThreadPoolExecutor(max_workers=max(1, min(len(jobs), os.cpu_count() or 1))) as pool:
         for f in [pool.submit(_compile, s, o, fl, verbose) for s, o, fl in jobs]:

@@ -211,6 +211,16 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           if (lane == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + lane - 1];
           const double Wbar0 = 1.0 / wave_sum(isp ? yl * V.rwt()[lane - 1] : 0.0);
+          if (dcfg->npe) {  // initial element contents: the element projection's target
+            const uint64_t cnt = isp ? elem_table(V)[lane - 1] : 0ull;
+            const double rw = isp ? V.rwt()[lane - 1] : 0.0;
+            double v[PROJ_MMAX];
+#pragma unroll
+            for (int e = 0; e < PROJ_MMAX; ++e) v[e] = elem_coef(cnt, rw, e) * yl;
+            wave_sum_multi<PROJ_MMAX>(v, lane);
+#pragma unroll
+            for (int e = 0; e < PROJ_MMAX; ++e) c.eb0[e] = v[e];
+          }
           R.pfr = PF ? (prob == 3 ? 1 : (prob == 4 ? 2 : 0)) : 0;
           R.conp = (prob == 1 || prob == 3);
           R.energy = cfg->energy;
@@ -518,26 +528,35 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
           S.nni++;
           if (S.gamrat != 1.0) x *= 2.0 / (1.0 + S.gamrat);
           if (!act) x = 0.0;
-          const double del = wrms_lane(x, b.ewt, n);
+          // the iteration's norms in one fused reduction (oracle nls: the same quantities): the correction
+          // (del), the accumulated correction (acnrm), NNEG's negative part and acnrm after NNEG's clipping
+          const double z0 = b.zn[0];
           b.acor += x;
-          b.y = b.zn[0] + b.acor;
+          b.y = z0 + b.acor;
+          const bool neg = S.nneg && act && lane >= 1 && b.y < 0.0;
+          double nv[4];
+          {
+            const double xe = x * b.ewt, ae = b.acor * b.ewt, ne = neg ? b.y * b.ewt : 0.0;
+            const double fe2 = neg ? z0 * b.ewt : ae;
+            nv[0] = xe * xe;
+            nv[1] = ae * ae;
+            nv[2] = ne * ne;
+            nv[3] = fe2 * fe2;
+          }
+          wave_sum_multi<4>(nv, lane);
+          const double del = sqrt(nv[0] / n);
           if (c.mm > 0) S.crate = fmax(CRDOWN * S.crate, del / c.delp);
           const double dcon = del * fmin(1.0, S.crate) / S.tq[4];
           if (dcon <= 1.0) {
             bool negfail = false, negfix = false;
-            if (S.nneg) {
-              const bool neg = act && lane >= 1 && b.y < 0.0;
-              const double xn = neg ? b.y * b.ewt : 0.0;
-              const double ss = wave_sum(xn * xn);
-              if (ss > 0.0) {
-                if (sqrt(ss / n) > NNEG_TOL) {
-                  negfail = true;
-                } else {
-                  negfix = true;
-                  if (neg) {
-                    b.y = 0.0;
-                    b.acor = -b.zn[0];
-                  }
+            if (S.nneg && nv[2] > 0.0) {
+              if (sqrt(nv[2] / n) > NNEG_TOL) {
+                negfail = true;
+              } else {
+                negfix = true;
+                if (neg) {
+                  b.y = 0.0;
+                  b.acor = -z0;
                 }
               }
             }
@@ -546,7 +565,7 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
               st = ST_NLS_FAIL;
               break;
             }
-            S.acnrm = (c.mm == 0 && !negfix) ? del : wrms_lane(b.acor, b.ewt, n);
+            S.acnrm = (c.mm == 0 && !negfix) ? del : sqrt((negfix ? nv[3] : nv[1]) / n);
             S.jcur = 0;
             st = ST_ERRTEST;
             break;
@@ -649,6 +668,38 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             if (i <= S.q) S.tau[i] = S.tau[i - 1];
           if (S.q == 1 && S.nst > 1) S.tau[2] = S.tau[1];
           S.tau[1] = S.h;
+          // the q - 1 and q + 1 error norms of a step that selects the next order (qwait reaches 0 below), from
+          // the corrector before the element projection (oracle bdf_step), in one fused 2-value reduction
+          double ddn = 0.0, dup = 0.0;
+          if (S.etamax != 1.0 && S.qwait == 1) {
+            const bool qm = S.q > 1, qp = S.q != QMAX && S.saved_tq5 != 0.0;
+            double cquot = 0.0;
+            if (qp) {
+              const double hr = S.h / S.tau[2];
+              double hrL = hr;
+              for (int j = 1; j < S.L; ++j) hrL *= hr;
+              cquot = (S.tq[5] / S.saved_tq5) * hrL;
+            }
+            double ov[2];
+            {
+              double znq = 0.0, lq = 0.0;
+#pragma unroll
+              for (int j = 0; j <= QMAX; ++j)
+                if (j == S.q) {
+                  znq = b.zn[j];
+                  lq = S.l[j];
+                }
+              const double a = (act && qm) ? (znq + lq * b.acor) * b.ewt : 0.0;
+              const double t = (act && qp) ? (b.acor - cquot * b.zn[QMAX]) * b.ewt : 0.0;
+              ov[0] = a * a;
+              ov[1] = t * t;
+            }
+            wave_sum_multi<2>(ov, lane);
+            ddn = sqrt(ov[0] / n) * S.tq[1];
+            dup = sqrt(ov[1] / n) * S.tq[3];
+          }
+          // element conservation held to PROJ_TOL rtol (oracle elem_project), before the history update
+          if (dcfg->npe) elem_project_wave(V, dcfg->npe, c.eb0, S.rtol, b.zn[0], b.acor, lane, L.ek());
 #pragma unroll
           for (int j = 0; j <= QMAX; ++j)
             if (j <= S.q) b.zn[j] += S.l[j] * b.acor;
@@ -670,23 +721,8 @@ __global__ __launch_bounds__(rwaves(F64)* WAVE) void reactor_kernel(MechImage im
             } else {
               S.qwait = 2;
               double etaqm1 = 0.0, etaqp1 = 0.0;
-              if (S.q > 1) {
-                double znq = 0.0;
-#pragma unroll
-                for (int j = 0; j <= QMAX; ++j)
-                  if (j == S.q) znq = b.zn[j];
-                const double ddn = wrms_lane(act ? znq : 0.0, b.ewt, n) * S.tq[1];
-                etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, S.q) + ADDON);
-              }
-              if (S.q != QMAX && S.saved_tq5 != 0.0) {
-                const double hr = S.h / S.tau[2];
-                double hrL = hr;
-                for (int j = 1; j < S.L; ++j) hrL *= hr;
-                const double cquot = (S.tq[5] / S.saved_tq5) * hrL;
-                const double tv = act ? b.acor - cquot * b.zn[QMAX] : 0.0;
-                const double dup = wrms_lane(tv, b.ewt, n) * S.tq[3];
-                etaqp1 = 1.0 / (eta_root(BIAS3 * dup, S.L + 1) + ADDON);
-              }
+              if (S.q > 1) etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, S.q) + ADDON);
+              if (S.q != QMAX && S.saved_tq5 != 0.0) etaqp1 = 1.0 / (eta_root(BIAS3 * dup, S.L + 1) + ADDON);
               const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
               if (etam < THRESH) {
                 S.eta = 1.0;
@@ -1471,14 +1507,11 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
   I.o_gsp = gsp.empty() ? put(&zero, 4) : put(gsp.data(), gsp.size() * 4);
   I.o_geff = geff.empty() ? put(&dzero, 8) : put(geff.data(), geff.size() * 8);
   // transposed dense efficiency table geffT[k][17] (64 species rows, stride 17: conflict-free) for
-  // the wave kernel (CKMI_MG_SPARSE restores the sparse loop); only for KK <= 63 and G <= 16, else a stub
-#ifndef CKMI_MG_SPARSE
-  // ... and only while the 64-wide launch (12 waves) still fits the 160 KB of LDS with it
-  const size_t lds_with = blob.size() + 64 * 17 * 8 + 16 * E2T_N + jscratch_bytes<64>() + 12 * (size_t)slice_bytes(G);
+  // the wave kernel (a per-lane walk of the sparse lists measured 0.6 % slower); only for KK <= 63 and
+  // G <= 16, and only while the 64-wide launch (12 waves) still fits the 160 KB of LDS with it, else a stub
+  const size_t lds_with = blob.size() + 64 * 17 * 8 + 8 * E2T_N + 8 * (size_t)KKp + jscratch_bytes<64>() +
+                          12 * (size_t)slice_bytes(G);
   const bool dense = KK <= SP_ONE && G <= 16 && lds_with <= 160 * 1024;
-#else
-  const bool dense = false;
-#endif
   std::vector<double> geffd(dense ? (size_t)64 * 17 : (size_t)2, 0.0);
   for (int g = 0; dense && g < G; ++g)
     for (int e = gptr[g]; e < gptr[g + 1]; ++e) geffd[(size_t)gsp[e] * 17 + g] = geff[e];
@@ -1487,6 +1520,30 @@ int build_image(ckmi_mech* m, const ckmi_mech_desc* d, const std::vector<int>& s
     double e2t[E2T_N];  // 2^(j / E2T_N): E2T_N doubles fill the 64 LDS banks once (conflict-free gathers)
     for (int j = 0; j < E2T_N; ++j) e2t[j] = (double)std::exp2((long double)j / (long double)E2T_N);
     I.o_e2t = put(e2t, sizeof(e2t));
+  }
+  {
+    // element counts of each species for the corrector's element projection, right after e2t (the kernels
+    // address it as o_e2t + 8 E2T_N: no extra view field): u64 per species, byte e = the count of the
+    // e-th element that occurs in the mechanism (m->npe of them, <= CKMI_PROJ_MMAX; none otherwise)
+    std::vector<uint64_t> el(KKp, 0ull);
+    m->npe = 0;
+    if (d->ncf && d->MM > 0) {
+      std::vector<int> used;
+      for (int e = 0; e < d->MM; ++e)
+        for (int k = 0; k < KK; ++k)
+          if (d->ncf[(size_t)e * KK + k] > 0) {
+            used.push_back(e);
+            break;
+          }
+      if ((int)used.size() <= CKMI_PROJ_MMAX) {
+        m->npe = (int)used.size();
+        for (int j = 0; j < m->npe; ++j)
+          for (int k = 0; k < KK; ++k)
+            el[k] |= (uint64_t)std::min(255, std::max(0, (int)d->ncf[(size_t)used[j] * KK + k])) << (8 * j);
+      }
+    }
+    const int o_el = put(el.data(), el.size() * 8);
+    if (o_el != I.o_e2t + 8 * E2T_N) return fail(CKMI_ERR_ARG, "image layout: element table not after e2t");
   }
   I.bytes = (int)blob.size();
   {
@@ -2147,6 +2204,7 @@ int ckmi_reactor_run_ex(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, int32_t
     dc.guard_y = std::max(1e-3, 1e3 * cfg->atol);
     dc.guard_tlo = m->tguard_lo;
     dc.guard_thi = m->tguard_hi;
+    dc.npe = cfg->no_elem_proj ? 0 : m->npe;
   }
   ReactorIO io{problem, T0, P0, V0, Y0, tau, Tend, Pend, Vend, Yend, stats, nsave, t_save, y_save,
                ext ? ext->afac_rxn : nullptr, ext ? ext->afac : nullptr, ext ? ext->max_adap : 0,
@@ -2216,6 +2274,7 @@ int ckmi_engine_heat_rates(const ckmi_mech* m, const ckmi_reactor_cfg* cfg, doub
   dc.guard_y = std::max(1e-3, 1e3 * cfg->atol);
   dc.guard_tlo = m->tguard_lo;
   dc.guard_thi = m->tguard_hi;
+  dc.npe = 0;  // (no integration)
   const hipStream_t st = (hipStream_t)stream;
   const size_t lds = (size_t)align16(m->img.bytes) + slice_vec_bytes(m->G) + align16((int)sizeof(RunCtx));
   const void* fn = m->has_plog ? (const void*)engine_heat_kernel<true> : (const void*)engine_heat_kernel<false>;

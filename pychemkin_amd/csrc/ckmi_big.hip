@@ -46,7 +46,7 @@ namespace {
 constexpr int BW = 4;           // waves per workgroup
 constexpr int NT = BW * WAVE;   // threads: state component / matrix row per thread
 constexpr int BIG_NMAX = 192;   // n = KK + 1 <= 192
-constexpr int RED_SET = 16;     // doubles per reduction set (two sets alternate)
+constexpr int RED_SET = 72;     // doubles per reduction set (two sets alternate): [BW][16] + [BW] for bsumn_max<16>
 constexpr int NDQ = 16;         // dq/dC slots per reaction: unit reactions 4 + 4, general ones GEN_SLOTS + GEN_SLOTS
 
 // Diagnostic build only (-DCKMI_PHASE_TIMERS, scripts/phase_profile.py --big): per-reactor shader
@@ -156,9 +156,95 @@ __device__ __forceinline__ double bmax(Blk& B, double v, int wid, int lane) {
   B.phase ^= 1;
   return s;
 }
+// NV (<= 8) sums over the workgroup in one barrier: each wave's multi-value reduction (wave_sum_multi's
+// stages), the lanes holding a value publish it, every thread adds the four wave partials in a fixed order
+template <int NV>
+__device__ __forceinline__ void bsumn(Blk& B, double (&v)[NV], int wid, int lane) {
+  static_assert(NV * BW <= RED_SET, "reduction set too small");
+  wave_sum_stages<0, NV>(v, lane);
+  double* r = B.set();
+  if ((lane & (64 / NV - 1)) == 0) r[wid * NV + wave_sum_index<NV>(lane)] = v[0];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = (r[j] + r[NV + j]) + (r[2 * NV + j] + r[3 * NV + j]);
+  B.phase ^= 1;
+}
+__device__ __forceinline__ void bsum8(Blk& B, double (&v)[8], int wid, int lane) { bsumn<8>(B, v, wid, lane); }
+// bsumn and the workgroup maximum of mx, in the same barrier
+template <int NV>
+__device__ __forceinline__ void bsumn_max(Blk& B, double (&v)[NV], double& mx, int wid, int lane) {
+  static_assert(NV * BW + BW <= RED_SET, "reduction set too small");
+  wave_sum_stages<0, NV>(v, lane);
+  const double wm = wave_max(mx);
+  double* r = B.set();
+  if ((lane & (64 / NV - 1)) == 0) r[wid * NV + wave_sum_index<NV>(lane)] = v[0];
+  if (lane == 0) r[BW * NV + wid] = wm;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = (r[j] + r[NV + j]) + (r[2 * NV + j] + r[3 * NV + j]);
+  mx = fmax(fmax(r[BW * NV], r[BW * NV + 1]), fmax(r[BW * NV + 2], r[BW * NV + 3]));
+  B.phase ^= 1;
+}
 __device__ __forceinline__ double bwrms(Blk& B, double v, double ewt, int n, int wid, int lane) {
   const double x = v * ewt;
   return sqrt(bsum(B, x * x, wid, lane) / n);
+}
+
+// ------------------------------------------------------------------ element projection
+// The workgroup form of elem_project_wave (ckmi_reactor.hpp; oracle elem_project): thread = component.  The
+// element sums r[e] = sum_k C_ek y_k come from the step's fused reduction (ST_STEP_COMPLETE); past the
+// threshold (rare) the Gram matrix by bsum8 batches and the solve by thread 0 in the scratch scr, read back
+// after a barrier.  Every wave takes the same decision from the same sums.
+__device__ __forceinline__ void elem_project_big(const MechView& V, Blk& B, int npe, const double (&r)[PROJ_MMAX],
+                                                 const double* eb0, double rtol, double y, double& acor, int tid,
+                                                 int wid, int lane, double* scr) {
+  double v[PROJ_MMAX];
+  double rmax = 0.0, bmax = 0.0;
+#pragma unroll
+  for (int e = 0; e < PROJ_MMAX; ++e) {
+    v[e] = 0.0;
+    if (e < npe) {
+      v[e] = r[e] - eb0[e];
+      rmax = fmax(rmax, fabs(v[e]));
+      bmax = fmax(bmax, eb0[e]);
+    }
+  }
+  if (!(rmax > PROJ_TOL * rtol * bmax)) return;
+  const bool isp = tid >= 1 && tid <= V.KK;
+  const int s = isp ? tid - 1 : 0;
+  const uint64_t cnt = isp ? elem_table(V)[s] : 0ull;
+  const double rw = isp ? V.rwt()[s] : 0.0;
+  const double w = (isp && y > 0.0) ? y * V.wt()[s] : 0.0;  // moles: relative changes of the drift's size
+  const int npair = npe * (npe + 1) / 2;
+#pragma unroll 1
+  for (int p0 = 0; p0 < npair; p0 += 8) {
+    double g[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      int m, l;
+      proj_pair(p0 + i, m, l);
+      g[i] = p0 + i < npair ? elem_coef(cnt, rw, m) * elem_coef(cnt, rw, l) * w : 0.0;
+    }
+    bsum8(B, g, wid, lane);
+    if (tid == 0) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        if (p0 + i < npair) scr[p0 + i] = g[i];
+    }
+  }
+  if (tid == 0) {
+#pragma unroll
+    for (int e = 0; e < PROJ_MMAX; ++e)
+      if (e < npe) scr[PROJ_SCR_RES + e] = v[e];
+    proj_solve_lds(scr, npe);
+  }
+  __syncthreads();
+  double sc = 0.0;
+#pragma unroll
+  for (int e = 0; e < PROJ_MMAX; ++e)
+    if (e < npe) sc += elem_coef(cnt, rw, e) * scr[PROJ_SCR_LAM + e];
+  acor -= w * sc;
+  __syncthreads();  // scr is free again (the next projection's thread 0 may not overwrite it earlier)
 }
 
 // ------------------------------------------------------------------ Newton matrix in registers
@@ -513,11 +599,7 @@ struct PanHdr {
   int pad[3];
 };
 
-// LA: the look-ahead factorisation (else the barrier form), an A/B form built with CKMI_BIG_LOOKAHEAD for the
-// NB = 11 kernel without pressure-dependent rates only: in the PLOG kernels and at NB = 9 it crashes the ROCm
-// 7.2 backend (AMDGPU Rewrite AGPR-Copy-MFMA, eliminateSpillsOfReassignedVGPRs), and it quadruples the
-// compile time of this file.  Measured: bitwise the same results, no faster.
-template <int NB, bool LA = true>
+template <int NB>
 struct BigMatrixM {
   static constexpr int NC = 16 * NB;
   static constexpr int NG = (NB + 3) / 4;    // accumulator groups of 4 register tiles
@@ -557,10 +639,9 @@ struct BigMatrixM {
 
   static constexpr int NJ = (NC + 63) / 64;  // rows per lane in the transposed panel
 
-  // xpart during a factorisation: panel buffers [3][4 s][NC], per-wave pivot rows [BW][4 s][4 q][NB c],
-  // per-wave diagonal-block rows [BW][16 ti][4 q][NB c]; after the 3 panel headers in phdr, the look-ahead's
-  // sync words: [0] panels published, [4 + w] last panel wave w has finished with
-  static constexpr int NPB = 3;
+  // xpart during a factorisation: panel buffers [2][4 s][NC] (alternating by panel parity), per-wave pivot
+  // rows [BW][4 s][4 q][NB c], per-wave diagonal-block rows [BW][16 ti][4 q][NB c]
+  static constexpr int NPB = 2;
   __device__ __forceinline__ static double* pan_buf(const BigLds& L, int i) {
     return lds_at<double>(L.xpart) + i * 4 * NC;
   }
@@ -569,13 +650,6 @@ struct BigMatrixM {
   }
   __device__ __forceinline__ static double* blk_buf(const BigLds& L, int wid) {
     return lds_at<double>(L.xpart) + NPB * 4 * NC + BW * 16 * NB + wid * 64 * NB;
-  }
-  // write-only scratch: the look-ahead's column staging of the waves that do not own the next panel
-  __device__ __forceinline__ static double* junk_buf(const BigLds& L) {
-    return lds_at<double>(L.xpart) + NPB * 4 * NC + BW * 16 * NB + BW * 64 * NB;
-  }
-  __device__ __forceinline__ static int* sync_words(const BigLds& L) {
-    return lds_at<int>(L.phdr + NPB * (int)sizeof(PanHdr));
   }
 
   // row r of the matrix has been a pivot row: bit (r & 63) of dm[r >> 6] (wave-uniform masks)
@@ -598,30 +672,15 @@ struct BigMatrixM {
       // the pivot row's entries of the 4 panel columns (wave-uniform, from lane pl)
       double pv[4];
       int p;
-#ifndef CKMI_BIG_PIVOT_MAX
       // Natural pivot first: the diagonal row k0 + s is the pivot whenever it is still free and no
       // free row's key exceeds its key (keys are unique: the row is in the low word).  That check is
       // one readlane of the row and a ballot of 3 compares per lane; the whole-wave u64 max (6
       // dependent DPP / row-swap stages) runs only when it fails.  Same pivot, same arithmetic.
       {
         const int pn = k0 + s, pnl = pn & 63;  // wave-uniform; pn >> 6 == JN
-#ifdef CKMI_BIG_PIVOT_SELECT
-        const int pnj = pn >> 6;
-        uint64_t dmn = dm[0];
-#pragma unroll
-        for (int j = 1; j < NJ; ++j) dmn = pnj == j ? dm[j] : dmn;
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) {
-          double v = y[0][s2];
-#pragma unroll
-          for (int j = 1; j < NJ; ++j) v = pnj == j ? y[j][s2] : v;
-          pv[s2] = bcast(v, pnl);
-        }
-#else
         const uint64_t dmn = dm[JN];
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) pv[s2] = bcast(y[JN][s2], pnl);
-#endif
         const uint64_t kn = ((uint64_t)__float_as_uint((float)fabs(pv[s])) << 32) | (0xffffffffu - (uint32_t)pn);
         bool above = false;
 #pragma unroll
@@ -634,9 +693,7 @@ struct BigMatrixM {
         if (((dmn >> pnl) & 1ull) || __builtin_amdgcn_ballot_w64(above) != 0ull) p = -1;
         else if ((uint32_t)(kn >> 32) == 0u) ok = false;
       }
-      if (p < 0)
-#endif
-      {
+      if (p < 0) {
         uint64_t key = 0;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
@@ -672,10 +729,8 @@ struct BigMatrixM {
     }
   }
 
-  // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo.  SKIP (timing
-  // experiments with CKMI_BIG_FACTOR_TWICE_SKIP, on a discarded factorisation only): 1 no MFMA update, 2 no
-  // pivot steps, 4 no pivot-row gather stores, 8 no workgroup barrier
-  template <int C, int SKIP = 0>
+  // panel of steps k0 .. k0 + 3 (k0 = 16 C + 4 wo): columns in register tile C of wave wo
+  template <int C>
   __device__ __forceinline__ void panel(const BigLds& L, int wo, int par, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                         int lane
 #ifdef CKMI_PHASE_TIMERS
@@ -694,7 +749,6 @@ struct BigMatrixM {
     double* Pb = pan_buf(L, par);   // [4 s][NC] P of the panel
     double* Rb = row_buf(L, wid);   // [4 s][4 q][NB c] pivot rows, per wave
     PanHdr* hdr = lds_at<PanHdr>(L.phdr) + par;
-#ifndef CKMI_BIG_PANEL_COLS
     if (wid == wo) {
       // the panel's columns into Pb ([s][NC], as published below) and back, row-per-lane
 #pragma unroll
@@ -719,12 +773,7 @@ struct BigMatrixM {
 #endif
       PPH(2);
       int ps[4];
-      if constexpr ((SKIP & 2) != 0) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) ps[s] = k0 + s;
-      } else {
-        pivot_steps<(16 * C) / 64>(y, rid, k0, dm, ok, lane, ps);
-      }
+      pivot_steps<(16 * C) / 64>(y, rid, k0, dm, ok, lane, ps);
       // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -742,84 +791,8 @@ struct BigMatrixM {
       }
       if (lane == 0) hdr->ok = ok ? 1 : 0;
     }
-#else  // A/B reference: the round-4 per-column pivot steps in the MFMA layout
-    if (wid == wo) {
-      uint32_t pivmask = 0u;  // bit r: row ti + 16 r has been a pivot row
-#pragma unroll
-      for (int r = 0; r < NB; ++r) {
-        const int row = ti + 16 * r;
-        uint64_t m = dm[0];
-#pragma unroll
-        for (int j = 1; j < NJ; ++j) m = (row >> 6) == j ? dm[j] : m;
-        if ((m >> (row & 63)) & 1ull) pivmask |= 1u << r;
-      }
-      double x[NB];
-#pragma unroll
-      for (int r = 0; r < NB; ++r) x[r] = a[r][G][E];
-      int ps[4];
-      // column / pivot-row exchange through LDS (one wave-local sync per step instead of ~26
-      // dependent ds_bpermute round trips): xc[r][ti] = column k0 + s, pvb[q] = pivot row
-      double* xc = lds_at<double>(L.gcol);
-      double* pvb = xc + 16 * NB;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        if (q == s) {
-#pragma unroll
-          for (int r = 0; r < NB; ++r) xc[r * 16 + ti] = x[r];
-        }
-        uint64_t key = 0;
-        if (q == s) {
-#pragma unroll
-          for (int r = 0; r < NB; ++r) {
-            const uint64_t kr =
-                ((uint64_t)__float_as_uint((float)fabs(x[r])) << 32) | (uint32_t)(0xffffffffu - (ti + 16 * r));
-            if (!((pivmask >> r) & 1u) && kr > key) key = kr;
-          }
-        }
-        key = row16_max_u64(key);
-        const uint32_t klo = __builtin_amdgcn_readlane((uint32_t)key, 16 * s);
-        const uint32_t khi = __builtin_amdgcn_readlane((uint32_t)(key >> 32), 16 * s);
-        if (khi == 0u) ok = false;
-        const int p = (int)(0xffffffffu - klo);
-        ps[s] = p;
-        const int tip = p & 15, rp = p >> 4;
-        const bool prow = ti == tip;
-        if (prow) {
-          double vr = x[0];
-#pragma unroll
-          for (int r = 1; r < NB; ++r) vr = r == rp ? x[r] : vr;  // the pivot row's entry of this column
-          pvb[q] = vr;
-        }
-        wave_lds_sync();
-        const double pvq = pvb[q];  // pivot row, this lane's column
-        const double piv = pvb[s];
-        double xs[NB];
-#pragma unroll
-        for (int r = 0; r < NB; ++r) xs[r] = xc[r * 16 + ti];  // column k0 + s, this lane's rows
-        const double rcp = rcp_nr(piv);
-#pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          const double g = (prow && r == rp) ? (piv - 1.0) * rcp : xs[r] * rcp;
-          x[r] = q == s ? ((prow && r == rp) ? rcp : -g) : fma(-g, pvq, x[r]);
-        }
-        wave_lds_sync();  // the next step rewrites xc / pvb
-        if (prow) pivmask |= 1u << rp;
-      }
-      // the processed panel columns P (P' = P - e_p is formed when the B operand is read)
-#pragma unroll
-      for (int r = 0; r < NB; ++r) Pb[q * NC + ti + 16 * r] = x[r];
-      if (lane < 4) {
-        const int pl = lane == 0 ? ps[0] : (lane == 1 ? ps[1] : (lane == 2 ? ps[2] : ps[3]));
-        lds_at<int>(L.perm)[k0 + lane] = pl;
-        lds_at<int>(L.rank)[pl] = k0 + lane;
-        hdr->p[lane] = pl;
-      }
-      if (lane == 0) hdr->ok = ok ? 1 : 0;
-    }
-#endif
     PPH(0);
-    if constexpr ((SKIP & 8) == 0) __syncthreads();  // the panel's P' and pivots are published
-    else wave_lds_sync();
+    __syncthreads();  // the panel's P' and pivots are published
     PPH(1);
     int pr[4];
 #pragma unroll
@@ -837,25 +810,19 @@ struct BigMatrixM {
     // that block (11 full-wave stores instead of 44 with 4 lanes each and 4 branches), and the A operand
     // reads the pivot rows out of it.
     double* Bk = blk_buf(L, wid);  // [16 ti][4 q][NB c]
-#ifndef CKMI_BIG_B_LATE
     // The B operands (P rows of this lane's step) are loaded here, before the gather: in the MFMA loop
     // each load had been followed by a wait for it (6 LDS round trips on the critical path).  The gather's
     // asm stores (memory clobbers) keep the compiler from sinking them.
     double Bl[NB];
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) Bl[rb] = Pb[(lane >> 4) * NC + 16 * rb + (lane & 15)];
-#endif
     bool allc = true;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       mark_done(dm, pr[s]);
       allc = allc && (pr[s] >> 4) == C;
     }
-#ifdef CKMI_BIG_GATHER_ROWS
-    allc = false;  // A/B: the per-row gather only
-#endif
     const uint32_t rbq = (uint32_t)(uintptr_t)(Rb + q * NB);
-    if constexpr ((SKIP & 4) == 0) {
     if (allc) {
       const uint32_t bkq = (uint32_t)(uintptr_t)(Bk + (ti * 4 + q) * NB);
 #pragma unroll
@@ -863,31 +830,30 @@ struct BigMatrixM {
         asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(bkq), "v"(a[C][c >> 2][c & 3]), "i"(8 * c) : "memory");
     } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int tip = pr[s] & 15, rp = pr[s] >> 4;
-      if (rp == C) {
-        if (ti == tip) {
+      for (int s = 0; s < 4; ++s) {
+        const int tip = pr[s] & 15, rp = pr[s] >> 4;
+        if (rp == C) {
+          if (ti == tip) {
 #pragma unroll
-          for (int c = 0; c < NB; ++c)
-            asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[C][c >> 2][c & 3]),
-                         "i"(8 * (s * 4 * NB + c)) : "memory");
-        }
-      } else {
+            for (int c = 0; c < NB; ++c)
+              asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[C][c >> 2][c & 3]),
+                           "i"(8 * (s * 4 * NB + c)) : "memory");
+          }
+        } else {
 #pragma unroll
-        for (int r = 0; r < NB; ++r) {
-          if (r != C && r == rp) {  // uniform: one scalar branch selects the register row
-            if (ti == tip) {
+          for (int r = 0; r < NB; ++r) {
+            if (r != C && r == rp) {  // uniform: one scalar branch selects the register row
+              if (ti == tip) {
 #pragma unroll
-              for (int c = 0; c < NB; ++c)
-                asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[r][c >> 2][c & 3]),
-                             "i"(8 * (s * 4 * NB + c)) : "memory");
+                for (int c = 0; c < NB; ++c)
+                  asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[r][c >> 2][c & 3]),
+                               "i"(8 * (s * 4 * NB + c)) : "memory");
+              }
+              asm volatile("" ::: "memory");
             }
-            asm volatile("" ::: "memory");
           }
         }
       }
-    }
-    }
     }
     wave_lds_sync();
     PPH(3);
@@ -902,47 +868,15 @@ struct BigMatrixM {
 #pragma unroll
       for (int g = 0; g < NG; ++g) A[g] = 4 * g + (j >> 2) < NB ? ra[4 * g] : 0.0;
     }
-    // Issue order (A/B, CKMI_BIG_MFMA_GROUP_FIRST): accumulator group G (tiles 4G .. 4G + 3, among them
-    // tile C, the next panel's) for every row block first, then the other groups, so that the next
-    // panel's owner would wait for 11 MFMAs only and the other 22 would run beside its pivot steps.
-    // Measured 1.3 % slower (509 vs 503 ms on 2,048 configs[4] reactors, bitwise the same results): at the
-    // wo loop's back-edge the compiler moves ~40 accumulator registers between AGPRs and VGPRs, which
-    // waits for every MFMA anyway.  Row-block-major order stays.
-#ifdef CKMI_BIG_MFMA_GROUP_FIRST
+    // row-block-major issue order (a group-first order that would let the next panel's owner start
+    // earlier measured 1.3 % slower: DESIGN.md §5)
 #pragma unroll
     for (int rb = 0; rb < NB; ++rb) {
       const int i = 16 * rb + (lane & 15);
       const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
-      a[rb][G] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[G], Bv, a[rb][G], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);  // keep the issue order: the scheduler may not mix the two loops
-#pragma unroll
-    for (int rb = 0; rb < NB; ++rb) {
-      const int i = 16 * rb + (lane & 15);
-      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
-#pragma unroll
-      for (int g = 0; g < NG; ++g)
-        if (g != G) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
-    }
-#else  // A/B reference: row-block-major issue order
-#pragma unroll
-    for (int rbi = 0; rbi < ((SKIP & 1) ? 0 : NB); ++rbi) {
-#ifdef CKMI_BIG_MFMA_ROT
-      // row block C first: the next panel's pivot-row gather (3 of 4 panels) reads it first
-      const int rb = (rbi + C) % NB;
-#else
-      const int rb = rbi;
-#endif
-      const int i = 16 * rb + (lane & 15);
-#ifndef CKMI_BIG_B_LATE
-      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
-#else
-      const double Bv = Pb[sl * NC + i] - (i == pl ? 1.0 : 0.0);
-#endif
 #pragma unroll
       for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
     }
-#endif
 #ifdef CKMI_PHASE_TIMERS
     {  // the MFMA results have landed before the stamp
       double chk = 0.0;
@@ -975,256 +909,17 @@ struct BigMatrixM {
 #define FPH_ARG
 #define FPH_PARAM
 #endif
-  template <int C, int SKIP = 0>
+  template <int C>
   __device__ __forceinline__ void panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, int t, int wid,
                                          int lane FPH_PARAM) {
     if constexpr (C < NB) {
 #pragma unroll 1  // (fully unrolled: 4x the code, and the ROCm 7.2 backend crashes in AMDGPU Rewrite AGPR-Copy-MFMA)
       for (int wo = 0; wo < 4; ++wo)
-        if (16 * C + 4 * wo < n) panel<C, SKIP>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
-      panels<C + 1, SKIP>(L, n, dm, ok, t, wid, lane FPH_ARG);
+        if (16 * C + 4 * wo < n) panel<C>(L, wo, (C * 4 + wo) & 1, dm, ok, t, wid, lane FPH_ARG);
+      panels<C + 1>(L, n, dm, ok, t, wid, lane FPH_ARG);
     }
   }
 
-  // ---------------------------------------------------------------- look-ahead form (default)
-  // The barrier form above serialises, per panel: the owner's 4 pivot steps -> barrier -> every wave's
-  // pivot-row gather and rank-4 MFMA update -> the next owner's pivot steps (it needs its columns
-  // updated).  Here the owner of panel t + 1 updates just its 4 panel columns with panel t's transforms
-  // on the VALU, in the row-per-lane layout of the pivot steps (from the same P' and pivot rows the MFMA
-  // uses), factors panel t + 1 and publishes it before issuing its own MFMAs for panel t; the other waves
-  // run their panel-t MFMAs meanwhile.  Waves synchronise through LDS words instead of workgroup
-  // barriers (a barrier would make every wave wait for the owner's MFMAs too): "panels published" and,
-  // per wave, "last panel finished"; the panel buffers rotate over 3 so that panel t + 1 is written only
-  // once every wave is done with panel t - 2.  The pivots and the arithmetic of every transform are those
-  // of the barrier form; only the 4 look-ahead columns are updated by FMAs instead of the MFMA (measured:
-  // bitwise the same results).  A/B form (CKMI_BIG_LOOKAHEAD): it did not shorten the factorisation
-  // (200 vs 211 ms per extra factorisation of 2,048 configs[4] reactors, CKMI_BIG_FACTOR_TWICE).
-  __device__ __forceinline__ static void la_wait(const int* f, int v, bool& live) {
-    if (!live) return;
-    for (int it = 0; it < (1 << 22); ++it) {  // bounded: a broken protocol fails the factorisation, not the GPU
-      const int x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      if (x >= v) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        return;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    live = false;
-  }
-  __device__ __forceinline__ static void la_wait_all(const int* g, int v, bool& live) {
-    if (!live) return;
-    for (int it = 0; it < (1 << 22); ++it) {
-      int m = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#pragma unroll
-      for (int w = 1; w < BW; ++w) m = min(m, __hip_atomic_load(g + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      if (__builtin_amdgcn_readfirstlane(m) >= v) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        return;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    live = false;
-  }
-  __device__ __forceinline__ static void la_signal(int* f, int v, int lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's LDS writes have landed
-    if (lane == 0) __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-
-  // owner of panel tn (columns in register tile CN of this wave): the columns into the row-per-lane layout
-  // through panel buffer tn % 3; with `upd`, panel tp's transforms applied to them (P' from panel buffer
-  // tp % 3, the pivot rows' entries from this wave's gather of panel tp); the 4 pivot steps; P, perm /
-  // rank and the header published, then "panels published" = tn + 1
-  // every wave: its column group q of register tile CN into panel buffer tn % 3 if it owns panel tn, else
-  // into the write-only scratch (the accumulators are read unconditionally: reading them under a branch
-  // makes the backend spill the matrix)
-  template <int CN>
-  __device__ __forceinline__ void la_stage(const BigLds& L, int tn, bool own, int lane) const {
-    constexpr int GN = CN >> 2, EN = CN & 3;
-    const int ti = lane & 15, q = lane >> 4;
-    const uint32_t dst = (uint32_t)(uintptr_t)((own ? pan_buf(L, tn % NPB) : junk_buf(L)) + q * NC + ti);
-#pragma unroll
-    for (int r = 0; r < NB; ++r)
-      asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(dst), "v"(a[r][GN][EN]), "i"(8 * 16 * r) : "memory");
-  }
-
-  template <int CN>
-  __device__ __forceinline__ static void la_own(const BigLds& L, int tn, bool upd, int tp, const int (&pr)[4], bool allc,
-                                                uint64_t (&dm)[NJ], bool& ok, int wid, int lane) {
-    const int k0 = 4 * tn;
-    double* Pn = pan_buf(L, tn % NPB);
-    wave_lds_sync();
-    double y[NJ][4];
-    uint64_t rid[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int row = lane + 64 * j;
-      rid[j] = 0xffffffffu - (uint32_t)row;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) y[j][s] = row < NC ? Pn[s * NC + row] : 0.0;
-    }
-    if (upd) {
-      const double* Pt = pan_buf(L, tp % NPB);
-      const double* Rb = row_buf(L, wid);
-      const double* Bk = blk_buf(L, wid);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        double u[4];  // pivot row s of panel tp, columns k0 .. k0 + 3 (lane group q = s2 of tile CN)
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) u[s2] = allc ? Bk[((pr[s] & 15) * 4 + s2) * NB + CN] : Rb[(s * 4 + s2) * NB + CN];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int row = lane + 64 * j;
-          const double pv = row < NC ? Pt[s * NC + row] - (row == pr[s] ? 1.0 : 0.0) : 0.0;
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) y[j][s2] = fma(pv, u[s2], y[j][s2]);
-        }
-      }
-    }
-    int ps[4];
-    pivot_steps<(16 * CN) / 64>(y, rid, k0, dm, ok, lane, ps);
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int row = lane + 64 * j;
-      if (row < NC) {
-#pragma unroll
-        for (int s = 0; s < 4; ++s) Pn[s * NC + row] = y[j][s];
-      }
-    }
-    PanHdr* hdr = lds_at<PanHdr>(L.phdr) + tn % NPB;
-    if (lane < 4) {
-      const int pl = lane == 0 ? ps[0] : (lane == 1 ? ps[1] : (lane == 2 ? ps[2] : ps[3]));
-      lds_at<int>(L.perm)[k0 + lane] = pl;
-      lds_at<int>(L.rank)[pl] = k0 + lane;
-      hdr->p[lane] = pl;
-    }
-    if (lane == 0) hdr->ok = ok ? 1 : 0;
-    la_signal(sync_words(L), tn + 1, lane);
-  }
-
-  // panel t = 4 C + wo (columns in register tile C of wave wo), every wave
-  // LAST: wo = 3, the next panel is in register tile C + 1 (wave 0)
-  template <int C, bool LAST>
-  __device__ __forceinline__ void la_panel(const BigLds& L, int wo, int n, uint64_t (&dm)[NJ], bool& ok, bool& live,
-                                           int wid, int lane FPH_PARAM) {
-#ifdef CKMI_PHASE_TIMERS
-    unsigned long long ft = __builtin_amdgcn_s_memtime();
-#define PPH(i) do { const unsigned long long f2 = __builtin_amdgcn_s_memtime(); fph[i] += f2 - ft; ft = f2; } while (0)
-#else
-#define PPH(i) (void)0
-#endif
-    constexpr int G = C >> 2, E = C & 3;
-    const int ti = lane & 15, q = lane >> 4;
-    const int t = 4 * C + wo;
-    int* sw = sync_words(L);
-    la_wait(sw, t + 1, live);  // panel t published
-    if (!live) ok = false;
-    PPH(1);
-    const PanHdr* hdr = lds_at<const PanHdr>(L.phdr) + t % NPB;
-    const double* Pb = pan_buf(L, t % NPB);
-    double* Rb = row_buf(L, wid);
-    double* Bk = blk_buf(L, wid);
-    int pr[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) pr[s] = __builtin_amdgcn_readfirstlane(hdr->p[s]);
-    if (!__builtin_amdgcn_readfirstlane(hdr->ok)) ok = false;
-    bool allc = true;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      mark_done(dm, pr[s]);
-      allc = allc && (pr[s] >> 4) == C;
-    }
-    // the pivot rows' entries of this wave's columns (values before the panel), as in panel<C>
-    const uint32_t rbq = (uint32_t)(uintptr_t)(Rb + q * NB);
-    if (allc) {
-      const uint32_t bkq = (uint32_t)(uintptr_t)(Bk + (ti * 4 + q) * NB);
-#pragma unroll
-      for (int c = 0; c < NB; ++c)
-        asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(bkq), "v"(a[C][c >> 2][c & 3]), "i"(8 * c) : "memory");
-    } else {
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int tip = pr[s] & 15, rp = pr[s] >> 4;
-        if (rp == C) {
-          if (ti == tip) {
-#pragma unroll
-            for (int c = 0; c < NB; ++c)
-              asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[C][c >> 2][c & 3]),
-                           "i"(8 * (s * 4 * NB + c)) : "memory");
-          }
-        } else {
-#pragma unroll
-          for (int r = 0; r < NB; ++r) {
-            if (r != C && r == rp) {
-              if (ti == tip) {
-#pragma unroll
-                for (int c = 0; c < NB; ++c)
-                  asm volatile("ds_write_b64 %0, %1 offset:%2" : : "v"(rbq), "v"(a[r][c >> 2][c & 3]),
-                               "i"(8 * (s * 4 * NB + c)) : "memory");
-              }
-              asm volatile("" ::: "memory");
-            }
-          }
-        }
-      }
-    }
-    wave_lds_sync();
-    PPH(3);
-    // look-ahead: the owner of panel t + 1 factors it now (its columns brought up to date by panel t here)
-    constexpr int CN = LAST ? C + 1 : C;
-    if constexpr (CN < NB) {
-      const int tn = t + 1;
-      const int won = LAST ? 0 : wo + 1;
-      if (4 * tn < n) {
-        if (wid == won) la_wait_all(sw + 4, tn - NPB, live);  // every wave is done with panel buffer tn % 3
-        la_stage<CN>(L, tn, wid == won, lane);
-        if (wid == won) la_own<CN>(L, tn, true, t, pr, allc, dm, ok, wid, lane);
-      }
-    }
-    PPH(0);
-    // the MFMA operands (loaded after the look-ahead block: live across it they overflow the register file)
-    const int sl = lane >> 4;
-    const int pl = sl == 0 ? pr[0] : (sl == 1 ? pr[1] : (sl == 2 ? pr[2] : pr[3]));
-    double A[NG];
-    {
-      const int j = lane & 15;
-      const double* ra = allc ? Bk + ((pl & 15) * 4 + (j & 3)) * NB + (j >> 2)
-                              : Rb + ((lane >> 4) * 4 + (j & 3)) * NB + (j >> 2);
-#pragma unroll
-      for (int g = 0; g < NG; ++g) A[g] = 4 * g + (j >> 2) < NB ? ra[4 * g] : 0.0;
-    }
-    double Bl[NB];
-#pragma unroll
-    for (int rb = 0; rb < NB; ++rb) Bl[rb] = Pb[(lane >> 4) * NC + 16 * rb + (lane & 15)];
-#pragma unroll
-    for (int rb = 0; rb < NB; ++rb) {
-      const int i = 16 * rb + (lane & 15);
-      const double Bv = Bl[rb] - (i == pl ? 1.0 : 0.0);
-#pragma unroll
-      for (int g = 0; g < NG; ++g) a[rb][g] = __builtin_amdgcn_mfma_f64_16x16x4f64(A[g], Bv, a[rb][g], 0, 0, 0);
-    }
-    PPH(4);
-    if (wid == wo) {  // the panel columns keep their processed values
-#pragma unroll
-      for (int r = 0; r < NB; ++r) a[r][G][E] = Pb[q * NC + ti + 16 * r];
-    }
-    la_signal(sw + 4 + wid, t, lane);  // this wave is done with panel buffer t % 3
-    PPH(5);
-#undef PPH
-  }
-
-  template <int C>
-  __device__ __forceinline__ void la_panels(const BigLds& L, int n, uint64_t (&dm)[NJ], bool& ok, bool& live, int wid,
-                                            int lane FPH_PARAM) {
-    if constexpr (C < NB) {
-#pragma unroll 1
-      for (int wo = 0; wo < 3; ++wo)
-        if (16 * C + 4 * wo < n) la_panel<C, false>(L, wo, n, dm, ok, live, wid, lane FPH_ARG);
-      if (16 * C + 12 < n) la_panel<C, true>(L, 3, n, dm, ok, live, wid, lane FPH_ARG);
-      la_panels<C + 1>(L, n, dm, ok, live, wid, lane FPH_ARG);
-    }
-  }
-
-  template <int SKIP = 0>
   __device__ __forceinline__ bool factor(const BigLds& L, Blk& B, int tid, int wid, int lane, int n
 #ifdef CKMI_PHASE_TIMERS
                                          , unsigned long long (&fph)[6]
@@ -1243,25 +938,7 @@ struct BigMatrixM {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) dm[j] = 0ull;
     bool ok = true;
-#ifndef CKMI_BIG_SYNC_BARRIER
-    if constexpr (!LA)
-#endif
-      panels<0, SKIP>(L, n, dm, ok, t, wid, lane FPH_ARG);
-#ifndef CKMI_BIG_SYNC_BARRIER
-    else {
-      int* sw = sync_words(L);
-      if (t < 4 + BW) sw[t] = t < 4 ? 0 : -1;  // nothing published, no panel finished
-      __syncthreads();
-      bool live = true;
-      if (n > 0) {
-        const int pr0[4] = {0, 0, 0, 0};
-        la_stage<0>(L, 0, wid == 0, lane);
-        if (wid == 0) la_own<0>(L, 0, false, 0, pr0, false, dm, ok, wid, lane);
-      }
-      la_panels<0>(L, n, dm, ok, live, wid, lane FPH_ARG);
-      __syncthreads();  // perm / rank complete, every wave's updates done
-    }
-#endif
+    panels<0>(L, n, dm, ok, t, wid, lane FPH_ARG);
     return ok;
   }
 
@@ -1305,21 +982,10 @@ struct BigMatrixM {
   }
 };
 
-#ifdef CKMI_BIG_VALU
-template <int NB, bool PL>
-using BigMat = BigMatrix<NB>;  // one workgroup barrier per column (VALU rank-1 updates)
-#else
 // NB = 12 (177..192 variables) keeps the per-column VALU factorisation: its MFMA form overflows
 // the register file (and crashes the ROCm 7.2 backend with the VGPR-form MFMA option)
-// The look-ahead factorisation (BigMatrixM::la_panels) is an A/B form: measured no faster (CKMI_BIG_LOOKAHEAD)
-#ifdef CKMI_BIG_LOOKAHEAD
 template <int NB, bool PL>
-using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB, (NB == 11 && !PL)>, BigMatrix<NB>>;
-#else
-template <int NB, bool PL>
-using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB, false>, BigMatrix<NB>>;
-#endif
-#endif
+using BigMat = std::conditional_t<(NB <= 11), BigMatrixM<NB>, BigMatrix<NB>>;
 
 // ------------------------------------------------------------------ general reactions
 // FORD / RORD orders and non-integral coefficients (mechanisms flagged has_general, PL = true):
@@ -1564,13 +1230,9 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
     for (int idx = tid; idx < jcb * LDJ; idx += NT) jb[idx] = 0.0;
     __syncthreads();
     const int lo = c0 + wid * cpw, hi = lo + cpw;  // this wave's columns
-#ifdef CKMI_BIG_JAC_LISTS
-    // A/B form: the unit slots naming this wave's species lo - 1 .. hi - 2 (host-built lists, ckmi.hip), one
-    // per lane: each wave visits only its own slots instead of all 8 IIp of them per column block.  3 % faster
-    // on configs[4] (427.0 vs 440.3 ms), but the atomics add into each Jacobian entry in another order, and
-    // the changed last bits reshuffle the step sequences: the c5 sample's worst element drift (3.06e-7, as
-    // before) then falls on a reactor whose oracle rtol envelope is 2.6e-9, outside test_configs4_sample's
-    // bar.  Off until that bar is a statistically robust one.
+    // the unit slots naming this wave's species lo - 1 .. hi - 2 (host-built CSR lists, ckmi.hip build_image),
+    // one per lane: each wave visits only its own slots instead of all 8 IIp of them per column block (3 % on
+    // configs[4]; the atomics add into each entry in another order than the all-slot walk did)
     {
       const int e0 = jptr[min(lo, n) - 1], e1 = jptr[min(hi, n) - 1];
       for (int e = e0 + lane; e < e1; e += WAVE) {
@@ -1602,45 +1264,6 @@ __device__ __forceinline__ double rhs_big(const MechView& V, const RunCtx& R, co
         if (inf & RX_GEN) gen_jac_cols_big(V, i, inf, Dg, IIp, jb, c0, lo, hi, LDJ);
       }
     }
-#else  // every slot of every reaction, per column block
-    (void)jptr;
-    (void)jent;
-    for (int base = 0; base < IIp; base += WAVE) {
-      const int i = base + lane;
-      const uint32_t inf = V.info()[i];
-      const int nr = rx_nr(inf), np = rx_np(inf);
-      if constexpr (PL) {
-        if (inf & RX_GEN) {  // the general reaction's slots and real coefficients (aux stream)
-          gen_jac_cols_big(V, i, inf, Dg, IIp, jb, c0, lo, hi, LDJ);
-          continue;
-        }
-      }
-      if (nr + np == 0) continue;
-      const uint32_t rs = V.rsp()[i], ps = V.psp()[i];
-#pragma unroll 1
-      for (int sl = 0; sl < 8; ++sl) {
-        const bool prod = sl >= 4;
-        const int u0 = sl & 3;
-        if (u0 >= (prod ? np : nr)) continue;
-        const int j = sp_of(prod ? ps : rs, u0);
-        const int col = 1 + j;
-        if (col < lo || col >= hi) continue;
-        const double dqw = Dg[sl * IIp + i] * V.rwt()[j];
-        double* jc = jb + (col - c0) * LDJ + 1;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (u < nr) {
-            const int k = sp_of(rs, u);
-            atomicAdd(&jc[k], -dqw * V.wt()[k]);
-          }
-          if (u < np) {
-            const int k = sp_of(ps, u);
-            atomicAdd(&jc[k], dqw * V.wt()[k]);
-          }
-        }
-      }
-    }
-#endif
     __syncthreads();
     // energy row J[0][c] = -(sum_k e_k J[1+k][c]) / cpm - fT c_{c-1} / cpm  (thread c = column c)
     if (tid >= c0 && tid < c0 + jcb && tid < n) {
@@ -1751,6 +1374,16 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           if (tid == 0) yl = T0;
           if (isp) yl = io.Y0[(size_t)r * KK + tid - 1];
           const double Wbar0 = 1.0 / bsum(B, isp ? yl * V.rwt()[tid - 1] : 0.0, wid, lane);
+          if (dcfg->npe) {  // initial element contents: the element projection's target
+            const uint64_t cnt = isp ? elem_table(V)[tid - 1] : 0ull;
+            const double rw = isp ? V.rwt()[tid - 1] : 0.0;
+            double v[PROJ_MMAX];
+#pragma unroll
+            for (int e = 0; e < PROJ_MMAX; ++e) v[e] = elem_coef(cnt, rw, e) * yl;
+            bsum8(B, v, wid, lane);
+#pragma unroll
+            for (int e = 0; e < PROJ_MMAX; ++e) c.eb0[e] = v[e];
+          }
           R.pfr = (prob == 3);
           R.conp = (prob == 1 || prob == 3);
           R.energy = cfg->energy;
@@ -2007,18 +1640,6 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
 #ifdef CKMI_PHASE_TIMERS
             ok = M.factor(L, B, tid, wid, lane, n, fph);
 #else
-#ifdef CKMI_BIG_FACTOR_TWICE  // timing experiment: the factorisation's share of the run time
-#ifndef CKMI_BIG_FACTOR_TWICE_SKIP
-#define CKMI_BIG_FACTOR_TWICE_SKIP 0
-#endif
-            if constexpr (NB <= 11 && CKMI_BIG_FACTOR_TWICE_SKIP != 0)
-              (void)M.template factor<CKMI_BIG_FACTOR_TWICE_SKIP>(L, B, tid, wid, lane, n);
-            else
-              (void)M.factor(L, B, tid, wid, lane, n);
-            __syncthreads();
-            M.build(Jg, S.gamma, tid, n);
-            __syncthreads();
-#endif
             ok = M.factor(L, B, tid, wid, lane, n);
 #endif
             BPH_ADD(3);
@@ -2049,26 +1670,35 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
           S.nni++;
           if (S.gamrat != 1.0) x *= 2.0 / (1.0 + S.gamrat);
           if (!act) x = 0.0;
-          const double del = bwrms(B, x, b.ewt, n, wid, lane);
+          // the iteration's norms in one barrier (ckmi.hip reactor_kernel): del, acnrm, NNEG's negative part
+          // and acnrm after NNEG's clipping
+          const double z0 = b.zn[0];
           b.acor += x;
-          b.y = b.zn[0] + b.acor;
+          b.y = z0 + b.acor;
+          const bool neg = S.nneg && act && tid >= 1 && b.y < 0.0;
+          double nv[4];
+          {
+            const double xe = x * b.ewt, ae = b.acor * b.ewt, ne = neg ? b.y * b.ewt : 0.0;
+            const double fe2 = neg ? z0 * b.ewt : ae;
+            nv[0] = xe * xe;
+            nv[1] = ae * ae;
+            nv[2] = ne * ne;
+            nv[3] = fe2 * fe2;
+          }
+          bsumn<4>(B, nv, wid, lane);
+          const double del = sqrt(nv[0] / n);
           if (c.mm > 0) S.crate = fmax(CRDOWN * S.crate, del / c.delp);
           const double dcon = del * fmin(1.0, S.crate) / S.tq[4];
           if (dcon <= 1.0) {
             bool negfail = false, negfix = false;
-            if (S.nneg) {
-              const bool neg = act && tid >= 1 && b.y < 0.0;
-              const double xn = neg ? b.y * b.ewt : 0.0;
-              const double ss = bsum(B, xn * xn, wid, lane);
-              if (ss > 0.0) {
-                if (sqrt(ss / n) > NNEG_TOL) {
-                  negfail = true;
-                } else {
-                  negfix = true;
-                  if (neg) {
-                    b.y = 0.0;
-                    b.acor = -b.zn[0];
-                  }
+            if (S.nneg && nv[2] > 0.0) {
+              if (sqrt(nv[2] / n) > NNEG_TOL) {
+                negfail = true;
+              } else {
+                negfix = true;
+                if (neg) {
+                  b.y = 0.0;
+                  b.acor = -z0;
                 }
               }
             }
@@ -2077,7 +1707,7 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
               st = ST_NLS_FAIL;
               break;
             }
-            S.acnrm = (c.mm == 0 && !negfix) ? del : bwrms(B, b.acor, b.ewt, n, wid, lane);
+            S.acnrm = (c.mm == 0 && !negfix) ? del : sqrt((negfix ? nv[3] : nv[1]) / n);
             S.jcur = 0;
             st = ST_ERRTEST;
             break;
@@ -2180,6 +1810,58 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             if (i <= S.q) S.tau[i] = S.tau[i - 1];
           if (S.q == 1 && S.nst > 1) S.tau[2] = S.tau[1];
           S.tau[1] = S.h;
+          // One workgroup barrier per accepted step: the element sums of the corrector, the q - 1 / q + 1 norms of
+          // a step that selects the next order (both from the corrector before the element projection, oracle
+          // bdf_step), thread 0's h dT/dt after the history update (the TIFP monitor) as a sum, and the runaway
+          // guard's maximum over the accepted state (ckmi.hip: a ballot; checked on y before the projection,
+          // which moves each Y_k by a relative ~1e-10 at most)
+          double ddn = 0.0, dup = 0.0;
+          {
+            const bool sel = S.etamax != 1.0 && S.qwait == 1;
+            const bool qm = sel && S.q > 1, qp = sel && S.q != QMAX && S.saved_tq5 != 0.0;
+            double cquot = 0.0;
+            if (qp) {
+              const double hr = S.h / S.tau[2];
+              double hrL = hr;
+              for (int j = 1; j < S.L; ++j) hrL *= hr;
+              cquot = (S.tq[5] / S.saved_tq5) * hrL;
+            }
+            double znq = 0.0, lq = 0.0;
+#pragma unroll
+            for (int j = 0; j <= QMAX; ++j)
+              if (j == S.q) {
+                znq = b.zn[j];
+                lq = S.l[j];
+              }
+            const double y = b.zn[0] + b.acor;
+            const int npe = dcfg->npe;
+            const uint64_t cnt = (isp && npe) ? elem_table(V)[tid - 1] : 0ull;
+            const double rw = isp ? V.rwt()[tid - 1] : 0.0;
+            double v[16];
+#pragma unroll
+            for (int e = 0; e < PROJ_MMAX; ++e) v[e] = elem_coef(cnt, rw, e) * y;
+            const double a = (act && qm) ? (znq + lq * b.acor) * b.ewt : 0.0;
+            const double t = (act && qp) ? (b.acor - cquot * b.zn[QMAX]) * b.ewt : 0.0;
+            v[8] = a * a;
+            v[9] = t * t;
+            v[10] = tid == 0 ? b.zn[1] + S.l[1] * b.acor : 0.0;
+#pragma unroll
+            for (int e = 11; e < 16; ++e) v[e] = 0.0;
+            double mx = isp ? -y : -1.0;
+            if (tid == 0 && R.energy == 1 && runaway_value_bad(dcfg, y)) mx = 1e300;
+            bsumn_max<16>(B, v, mx, wid, lane);
+            c.rc = mx > dcfg->guard_y ? CKMI_RUN_RUNAWAY : 0;
+            c.tdh = v[10];
+            ddn = sqrt(v[8] / n) * S.tq[1];
+            dup = sqrt(v[9] / n) * S.tq[3];
+            // element conservation held to PROJ_TOL rtol (oracle elem_project), before the history update
+            if (npe) {
+              double r[PROJ_MMAX];
+#pragma unroll
+              for (int e = 0; e < PROJ_MMAX; ++e) r[e] = v[e];
+              elem_project_big(V, B, npe, r, c.eb0, S.rtol, y, b.acor, tid, wid, lane, lds_at<double>(L.ek));
+            }
+          }
 #pragma unroll
           for (int j = 0; j <= QMAX; ++j)
             if (j <= S.q) b.zn[j] += S.l[j] * b.acor;
@@ -2201,23 +1883,8 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             } else {
               S.qwait = 2;
               double etaqm1 = 0.0, etaqp1 = 0.0;
-              if (S.q > 1) {
-                double znq = 0.0;
-#pragma unroll
-                for (int j = 0; j <= QMAX; ++j)
-                  if (j == S.q) znq = b.zn[j];
-                const double ddn = bwrms(B, act ? znq : 0.0, b.ewt, n, wid, lane) * S.tq[1];
-                etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, S.q) + ADDON);
-              }
-              if (S.q != QMAX && S.saved_tq5 != 0.0) {
-                const double hr = S.h / S.tau[2];
-                double hrL = hr;
-                for (int j = 1; j < S.L; ++j) hrL *= hr;
-                const double cquot = (S.tq[5] / S.saved_tq5) * hrL;
-                const double tv = act ? b.acor - cquot * b.zn[QMAX] : 0.0;
-                const double dup = bwrms(B, tv, b.ewt, n, wid, lane) * S.tq[3];
-                etaqp1 = 1.0 / (eta_root(BIAS3 * dup, S.L + 1) + ADDON);
-              }
+              if (S.q > 1) etaqm1 = 1.0 / (eta_root(BIAS1 * ddn, S.q) + ADDON);
+              if (S.q != QMAX && S.saved_tq5 != 0.0) etaqp1 = 1.0 / (eta_root(BIAS3 * dup, S.L + 1) + ADDON);
               const double etam = fmax(etaqm1, fmax(etaq, etaqp1));
               if (etam < THRESH) {
                 S.eta = 1.0;
@@ -2244,13 +1911,6 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             }
           }
           S.etamax = (S.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-          {  // runaway guard on the accepted state (ckmi.hip reactor_kernel): one workgroup max per step,
-             // the reactor ends through ST_STEP_END's failure exit
-            const double z0 = b.zn[0];
-            double v = isp ? -z0 : -1.0;
-            if (tid == 0 && R.energy == 1 && runaway_value_bad(dcfg, z0)) v = 1e300;
-            c.rc = bmax(B, v, wid, lane) > dcfg->guard_y ? CKMI_RUN_RUNAWAY : 0;
-          }
           if (R.pfr && R.npv == 0 && c.rc == 0) {  // plug flow past the choke point (pfr_pressure)
             double Tz = b.zn[0];
             const double sYW = bsum_bcast(B, isp ? Tz * V.rwt()[tid - 1] : 0.0, Tz, 0, tid, wid, lane);
@@ -2271,14 +1931,16 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
             if (act) io.y_save[((size_t)c.r * io.nsave + c.isave) * n + tid] = ys;
             c.isave++;
           }
-          // every thread's Nordsieck update of this step is visible after this barrier: component
-          // 0's history (b0) is read directly from LDS below
-          const double T_n = bbcast(B, b.zn[0], 0, tid);
+          // T of the accepted state (thread 0), when a monitor or the stop rule needs it; TIFP reads h dT/dt
+          // from the step's fused reduction
+          const bool need_T = ((g.mode == 2 || g.mode == 3) && !g.found) || (cfg->ign_stop && g.mode == 1);
+          const double T_n = need_T ? bbcast(B, b.zn[0], 0, tid) : 0.0;
           if (g.mode == 1) {
-            ign_peak_update(g, tn, b0.zn[1] / S.h);
+            ign_peak_update(g, tn, c.tdh / S.h);
           } else if (g.mode == 4) {
             ign_peak_update(g, tn, bbcast(B, b.zn[0], g.comp, tid));
           } else if ((g.mode == 2 || g.mode == 3) && !g.found && T_n >= g.thresh) {
+            // (the bbcast above ordered every thread's history update: thread 0's history is read from LDS)
             double lo = c.told, hi = tn;
             for (int it = 0; it < 60; ++it) {
               const double mid = 0.5 * (lo + hi);
@@ -2408,28 +2070,36 @@ __global__ __launch_bounds__(NT, 1) void big_reactor_kernel(MechImage img, BigLd
 }
 
 // ------------------------------------------------------------------ host side
-BigLds big_layout(const ckmi_mech* m, int NC, int lds_max) {
+// doubles of the xpart region (solve partial sums / MFMA factorisation buffers) for an NC x NC matrix
+int big_xpart_doubles(int NC) {
+  const int NB = NC / 16, NBP = (NB + 1) & ~1;
+  const int mfma = NB <= 11 ? 2 * 4 * NC + BW * 16 * NB + BW * 64 * NB : 0;
+  return std::max(NT * NBP, mfma);
+}
+
+// LDS layout for a mechanism image of img_bytes (KKp padded species, G third-body groups)
+BigLds big_layout(int img_bytes, int KKp, int G, int NC, int lds_max) {
   BigLds L;
-  const MechImage& I = m->img;
-  int o = I.bytes;
+  int o = img_bytes;
   auto take = [&](int bytes) {
     const int r = o;
     o += align16(bytes);
     return r;
   };
-  const int KKp = I.KKp;
+  const int NB = NC / 16;
   L.C = take(8 * KKp);
   L.gRT = take(8 * KKp);
   L.hRT = take(8 * KKp);
   L.ek = take(8 * KKp);
   L.wdot = take(8 * BW * KKp);
   L.dwdT = take(8 * BW * KKp);
-  L.Mg = take(8 * std::max(1, I.G));
+  L.Mg = take(8 * std::max(1, G));
   L.zn = take(8 * (QMAX + 1) * NT);
-  const int NBP = (NC / 16 + 1) & ~1;
-  L.prow = take(8 * BW * 4 * NBP);
-  L.gcol = take(8 * 2 * 16 * NBP);
-  L.phdr = take(3 * 32 + 32);  // [2] PivHdr (VALU factor) or [3] PanHdr + sync words (MFMA factor)
+  const int NBP = (NB + 1) & ~1;
+  const bool valu = NB > 11;  // BigMatrix (per-column steps) needs the pivot-row and column buffers
+  L.prow = valu ? take(8 * BW * 4 * NBP) : 0;
+  L.gcol = valu ? take(8 * 2 * 16 * NBP) : 0;
+  L.phdr = take(2 * 32);  // [2] PivHdr (VALU factor) or [2] PanHdr (MFMA factor)
   L.perm = take(4 * NT);
   L.rank = take(4 * NT);
   L.bp = take(8 * 16 * NBP);
@@ -2438,10 +2108,10 @@ BigLds big_layout(const ckmi_mech* m, int NC, int lds_max) {
   // the Jacobian column block takes what is left (multiple of BW columns, at most the matrix)
   const int LDJ = NT + 1;
   int jcb = (lds_max - align16(o) - 16) / (8 * LDJ);
-  // xpart: the solve's partial sums [NT][NBP], or the factorisation's panel buffers [3][4][NC], per-wave
-  // pivot rows [BW][16 NB], per-wave diagonal block rows [BW][64 NB] and a [4][NC] staging scratch
-  // (BigMatrixM::pan_buf etc.)
-  const int xneed = 8 * std::max(NT * NBP, 16 * NC + BW * 16 * (NC / 16) + BW * 64 * (NC / 16));
+  // xpart: the solve's partial sums [NT][NBP]; with the MFMA factorisation (NB <= 11, BigMat) also its panel
+  // buffers [2][4][NC], per-wave pivot rows [BW][16 NB] and per-wave diagonal block rows [BW][64 NB]
+  // (BigMatrixM::pan_buf / row_buf / blk_buf)
+  const int xneed = 8 * big_xpart_doubles(NC);
   if (8 * LDJ * jcb < xneed && lds_max - align16(o) - 16 < xneed) jcb = 0;  // xpart must fit
   jcb = std::min(jcb, (NC + BW - 1) / BW * BW);
   jcb = jcb / BW * BW;
@@ -2457,7 +2127,7 @@ int launch_big_nc(const ckmi_mech* m, int n, const DevCfg& dc, const ReactorIO& 
   int lds_max = 0, ncu = 0, per_cu = 0;
   BIG_CHECK(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, m->device));
   BIG_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
-  const BigLds L = big_layout(m, 16 * NB, lds_max);
+  const BigLds L = big_layout(m->img.bytes, m->img.KKp, m->img.G, 16 * NB, lds_max);
   if (L.jcb < BW)
     return set_error(CKMI_ERR_SIZE, "mechanism image too large for the workgroup-per-reactor kernel's LDS (" +
                                         std::to_string(m->img.bytes) + " B image)");
@@ -2541,3 +2211,22 @@ extern "C" int ckmi_debug_big_phase_buffer(void* buf) {
   return CKMI_OK;
 }
 #endif
+
+// largest mechanism image (bytes, 16-B multiple) the workgroup kernel accepts for nvar = KK + 1 state variables
+// (KKp padded species, G third-body groups) on a CU with lds_max bytes of LDS; -1 if none fits.  Host-only.
+extern "C" int ckmi_big_max_image_bytes(int nvar, int KKp, int G, int lds_max) {
+  if (nvar < 1 || nvar > ckmi::BIG_NMAX) return -1;
+  const int NC = 16 * ((nvar + 15) / 16 < 4 ? 4 : (nvar + 15) / 16);
+  int best = -1;
+  for (int lo = 0, hi = lds_max; lo <= hi;) {
+    const int mid = ((lo + hi) / 2) & ~15;
+    const ckmi::BigLds L = ckmi::big_layout(mid, KKp, G, NC, lds_max);
+    if (L.jcb >= ckmi::BW && L.bytes <= lds_max) {
+      best = mid;
+      lo = mid + 16;
+    } else {
+      hi = mid - 16;
+    }
+  }
+  return best;
+}

@@ -83,50 +83,96 @@ constexpr int DPP_QUAD_2301 = 0x4E;  // quad_perm [2,3,0,1]
 constexpr int DPP_ROW_HALF_MIRROR = 0x141;
 constexpr int DPP_ROW_MIRROR = 0x140;
 
-// Across the four rows: the gfx950 row swaps (v_permlane16_swap pairs rows 0-1 and 2-3,
-// v_permlane32_swap the two halves) hand every lane its partner row's value, so each lane forms
-// (s0 + s1) + (s2 + s3) itself -- the association of the readlane form, bitwise, without the 8
-// readlanes and their SGPR round trip.  A/B form (CKMI_REDUCE_SWAP): bitwise the same results, no faster
-// (c3 244.7 vs 243.1 ms, c5 438.7 vs 439.5 ms on the A/B samples, profiles/r05_ab_reduce_swap_*.log).
-template <bool HALVES>
-__device__ __forceinline__ void row_swap(double v, double& own, double& other) {
-  const uint32_t lo = (uint32_t)__double2loint(v), hi = (uint32_t)__double2hiint(v);
-  const auto l = HALVES ? __builtin_amdgcn_permlane32_swap(lo, lo, false, false)
-                        : __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-  const auto h = HALVES ? __builtin_amdgcn_permlane32_swap(hi, hi, false, false)
-                        : __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-  own = __hiloint2double((int)h[0], (int)l[0]);  // {own, partner} in a row-dependent order:
-  other = __hiloint2double((int)h[1], (int)l[1]);  // only commutative combinations of the two
-}
 __device__ __forceinline__ double wave_sum(double v) {
   v += dpp_mov<DPP_QUAD_1032>(v);
   v += dpp_mov<DPP_QUAD_2301>(v);
   v += dpp_mov<DPP_ROW_HALF_MIRROR>(v);
   v += dpp_mov<DPP_ROW_MIRROR>(v);
-#ifndef CKMI_REDUCE_SWAP
   return uni((bcast(v, 0) + bcast(v, 16)) + (bcast(v, 32) + bcast(v, 48)));
-#else
-  double a, b;
-  row_swap<false>(v, a, b);
-  v = a + b;
-  row_swap<true>(v, a, b);
-  return uni(a + b);
-#endif
 }
 __device__ __forceinline__ double wave_max(double v) {
   v = fmax(v, dpp_mov<DPP_QUAD_1032>(v));
   v = fmax(v, dpp_mov<DPP_QUAD_2301>(v));
   v = fmax(v, dpp_mov<DPP_ROW_HALF_MIRROR>(v));
   v = fmax(v, dpp_mov<DPP_ROW_MIRROR>(v));
-#ifndef CKMI_REDUCE_SWAP
   return uni(fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48))));
-#else
-  double a, b;
-  row_swap<false>(v, a, b);
-  v = fmax(a, b);
-  row_swap<true>(v, a, b);
-  return uni(fmax(a, b));
-#endif
+}
+
+// ------------------------------------------------------------------ multi-value wave sums
+// NV values per lane summed over the wave in one pass: a reduce-scatter over the six lane bits, each
+// stage halving the registers (the lane's bit picks which one of a pair it keeps; its partner gets the
+// other), then plain all-reduce stages once one register is left.  Stages: bit 5 by v_permlane32_swap,
+// bit 4 by v_permlane16_swap (each pairs two registers in one instruction per dword: no selects), bits
+// 3 / 2 / 1 / 0 by DPP row_mirror / row_half_mirror / quad_perm (partners 15 - i, 7 - i, i ^ 2, i ^ 1 of
+// the 16-lane row).  8 values: 4 + 2 + 1 pair stages + 3 all-reduce stages (~34 VALU issues) instead of 8
+// wave_sums (~180).  The sum of value j ends in the lanes whose bits 5, 4, 3, .. are the binary digits
+// 0, 1, 2, .. of j (wave_sum_lane); the association is fixed, so results are deterministic and the same
+// in every wave.
+__device__ __forceinline__ void swap_rows(double& a, double& b, bool halves) {
+  const uint32_t al = (uint32_t)__double2loint(a), ah = (uint32_t)__double2hiint(a);
+  const uint32_t bl = (uint32_t)__double2loint(b), bh = (uint32_t)__double2hiint(b);
+  const auto l = halves ? __builtin_amdgcn_permlane32_swap(al, bl, false, false)
+                        : __builtin_amdgcn_permlane16_swap(al, bl, false, false);
+  const auto h = halves ? __builtin_amdgcn_permlane32_swap(ah, bh, false, false)
+                        : __builtin_amdgcn_permlane16_swap(ah, bh, false, false);
+  a = __hiloint2double((int)h[0], (int)l[0]);
+  b = __hiloint2double((int)h[1], (int)l[1]);
+}
+template <int S>
+__device__ __forceinline__ double dpp_partner(double v) {  // stage S = 2..5: the partner across lane bit 5 - S
+  if constexpr (S == 2) return dpp_mov<DPP_ROW_MIRROR>(v);
+  else if constexpr (S == 3) return dpp_mov<DPP_ROW_HALF_MIRROR>(v);
+  else if constexpr (S == 4) return dpp_mov<DPP_QUAD_2301>(v);
+  else return dpp_mov<DPP_QUAD_1032>(v);
+}
+template <int S, int R, int NV>
+__device__ __forceinline__ void wave_sum_stages(double (&v)[NV], int lane) {
+  if constexpr (S < 6) {
+    if constexpr (R > 1) {
+#pragma unroll
+      for (int j = 0; j < R / 2; ++j) {
+        double a = v[2 * j], b = v[2 * j + 1];
+        if constexpr (S < 2) {
+          swap_rows(a, b, S == 0);  // lanes with bit 5 - S clear: a = (own, partner) of v[2j], else of v[2j+1]
+          v[j] = a + b;
+        } else {
+          const bool hi = (lane >> (5 - S)) & 1;
+          const double send = hi ? a : b, keep = hi ? b : a;
+          v[j] = keep + dpp_partner<S>(send);
+        }
+      }
+      wave_sum_stages<S + 1, R / 2>(v, lane);
+    } else {
+      if constexpr (S < 2) {
+        double a = v[0], b = v[0];
+        swap_rows(a, b, S == 0);
+        v[0] = a + b;
+      } else {
+        v[0] += dpp_partner<S>(v[0]);
+      }
+      wave_sum_stages<S + 1, 1>(v, lane);
+    }
+  }
+}
+// the lane holding the sum of value j (any lane with these upper bits holds it)
+__device__ __forceinline__ constexpr int wave_sum_lane(int j) {
+  return ((j & 1) << 5) | ((j & 2) << 3) | ((j & 4) << 1) | ((j & 8) >> 1) | ((j & 16) >> 3) | ((j & 32) >> 5);
+}
+// the value index a lane holds after wave_sum_multi<NV> (inverse of wave_sum_lane on the top log2 NV bits)
+template <int NV>
+__device__ __forceinline__ int wave_sum_index(int lane) {
+  int j = 0;
+#pragma unroll
+  for (int s = 0; (1 << s) < NV; ++s) j |= ((lane >> (5 - s)) & 1) << s;
+  return j;
+}
+// v[j] <- sum over the wave of v[j], in every lane (wave-uniform); NV a power of two <= 64
+template <int NV>
+__device__ __forceinline__ void wave_sum_multi(double (&v)[NV], int lane) {
+  wave_sum_stages<0, NV>(v, lane);
+  const double x = v[0];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = bcast(x, wave_sum_lane(j));
 }
 
 // max of a u32 over the wave (DPP inside rows, readlanes across them); the pivot search

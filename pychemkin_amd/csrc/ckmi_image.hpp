@@ -152,19 +152,11 @@ __device__ __forceinline__ double powi(double c, int nu) {
 // so a wave's random-index gathers never conflict (a 64-entry table put entries j and j + 32 on one
 // bank pair: ~2-way on most gathers).  ~17 VALU instructions + 1 LDS read instead of ~40 for the
 // library exp.  NaN propagates; |x| > 1000 saturates to 0 / inf.
-#ifndef CKMI_E2T_64
 constexpr int E2T_N = 32;
 constexpr int E2T_SHIFT = 5;
 constexpr double E2T_INV_L = 46.166241308446828;          // 32 / ln 2
 constexpr double E2T_L_HI = 0x1.62e42fefa39efp-6;         // (ln 2)_hi / 32
 constexpr double E2T_L_LO = 0x1.abc9e3b39803fp-61;        // (ln 2)_lo / 32
-#else  // A/B only: the round-3 64-entry table
-constexpr int E2T_N = 64;
-constexpr int E2T_SHIFT = 6;
-constexpr double E2T_INV_L = 92.332482616893656;
-constexpr double E2T_L_HI = 0x1.62e42fefa39efp-7;
-constexpr double E2T_L_LO = 0x1.abc9e3b39803fp-62;
-#endif
 __device__ __forceinline__ double fexp(double x, const double* e2t) {
   constexpr double INV_L = E2T_INV_L, L_HI = E2T_L_HI, L_LO = E2T_L_LO;
   x = x < -1000.0 ? -1000.0 : (x > 1000.0 ? 1000.0 : x);

@@ -74,6 +74,7 @@ struct ckmi_mech {
   bool has_general = false;  // FORD / RORD / non-integral coefficients (rxn_general)
   std::vector<int> slot_of;  // original reaction -> device slot
   double tguard_lo = 0.0, tguard_hi = 1e300;  // runaway guard: min_k T_low,k / 2, max_k T_high,k
+  int npe = 0;  // elements of the corrector's element projection (image element table), 0 = none
   ckmi::JitRop* jit = nullptr;
 };
 

@@ -507,7 +507,12 @@ int register_set(const ckmi_mech_desc* desc, int32_t MM, const char* names, cons
                  const double* awt, const int32_t* ncf, int32_t* chemset, ChemSet** out) {
   if (!desc || !chemset || MM < 0) return fail(CKMI_ERR_ARG, "null argument");
   auto* s = new ChemSet();
-  int rc = ckmi_mech_create(desc, &s->mech);
+  ckmi_mech_desc dd = *desc;  // the element counts also drive the reactors' element projection
+  if (!dd.ncf && ncf && MM > 0) {
+    dd.MM = MM;
+    dd.ncf = ncf;
+  }
+  int rc = ckmi_mech_create(&dd, &s->mech);
   if (rc) {
     delete s;
     return fail(rc, ckmi_last_error());

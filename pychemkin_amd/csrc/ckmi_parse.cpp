@@ -873,6 +873,8 @@ int ckmi_parsed_desc(const ckmi_parsed* p, ckmi_mech_desc* d) {
   d->eff_ptr = m.eff_ptr.data(), d->eff_sp = m.eff_sp.data(), d->eff_val = m.eff_val.data();
   d->plog_ptr = m.plog_ptr.data(), d->plog_par = m.plog_par.data();
   d->ford = m.ford.data(), d->rord = m.rord.data();
+  d->MM = (int32_t)m.elements.size();
+  d->ncf = m.ncf.data();
   return CKMI_OK;
 }
 

@@ -59,6 +59,9 @@ struct DevCfg {
   double tcrit[192];  // breakpoints of the three profiles (64 each)
   // runaway guard (CKMI_RUN_RUNAWAY): -Y_k above guard_y, or T outside [guard_tlo, guard_thi]
   double guard_y, guard_tlo, guard_thi;
+  // element projection of the accepted corrector (oracle elem_project): elements in the image's element
+  // table (0 = off: no element counts, more than CKMI_PROJ_MMAX elements, or cfg.no_elem_proj)
+  int npe;
 };
 // true when an accepted state has left the physical domain (tested once per step by both kernels;
 // oracle/ckoracle.c runaway() is the same test)
@@ -96,6 +99,8 @@ struct Ctl {
   double delp, saved_t, told, dsm, tc, tend, hmax, T0;
   double yguard, tguard_lo, tguard_hi;  // runaway guard (DevCfg), copied per reactor
   double st_h0, st_tout, st_h, is_hg, is_hub, is_hlb, is_t0;
+  double eb0[PROJ_MMAX];  // the reactor's initial element contents (element projection)
+  double tdh;             // h dT/dt of the accepted state (workgroup kernel: from the step's fused reduction)
 };
 
 // Per-wave LDS slice: 6 species vectors, third-body sums, integrator scalars, control state,

@@ -157,11 +157,10 @@ def register(mech) -> int:
     """Register a parsed Mechanism (pychemkin_amd.mechanism) as a KIN chemistry set on the current
     GPU; returns the chemistry-set index (the value KINPreProcess returns in the reference)."""
     L = bind()
-    tables = {k: np.ascontiguousarray(v) for k, v in mech.to_tables().items() if isinstance(v, np.ndarray)}
+    t = mech.to_tables()
+    tables = {k: np.ascontiguousarray(v) for k, v in t.items() if isinstance(v, np.ndarray) and v.ndim > 0}
     d = _native.MechDesc()
-    d.KK, d.II = int(mech.KK), int(mech.II)
-    for name, _ in _native.MechDesc._fields_[2:]:
-        setattr(d, name, tables[name].ctypes.data)
+    _native.fill_desc(d, t, tables)
     awt = np.ascontiguousarray(mech.awt, dtype=np.float64)
     ncf = np.ascontiguousarray(mech.ncf, dtype=np.int32)  # [MM][KK]
     cs = ct.c_int32(0)

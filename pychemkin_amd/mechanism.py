@@ -701,6 +701,8 @@ class Mechanism:
             eff_val=np.asarray(eff_val, np.float64),
             plog_ptr=plog_ptr,
             plog_par=np.asarray(plog_par if plog_par else [(0.0, 0.0, 0.0, 0.0)], np.float64).reshape(-1, 4),
+            # element counts (KINGetGasSpeciesComposition): the reactors' element projection
+            MM=np.int32(self.ncf.shape[0]), ncf=np.ascontiguousarray(self.ncf, np.int32),
         )
 
 

@@ -46,6 +46,13 @@ class Keyword:
             line = f"{self.keyphrase}    {self.value}"
         return len(line), line
 
+    @staticmethod
+    def setfullkeywords(mode: bool) -> None:
+        """Full-keyword mode ON/OFF (reference reactormodel.py:183-197): protected keywords may then be set
+        with setkeyword, and run() hands the whole keyword block to the KIN full-keyword input path
+        (KINAll0D_CalculateInput, include/ckmi_kin.h) instead of the typed configuration."""
+        Keyword.noFullKeyword = not bool(mode)
+
 
 class Profile:
     """A piecewise-linear profile keyword such as VPRO (reference reactormodel.py:467-665)."""
@@ -90,6 +97,9 @@ class ReactorModel:
         self._solution_rawarray: dict = {}
         self._solution_mixturearray: List[Mixture] = []
         self._gasratemultiplier = 1.0
+        # required inputs (batchreactor.py:1814-1815 for the batch reactors) and the ones given so far
+        self._requiredlist: List[str] = []
+        self._inputcheck: List[str] = []
 
     # ------------------------------------------------------------------ state
     @property
@@ -183,6 +193,28 @@ class ReactorModel:
             raise ReactorError("gas rate multiplier must be > 0")
         self._gasratemultiplier = float(value)
         self._set_internal("GFAC", float(value))
+
+    def usefullkeywords(self, mode: bool) -> None:
+        """Specify all keywords explicitly (reference reactormodel.py:814-835): turns the process-wide
+        full-keyword mode ON/OFF (Keyword.setfullkeywords)."""
+        Keyword.setfullkeywords(mode)
+        if mode:
+            logger.info("reactor %s will be run with full keyword input mode", self.label)
+
+    def setsolutionspeciesfracmode(self, mode: str = "mass") -> None:
+        """Species fractions returned by the post-processor, 'mass' or 'mole' (reference
+        reactormodel.py:1816-1838): process_solution's species profiles and the solution mixtures' composition."""
+        m = str(mode).lower()
+        if m not in ("mole", "mass"):
+            raise ReactorError('invalid species fraction mode, use mode = "mass" or mode = "mole"')
+        self._speciesmode = m
+
+    def validate_inputs(self) -> int:
+        """Number of required inputs still missing, each logged (reference batchreactor.py:794-820)."""
+        missing = [k for k in self._requiredlist if k not in self._inputcheck]
+        for k in missing:
+            logger.error("missing required input: %s", k)
+        return len(missing)
 
     # ------------------------------------------------------------------ status
     def setrunstatus(self, code: int) -> None:

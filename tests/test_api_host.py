@@ -217,3 +217,44 @@ def test_static_rate_calls_check_arguments(chem):
     air = ck.Mixture(chem)
     air.use_idealgas_law()
     assert air.userealgas is False
+
+
+def test_dropin_gap_methods_with_reference_signatures(chem):
+    """setsolutionspeciesfracmode (reactormodel.py:1816), usefullkeywords (:814), validate_inputs
+    (batchreactor.py:794) and create_solution_mixtures (:1487) with the reference's signatures (host only)."""
+    from pychemkin_amd.reactormodel import Keyword
+
+    r = _reactor(chem)
+    assert r.validate_inputs() == 1  # TIME (batchreactor.py:1814-1815)
+    r.time = 5e-4
+    assert r.validate_inputs() == 0
+    r.setsolutionspeciesfracmode(mode="mole")
+    assert r._speciesmode == "mole"
+    r.setsolutionspeciesfracmode()
+    assert r._speciesmode == "mass"
+    with pytest.raises(ReactorError):
+        r.setsolutionspeciesfracmode("volume")
+    assert r.create_solution_mixtures(np.zeros((chem.KK, 1))) == 1  # nothing processed yet
+    with pytest.raises(ReactorError):
+        r.setkeyword("CONP", True)  # protected in API mode
+    try:
+        r.usefullkeywords(True)
+        assert Keyword.noFullKeyword is False
+        r.setkeyword("CONP", True)  # full-keyword mode: protected keywords may be set
+        r.removekeyword("CONP")
+        r.tolerances = (1e-20, 1e-8)
+        r.force_nonnegative = True
+        r.set_ignition_delay(method="T_rise", val=400)
+        lines = r.full_keyword_lines()
+    finally:
+        r.usefullkeywords(False)
+    assert Keyword.noFullKeyword is True
+    # the block of batchreactor.py:822-925: keywords, TRAN, CONP, ENRG, PRES [atm], TEMP, TIME, REAC, QRGEQ, END
+    assert lines[-2:] == ["QRGEQ", "END"]
+    for must in ("ATOL    1e-20", "RTOL    1e-08", "NNEG", "DTIGN    400.0", "TRAN", "CONP", "ENRG", "PRES    1.0",
+                 "TEMP    1000.0", "TIME    0.0005"):
+        assert must in lines, must
+    reac = [x for x in lines if x.startswith("REAC")]
+    assert sorted(x.split()[1] for x in reac) == ["H2", "N2", "O2"]
+    X = dict((x.split()[1], float(x.split()[2])) for x in reac)
+    assert abs(X["O2"] - 1.0 / 6.76) < 1e-15 and abs(sum(X.values()) - 1.0) < 1e-15

@@ -21,13 +21,13 @@ def _drift(mech, Y0, Y):
     return np.max(np.abs(e1 - e0) / np.max(e0, axis=1, keepdims=True), axis=1)
 
 
-def _conservation(mech, Y0, Y, tol=1e-7):
-    """Mass closes to 1e-7 and elements are conserved to `tol` in every reactor.  Elements are kept
-    only up to the Newton convergence of each BDF step (the corrector is not projected), so the
-    drift is a chaotic property of the step sequence: per reactor it does not correlate between
-    GPU and oracle (rounding flips step decisions), but its distribution matches
-    (scripts/drift_diag.py: median 1.7e-12 vs 1.5e-12, 99th pct 2e-10 vs 3e-10 on 1024 configs[2]
-    reactors).  The worst of 2^20 reactors drifts ~1e-7."""
+def _conservation(mech, Y0, Y, tol=2e-9):
+    """Mass closes to 1e-7 and elements are conserved to `tol` in every reactor.  The integrators hold
+    element conservation to 0.1 rtol (1e-9 at the bench's rtol 1e-8): an accepted step whose element
+    content has drifted further is projected back (include/ckmi.h no_elem_proj, oracle elem_project);
+    below that the drift is the chaotic residue of the Newton convergence of each step (round 5, without
+    the projection: a tail up to 3e-7 on the GPU, 13x the oracle's on some configs[4] reactors).  The
+    final state is interpolated inside the last step, hence the bar of 0.2 rtol."""
     assert np.allclose(Y.sum(axis=1), 1.0, atol=1e-7)
     d = _drift(mech, Y0, Y)
     assert d.max() < tol
@@ -36,7 +36,8 @@ def _conservation(mech, Y0, Y, tol=1e-7):
 
 def _oracle_sample(mech, T0, P0, Y0, prob, res, nsample, d_gpu, threads=16):
     """tau and final T of a strided subsample against the oracle (1e-4), and the element-drift
-    distribution of the GPU on that subsample against the oracle's (90th percentile within 10x)."""
+    distribution of the GPU on that subsample against the oracle's (90th percentile within 10x).
+    Returns the oracle's drifts."""
     from oracle.oracle import Oracle
 
     import bench
@@ -52,6 +53,7 @@ def _oracle_sample(mech, T0, P0, Y0, prob, res, nsample, d_gpu, threads=16):
     assert np.max(np.abs(res["T"][idx] / T_o - 1)) < 1e-4
     d_o = _drift(mech, Y0[idx], np.asarray(Yo))
     assert np.percentile(d_gpu[idx], 90) <= 10.0 * np.percentile(d_o, 90) + 1e-11
+    return d_o
 
 
 def _run(dm, T0, P0, Y0, prob):
@@ -94,7 +96,7 @@ def test_configs3_full_sweep(tables, mech):
     res = _run(dm, T0, P0, Y0, prob)
     assert np.all(res["stats"][:, 6] == 0)
     assert np.all(res["tau"] > 0) and np.all(res["tau"] < 1.0)
-    d = _conservation(mech, Y0, res["Y"], tol=3e-7)
+    d = _conservation(mech, Y0, res["Y"])
     conp, conv = prob == 1, prob == 2
     # CONP keeps P, CONV keeps V (V0 = 1) and raises P with the temperature
     assert np.allclose(res["P"][conp], P0[conp], rtol=1e-12)
@@ -120,19 +122,14 @@ def test_configs4_sample(big_mech):
     assert np.all(res["stats"][:, 6] == 0)
     assert np.all(res["tau"] > 0) and np.all(res["tau"] < 1.0)
     assert np.all(res["T"] > T0 + 300.0)
-    d = _conservation(big_mech, Y0, res["Y"], tol=1e-6)
-    _oracle_sample(big_mech, T0, P0, Y0, prob, res, 64, d)
-    # the worst drift of the 32,768 reactors (3e-7 in round 3, 4.9e-7 after round 4's reaction-strip order):
-    # a chaotic tail.  The bar is the oracle's own envelope for that reactor: its drift under a +-1 %
-    # perturbation of rtol (9 runs), 3x its worst
-    from oracle.oracle import Oracle
-
-    w = int(np.argmax(d))
-    orc = Oracle(big_mech)
-    env = []
-    for f in np.linspace(0.99, 1.01, 9):
-        r, Ye = orc.reactor(T0[w], P0[w], 1.0, Y0[w], problem=int(prob[w]), **dict(bench.RUN, rtol=bench.RUN["rtol"] * f))
-        assert r.status == 0
-        env.append(_drift(big_mech, Y0[w:w + 1], Ye[None])[0])
-    print(f"configs[4] sample: worst drift {d[w]:.3e} (reactor {w}); oracle envelope {min(env):.3e} .. {max(env):.3e}")
-    assert d[w] <= 3.0 * max(env) + 1e-9
+    d = _conservation(big_mech, Y0, res["Y"])
+    # the drift distribution of all 32,768 against the oracle's on a 1,024-reactor strided subsample of the
+    # same sweep: 99th / 99.9th percentile and maximum within 2x (round-5 verdict item 1; the round-5
+    # single-reactor envelope bar broke on legitimate summation-order changes of the Jacobian)
+    d_o = _oracle_sample(big_mech, T0, P0, Y0, prob, res, 1024, d)
+    q_g = [np.percentile(d, 99), np.percentile(d, 99.9), d.max()]
+    q_o = [np.percentile(d_o, 99), np.percentile(d_o, 99.9), d_o.max()]
+    print("configs[4] sample drift p99 / p99.9 / max: GPU", ["%.3e" % x for x in q_g], "oracle",
+          ["%.3e" % x for x in q_o])
+    assert all(g <= 2.0 * o + 1e-12 for g, o in zip(q_g, q_o))
+    assert d.max() <= 2.0 * np.percentile(d_o, 99.9) + 1e-12
