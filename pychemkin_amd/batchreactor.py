@@ -376,7 +376,7 @@ class BatchReactors(ReactorModel):
             raise ReactorError("missing required input keywords")
         L = kin.bind()
         mix = self.reactormixture
-        cs = ct.c_int(kin.register(self._chem.mechanism()))
+        cs = ct.c_int(kin.register(self._chem.mechanism))
         try:
             zero = np.zeros(1, np.int32)
             rc = L.KINAll0D_Setup(ct.byref(cs), ct.byref(ct.c_int(self._reactortype)), ct.byref(ct.c_int(self._problemtype)),

@@ -10,6 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "ckmi.hip")        # kinetics, thermo and reactor kernels + C ABI
 LU_SRC = os.path.join(HERE, "csrc", "ckmi_lu.hip")  # batched MFMA LU (large mechanisms)
 BIG_SRC = os.path.join(HERE, "csrc", "ckmi_big.hip")  # workgroup-per-reactor integrator (64 <= KK + 1 <= 192)
+BIG_HDR = os.path.join(HERE, "csrc", "ckmi_big_matrix.hpp")  # its register-resident Newton matrix forms
 KIN_SRC = os.path.join(HERE, "csrc", "ckmi_kin.cpp")  # KIN-compatible host shims (include/ckmi_kin.h)
 JIT_SRC = os.path.join(HERE, "csrc", "ckmi_jit.cpp")  # mechanism-specialised ROP kernel generator (hipRTC)
 PARSE_SRC = os.path.join(HERE, "csrc", "ckmi_parse.cpp")  # native Chemkin-II interpreter (KINPreProcess)
@@ -81,7 +82,7 @@ def build(force: bool = False, verbose: bool = False, prof: bool = False, out: s
     big_extra = [f for f in extra if "CKMI_BIG" in f]
     big_tag = "prof" if prof else ("main" if not big_extra else "v_" + os.path.splitext(os.path.basename(out))[0])
     big_obj = os.path.join(OBJ_DIR, "ckmi_big.o" if default else f"ckmi_big_{big_tag}.o")
-    if force or big_extra or _stale(big_obj, [BIG_SRC] + DEPS):
+    if force or big_extra or _stale(big_obj, [BIG_SRC, BIG_HDR] + DEPS):
         jobs.append((BIG_SRC, big_obj, BIG_FLAGS + (["-DCKMI_PHASE_TIMERS"] if prof else []) + big_extra))
     kin_obj = os.path.join(OBJ_DIR, "ckmi_kin.o")
     if force or _stale(kin_obj, [KIN_SRC] + DEPS):

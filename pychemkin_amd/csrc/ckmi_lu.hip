@@ -36,11 +36,6 @@ constexpr int WAVE = 64;
 constexpr int LU_WAVES = 8;  // waves per workgroup (one matrix per workgroup)
 constexpr int TB = 16;       // tile edge = the 16x16x4 MFMA shape
 constexpr int LU_NB_MAX = CKMI_LU_NMAX / TB;
-#ifdef CKMI_LU_EXPT_NOSWAP  // timing experiment only (wrong factors): skip the row interchanges
-constexpr bool LU_EXPT_NOSWAP = true;
-#else
-constexpr bool LU_EXPT_NOSWAP = false;
-#endif
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -107,13 +102,7 @@ struct LuSmem {
   int sslot[NP], dslot[NP]; // per row: the slot q < 32 it is the source / destination of, or -1
   int piv[TB];
   int info;
-#if !defined(CKMI_LU_PANEL_LDS) && !defined(CKMI_LU_LOOKAHEAD)
   double TS[((NB * NB + LU_WAVES - 1) / LU_WAVES) * 4 * WAVE];  // wave 0's tiles, parked during the panel
-#endif
-#ifdef CKMI_LU_LOOKAHEAD
-  double P2[NP * PLD];  // the next panel (look-ahead), alternating with P
-  double SB[TB];        // the pivot row of a panel step
-#endif
 };
 
 // L11^-1 (unit lower) by forward substitution on the identity, right-looking over columns m of
@@ -150,111 +139,6 @@ __device__ __forceinline__ void l11_inverse(LuSmem<NB>& S, const double* Pp, int
   for (int k = 0; k < 4; ++k) S.Linv[i * PLD + g + 4 * k] = x[k];
 }
 
-// Step 2 tail: L11^-1 and the net row permutation of the panel's interchanges (wave 0).
-template <int NB>
-__device__ __forceinline__ void panel_finish(LuSmem<NB>& S, int K, int lane LU_PHP) {
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD;
-  const int r0 = K * TB;
-  l11_inverse<NB>(S, S.P, r0, lane);
-  LU_PH(9);
-  // Net row permutation of the 16 interchanges.  Lanes 0..15 track rows r0 + l, lanes 16..31 the
-  // pivot rows; each lane's `val` is the original row whose content its row holds now.
-  const int key = lane < TB ? r0 + lane : (lane < 2 * TB ? S.piv[lane - TB] : -1);
-  int val = key;
-#pragma unroll
-  for (int c = 0; c < TB; ++c) {
-    const int a = r0 + c, b = S.piv[c];
-    if (a != b) {
-      const uint64_t ma = __ballot(key == a), mb = __ballot(key == b);
-      const int va = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)ma) - 1);
-      const int vb = __builtin_amdgcn_readlane(val, __ffsll((unsigned long long)mb) - 1);
-      if (key == a) val = vb;
-      if (key == b) val = va;
-    }
-  }
-  // keep the first lane of each key whose row actually changed; slot = lane
-  bool rep = key >= 0 && val != key;
-#pragma unroll
-  for (int j = 0; j < 2 * TB; ++j) {
-    const int kj = __builtin_amdgcn_readlane(key, j);
-    if (j < lane && kj == key) rep = false;
-  }
-  // row -> slot tables: every tile lane then finds its rows' slots with independent LDS reads
-  // (no serial walk over the slots)
-  for (int i = lane; i < NP; i += WAVE) {
-    S.sslot[i] = -1;
-    S.dslot[i] = -1;
-  }
-  wave_lds_sync();
-  if (rep) {
-    S.sslot[val] = lane;
-    S.dslot[key] = lane;
-  }
-  LU_PH(10);
-}
-
-// Step 2: wave 0 factors panel K in LDS.  Rows K*16 .. NP-1, columns 0..15 of S.P.
-template <int NB>
-__device__ __forceinline__ void panel_factor(LuSmem<NB>& S, int K, int lane, int n LU_PHP) {
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
-  const int r0 = K * TB;
-#pragma unroll
-  for (int c = 0; c < TB; ++c) {
-    const int col = r0 + c;
-    // pivot: first row of maximal |a| among rows >= col (idamax; exact FP64 comparison)
-    double best = -1.0;
-    int bq = 0;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int r = r0 + lane + WAVE * q;
-      if (r >= col && r < NP) {
-        const double v = fabs(S.P[r * PLD + c]);
-        if (v > best) {
-          best = v;
-          bq = q;
-        }
-      }
-    }
-    const double maxv = wave_max(best);
-    // the smallest row among the maxima: lowest q level first (rows r0 + l + 64 q), then lowest lane
-    int p = col;
-#pragma unroll
-    for (int q = NQ - 1; q >= 0; --q) {
-      const uint64_t mq = __ballot(best == maxv && bq == q);
-      if (mq) p = r0 + (int)__ffsll((unsigned long long)mq) - 1 + WAVE * q;
-    }
-    p = __builtin_amdgcn_readfirstlane(p);
-    if (lane == 0) S.piv[c] = p;
-    if (maxv != 0.0) {
-      if (p != col && lane < TB) {
-        const double a = S.P[col * PLD + lane], b = S.P[p * PLD + lane];
-        S.P[col * PLD + lane] = b;
-        S.P[p * PLD + lane] = a;
-      }
-      wave_lds_sync();
-      double prow[TB];
-#pragma unroll
-      for (int cc = c; cc < TB; ++cc) prow[cc] = S.P[col * PLD + cc];
-      const double rp = 1.0 / prow[c];
-#pragma unroll 1  // a full unroll spills (wave 0 also holds its 16 tiles): 41 VGPRs measured
-      for (int q = 0; q < NQ; ++q) {
-        const int r = r0 + lane + WAVE * q;
-        if (r > col && r < NP) {
-          double* row = &S.P[r * PLD];
-          const double l = row[c] * rp;
-          row[c] = l;
-#pragma unroll
-          for (int cc = c + 1; cc < TB; ++cc) row[cc] = fma(-l, prow[cc], row[cc]);
-        }
-      }
-    } else if (lane == 0 && S.info == 0 && col < n) {
-      S.info = col + 1;  // LAPACK: U(col, col) is exactly zero
-    }
-    wave_lds_sync();
-  }
-  panel_finish<NB>(S, K, lane LU_PHA);
-}
-
 // exact int min over the wave
 __device__ __forceinline__ int wave_min_i32(int v) {
   v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));
@@ -272,7 +156,7 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 // step is a max reduction, a position swap, one broadcast of the pivot row through LDS and the
 // rank-1 update in registers; the rows go back to S.P at their final positions.  Wave 0 parks
 // its own matrix tiles in LDS around the call (kernel register budget: 2 waves per SIMD).
-// Same arithmetic, pivots (first position of maximal |a|) and factors as panel_factor.
+// Pivots: the first position of maximal |a| (LAPACK dgetf2 / idamax).
 template <int NB>
 __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, double* sb, int K, int lane, int n LU_PHP) {
   constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
@@ -438,9 +322,6 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       __syncthreads();
       LU_PH(1);
       // 2. factor the panel
-#ifdef CKMI_LU_PANEL_LDS
-      if (w == 0) panel_factor<NB>(S, K, lane, n LU_PHA);
-#else
       if (w == 0) {
         // park the tiles: the panel's 48 doubles per lane take their registers meanwhile
 #pragma unroll
@@ -453,13 +334,11 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
 #pragma unroll
           for (int r = 0; r < 4; ++r) t[s][r] = S.TS[(4 * s + r) * WAVE + lane];
       }
-#endif
       __syncthreads();
       LU_PH(2);
       // 3. row interchanges in the other block columns (sources out), factored panel back in.
       // The slot numbers of all of this wave's rows are loaded first, unconditionally (straight-line
       // LDS reads, one wait), so the lane-masked moves below do not wait on one lookup at a time.
-#ifndef CKMI_LU_XCHG_SERIAL
       {
         int qs[NT][4];
 #pragma unroll
@@ -473,7 +352,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         for (int s = 0; s < NT; ++s) {
           const int ti = w + LU_WAVES * s;
           const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
+          if (ti < NB * NB && J != K && I >= K) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qs[s][r] >= 0) S.X[qs[s][r] * NP + J * TB + lc] = t[s][r];
@@ -494,43 +373,13 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         for (int s = 0; s < NT; ++s) {
           const int ti = w + LU_WAVES * s;
           const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
+          if (ti < NB * NB && J != K && I >= K) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qs[s][r] >= 0) t[s][r] = S.X[qs[s][r] * NP + J * TB + lc];
           }
         }
       }
-#else
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + LU_WAVES * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = S.sslot[I * TB + lg + 4 * r];
-            if (q >= 0) S.X[q * NP + J * TB + lc] = t[s][r];
-          }
-        } else if (ti < NB * NB && J == K && I >= K) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) t[s][r] = S.P[(I * TB + lg + 4 * r) * PLD + lc];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + LU_WAVES * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J != K && I >= K && !LU_EXPT_NOSWAP) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int q = S.dslot[I * TB + lg + 4 * r];
-            if (q >= 0) t[s][r] = S.X[q * NP + J * TB + lc];
-          }
-        }
-      }
-#endif
       __syncthreads();
       LU_PH(3);
       // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (X reused as [16][NP])
@@ -590,188 +439,6 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
 #endif
 }
 
-#ifdef CKMI_LU_LOOKAHEAD
-// Look-ahead form: wave 0 owns no tiles and only factors panels; waves 1..7 own the 121 tiles
-// (tile ti = (w - 1) + 7 s).  Per panel K, with panel K already factored into P[K & 1]:
-//   (a) interchanges of panel K on the tile rows (and the panel column's tiles read back);
-//   (b) U12 = L11^-1 A12 on block row K;
-//   (c) the trailing update of block column K + 1 only, whose tiles then go to P[(K + 1) & 1];
-//   (d) wave 0 factors panel K + 1 while waves 1..7 finish the trailing update of columns > K + 1.
-// So the panel of step K + 1 (wave 0, one SIMD) overlaps the MFMA update of step K instead of
-// following it.  Same arithmetic per element as lu_factor_kernel: bitwise the same factors.
-template <int NB>
-__global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel_la(int nsys, int n, double* __restrict__ A,
-                                                                      int* __restrict__ ipiv, int* __restrict__ info) {
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, TW = LU_WAVES - 1, NT = (NB * NB + TW - 1) / TW;
-  __shared__ LuSmem<NB> S;
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int w0 = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const int lc0 = lane & 15, lg0 = lane >> 4;
-#ifdef CKMI_LU_PHASE
-  unsigned long long ph_[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t1_ = __builtin_amdgcn_s_memtime();
-#endif
-  for (int sys = blockIdx.x; sys < nsys; sys += gridDim.x) {
-    double* As = A + (size_t)sys * n * n;
-    d4 t[NT];
-    {
-      int w = w0, lc = lc0, lg = lg0, nl = n;
-      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg), "+s"(nl));
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w - 1 + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        const int col = J * TB + lc;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = I * TB + lg + 4 * r;
-          double v = row == col ? 1.0 : 0.0;
-          if (w > 0 && ti < NB * NB && row < nl && col < nl) v = As[(size_t)row * nl + col];
-          t[s][r] = v;
-        }
-      }
-      // panel 0 to P
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w - 1 + TW * s;
-        if (w > 0 && ti < NB * NB && ti % NB == 0) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) S.P[((ti / NB) * TB + lg + 4 * r) * PLD + lc] = t[s][r];
-        }
-      }
-    }
-    if (threadIdx.x == 0) S.info = 0;
-    __syncthreads();
-    if (w0 == 0) {
-      panel_factor_reg<NB>(S, S.P, S.SB, 0, lane, n LU_PHA);
-#pragma unroll
-      for (int s = 0; s < NT; ++s) t[s] = d4{0.0, 0.0, 0.0, 0.0};  // wave 0 holds no tiles
-    }
-    __syncthreads();
-    LU_PH(0);
-    for (int K = 0; K < NB; ++K) {
-      int w = w0, lc = lc0, lg = lg0;
-      asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg));
-      double* Pc = (K & 1) ? S.P2 : S.P;
-      double* Pn = (K & 1) ? S.P : S.P2;
-      // (a) interchanges of panel K; the panel column's tiles take their factored values
-      if (w > 0) {
-#pragma unroll
-        for (int s = 0; s < NT; ++s) {
-          const int ti = w - 1 + TW * s;
-          const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && J != K && I >= K) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int q = S.sslot[I * TB + lg + 4 * r];
-              if (q >= 0) S.X[q * NP + J * TB + lc] = t[s][r];
-            }
-          } else if (ti < NB * NB && J == K && I >= K) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) t[s][r] = Pc[(I * TB + lg + 4 * r) * PLD + lc];
-          }
-        }
-      }
-      __syncthreads();
-      if (w > 0) {
-#pragma unroll
-        for (int s = 0; s < NT; ++s) {
-          const int ti = w - 1 + TW * s;
-          const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && J != K && I >= K) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int q = S.dslot[I * TB + lg + 4 * r];
-              if (q >= 0) t[s][r] = S.X[q * NP + J * TB + lc];
-            }
-          }
-        }
-      }
-      __syncthreads();
-      LU_PH(3);
-      // (b) U12 = L11^-1 A12 on block row K, to X as [16][NP]
-      if (w > 0) {
-#pragma unroll
-        for (int s = 0; s < NT; ++s) {
-          const int ti = w - 1 + TW * s;
-          const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && I == K && J > K) {
-            d4 u = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) u = mfma16(S.Linv[lc * PLD + 4 * kk + lg], t[s][kk], u);
-            t[s] = u;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) S.X[(lg + 4 * r) * NP + J * TB + lc] = u[r];
-          }
-        }
-      }
-      __syncthreads();
-      LU_PH(4);
-      // (c) block column K + 1: trailing update, then the next panel's tiles to Pn
-      if (w > 0 && K + 1 < NB) {
-#pragma unroll
-        for (int s = 0; s < NT; ++s) {
-          const int ti = w - 1 + TW * s;
-          const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && I > K && J == K + 1) {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-              t[s] = mfma16(-Pc[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) Pn[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
-          }
-        }
-      }
-      __syncthreads();
-      LU_PH(1);
-      // (d) wave 0: pivots of K out, then panel K + 1; waves 1..7: the rest of the trailing update
-      if (w == 0) {
-        if (lane < TB && K * TB + lane < n) ipiv[(size_t)sys * n + K * TB + lane] = S.piv[lane];
-        if (K + 1 < NB) panel_factor_reg<NB>(S, Pn, S.SB, K + 1, lane, n LU_PHA);
-#pragma unroll
-        for (int s = 0; s < NT; ++s) t[s] = d4{0.0, 0.0, 0.0, 0.0};  // wave 0 holds no tiles
-      } else {
-#pragma unroll
-        for (int s = 0; s < NT; ++s) {
-          const int ti = w - 1 + TW * s;
-          const int I = ti / NB, J = ti % NB;
-          if (ti < NB * NB && I > K && J > K + 1) {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-              t[s] = mfma16(-Pc[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
-          }
-        }
-      }
-      LU_PH(2);
-      __syncthreads();
-      LU_PH(5);
-    }
-    int n_st = n, lc_st = lc0, lg = lg0, w = w0;
-    double* Ast = As;
-    asm volatile("" : "+s"(n_st), "+v"(lc_st), "+s"(Ast), "+v"(lg), "+s"(w));
-    if (w > 0) {
-#pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w - 1 + TW * s;
-        const int I = ti / NB, J = ti % NB;
-        const int col = J * TB + lc_st;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = I * TB + lg + 4 * r;
-          if (ti < NB * NB && row < n_st && col < n_st) Ast[(size_t)row * n_st + col] = t[s][r];
-        }
-      }
-    }
-    if (threadIdx.x == 0) info[sys] = S.info;
-    __syncthreads();
-    LU_PH(6);
-  }
-#ifdef CKMI_LU_PHASE
-  if (threadIdx.x == 0)
-    for (int k = 0; k < 12; ++k) atomicAdd(&g_lu_phase[k], ph_[k]);
-#endif
-}
-#endif
-
 // One wave per right-hand side: x = U^-1 L^-1 P b, in place in B[sys][n].
 constexpr int SOLVE_WAVES = 4;
 __global__ __launch_bounds__(SOLVE_WAVES* WAVE) void lu_solve_kernel(int nsys, int n, const double* __restrict__ LU,
@@ -818,11 +485,7 @@ thread_local std::string g_lu_err;
 template <int NB>
 hipError_t launch_factor(int nsys, int n, double* A, int* ipiv, int* info, hipStream_t st) {
   const int grid = nsys < 8192 ? nsys : 8192;
-#ifdef CKMI_LU_LOOKAHEAD
-  hipLaunchKernelGGL(lu_factor_kernel_la<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
-#else
   hipLaunchKernelGGL(lu_factor_kernel<NB>, dim3(grid), dim3(LU_WAVES * WAVE), 0, st, nsys, n, A, ipiv, info);
-#endif
   return hipGetLastError();
 }
 

@@ -505,7 +505,9 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
 // C y = eb0 in the mole-weighted norm (w_k = Y_k W_k: every species moves by a relative amount of the drift's
 // size), with a ridge PROJ_RIDGE on the Gram matrix.  The element counts are
 // the image's u64 table after e2t (byte e: element e of the mechanism's npe); the residual is one fused
-// 8-value reduction per accepted step, the Gram matrix (rare: only on a step past the threshold) batches
+// 8-value reduction per accepted step (checking only every 4th step was measured and rejected: the BDF error
+// estimate then sees the 4-step correction as a periodic perturbation and the step counts blow up; oracle
+// ckoracle.c PROJ_EVERY), the Gram matrix (rare: only on a step past the threshold) batches
 // of 8 packed pairs.
 constexpr int PROJ_MMAX = CKMI_PROJ_MMAX;
 constexpr double PROJ_RIDGE = 1e-8, PROJ_TOL = 0.1;

@@ -15,6 +15,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+os.environ.setdefault("CKMI_LIB", os.path.join(ROOT, "pychemkin_amd", "_lib", "libckmi_prof.so"))
 import torch  # noqa: E402
 
 import bench  # noqa: E402

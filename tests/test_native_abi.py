@@ -109,7 +109,8 @@ def test_workgroup_kernel_image_capacity():
     """The workgroup-per-reactor kernel reserves LDS only for the factorisation form it is compiled with
     (round-5 advice: the look-ahead form's reserve had cut the largest accepted mechanism image by ~11 KB).
     Host-only query of the layout (ckmi_big.hip big_layout): at NB = 11 (MFMA panels) the xpart region holds
-    2 panel buffers + per-wave pivot rows + diagonal-block rows (39,424 B at NC = 176), at NB = 12 (VALU
+    2 panel buffers + per-wave pivot rows + diagonal-block rows (42,496 B at NC = 176: the diagonal blocks'
+    q-block stride padded to 8 mod 32 doubles for conflict-free A-operand reads), at NB = 12 (VALU
     columns) the solve's partial sums (24,576 B) plus the pivot-row / column buffers (4,608 B)."""
     from pychemkin_amd import _native
 
@@ -118,7 +119,7 @@ def test_workgroup_kernel_image_capacity():
     nb11 = f(162, 192, 12, lds)   # the 161-species configs[4] stand-in
     nb12 = f(177, 192, 12, lds)
     assert nb11 >= 80_000 and nb11 % 16 == 0
-    assert nb12 - nb11 == (39_424 - 24_576) - 4_608
+    assert nb12 - nb11 == (42_496 - 24_576) - 4_608
     assert f(176, 192, 12, lds) == nb11 and f(192, 192, 12, lds) == nb12
     assert f(193, 256, 12, lds) == -1 and f(162, 192, 12, 64 * 1024) == -1
     assert f(54, 64, 11, lds) > nb11  # GRI-3.0 forced onto the workgroup kernel (ckmi_set_reactor_path(1))
