@@ -527,7 +527,7 @@ def c1_line(args):
     stats = r.solver_statistics
     from oracle.oracle import Oracle  # noqa: E402  (cpu_baseline leg only)
 
-    orc = Oracle(chem.mechanism())
+    orc = Oracle(chem.mechanism)
     cl = []
     for _ in range(3):
         t0 = time.perf_counter()

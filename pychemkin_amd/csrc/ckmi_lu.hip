@@ -92,14 +92,26 @@ __device__ __forceinline__ double wave_max(double v) {
   return fmax(fmax(bcast(v, 0), bcast(v, 16)), fmax(bcast(v, 32), bcast(v, 48)));
 }
 
+// row -> index of the slot tables: the 4 rows lg + 4 r (r = 0..3) of a tile lane are consecutive
+__device__ __forceinline__ int slot_idx(int row) { return (row & ~15) + ((row & 3) << 2) + ((row >> 2) & 3); }
+
 template <int NB>
 struct LuSmem {
   static constexpr int NP = NB * TB;
   static constexpr int PLD = TB + 1;  // odd row stride: lanes on different rows hit different banks
-  double P[NP * PLD];                 // panel block column, indexed by global row
-  double X[32 * NP];                  // row-exchange buffer, then the U12 block row [16][NP]
+  // two panel buffers (by panel parity) and a U12 buffer of its own when the LDS holds them (NB <= 11): two
+  // workgroup barriers fewer per panel (the U12 step no longer overwrites the exchange buffer, and the next
+  // panel's tiles go to the other buffer while slower waves still read this one)
+  static constexpr bool FEW = 8 * (2 * NP * PLD + 48 * NP + TB * PLD + ((NB * NB + LU_WAVES - 1) / LU_WAVES) * 4 * WAVE) +
+                                  8 * NP + 4 * TB + 4 <= 160 * 1024;
+  double P[FEW ? 2 : 1][NP * PLD];    // panel block column, indexed by global row (by panel parity)
+  double X[32 * NP];                  // row-exchange buffer (and the U12 block row [16][NP] without U)
+  double U[FEW ? 16 * NP : 1];        // the U12 block row
   double Linv[TB * PLD];
-  int sslot[NP], dslot[NP]; // per row: the slot q < 32 it is the source / destination of, or -1
+  // per row: the slot q < 32 it is the source / destination of, or -1; stored by slot_idx so that a tile
+  // lane's 4 rows (lg + 4 r, r = 0..3) are 4 consecutive ints (one 16-byte LDS read)
+  alignas(16) int sslot[NP];
+  alignas(16) int dslot[NP];
   int piv[TB];
   int info;
   double TS[((NB * NB + LU_WAVES - 1) / LU_WAVES) * 4 * WAVE];  // wave 0's tiles, parked during the panel
@@ -153,13 +165,15 @@ __device__ __forceinline__ int wave_min_i32(int v) {
 // (lane l: rows r0 + l + 64 q at the start).  Rows are never moved: each carries its current
 // position pos (LAPACK's row index after the interchanges so far), an interchange swaps two
 // positions, and a row is finished once its position is below the current column.  So a pivot
-// step is a max reduction, a position swap, one broadcast of the pivot row through LDS and the
+// step is a max reduction, a position swap, the pivot row broadcast by readlane and the
 // rank-1 update in registers; the rows go back to S.P at their final positions.  Wave 0 parks
 // its own matrix tiles in LDS around the call (kernel register budget: 2 waves per SIMD).
-// Pivots: the first position of maximal |a| (LAPACK dgetf2 / idamax).
-template <int NB>
-__device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, double* sb, int K, int lane, int n LU_PHP) {
-  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD, NQ = (NP + WAVE - 1) / WAVE;
+// Pivots: the first position of maximal |a| (LAPACK dgetf2 / idamax).  NQ: row levels of 64 the panel
+// still has (NP - 16 K rows), a template parameter so that the late panels carry 2 or 1 levels instead
+// of 3 through every column step (panel_factor_lv).
+template <int NB, int NQ>
+__device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, int K, int lane, int n LU_PHP) {
+  constexpr int NP = NB * TB, PLD = LuSmem<NB>::PLD;
   constexpr int NOPOS = 1 << 30;
   const int r0 = K * TB;
   double x[NQ][TB];
@@ -172,6 +186,7 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, doub
     for (int c = 0; c < TB; ++c) x[q][c] = r < NP ? Pp[r * PLD + c] : 0.0;
   }
   LU_PH(7);
+  int zinfo = 0;  // first exactly-zero pivot column + 1 of this panel
 #pragma unroll
   for (int c = 0; c < TB; ++c) {
     const int col = r0 + c;
@@ -187,7 +202,11 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, doub
       bval = take ? x[q][c] : bval;
       bpos = take ? pos[q] : bpos;
     }
-    const double rb = 1.0 / bval;
+    // 1 / bval from the hardware reciprocal and two Newton steps (the IEEE division sequence is ~3x the
+    // instructions; the multipliers came out bitwise the same on the A/B matrices)
+    double rb = __builtin_amdgcn_rcp(bval);
+    rb = fma(rb, fma(-bval, rb, 1.0), rb);
+    rb = fma(rb, fma(-bval, rb, 1.0), rb);
     const double maxv = wave_max(best);
     uint64_t cand = __ballot(best == maxv);
     int p = __builtin_amdgcn_readlane(bpos, (int)__ffsll((unsigned long long)cand) - 1);
@@ -197,43 +216,45 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, doub
     }
     p = __builtin_amdgcn_readfirstlane(p);
     if (lane == 0) S.piv[c] = p;
-    if (maxv != 0.0) {
-      const double rp = bcast(rb, (int)__ffsll((unsigned long long)cand) - 1);
-      // the pivot row (position p) to LDS; then it takes position col and the row at col takes p.
-      // No wave barrier around sb: one wave's LDS operations execute in issue order, so the
-      // reads below see this store and the next column's store follows these reads.  The empty
-      // asm with a memory clobber keeps the compiler from hoisting the reads above the store
-      // (per thread, a load after a conditional store may legally become load + select).
+    // the pivot row (position p) straight from its lane's registers: its level (wave-uniform after a
+    // readlane) picks the register row by a scalar branch, its entries come over by readlane (no LDS
+    // round trip); then it takes position col and the row at col takes p
+    const int pl = (int)__ffsll((unsigned long long)cand) - 1;
+    double prow[TB];
+    {
+      int myq = 0;
+#pragma unroll
+      for (int q = 1; q < NQ; ++q) myq = pos[q] == p ? q : myq;
+      const int pq = __builtin_amdgcn_readlane(myq, pl);
+#pragma unroll
+      for (int cc = 0; cc < TB; ++cc) prow[cc] = 0.0;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
-        if (pos[q] == p) {
+        if (pq == q) {
 #pragma unroll
           for (int cc = 0; cc < TB; ++cc)
-            if (cc > c) sb[cc] = x[q][cc];
+            if (cc > c) prow[cc] = bcast(x[q][cc], pl);
         }
       }
-      asm volatile("" ::: "memory");
+    }
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) pos[q] = pos[q] == p ? col : (pos[q] == col ? p : pos[q]);
-      double prow[TB];
+    for (int q = 0; q < NQ; ++q) pos[q] = pos[q] == p ? col : (pos[q] == col ? p : pos[q]);
+    // branch-free: a zero pivot column (maxv == 0, LAPACK info) multiplies by 0, rows that are not below
+    // the pivot get l = 0 (x + (-0) p = x); no basic-block boundary between this column's update and the
+    // next column's pivot search
+    const double rp = maxv != 0.0 ? bcast(rb, pl) : 0.0;
+    zinfo = (maxv == 0.0 && zinfo == 0 && col < n) ? col + 1 : zinfo;
 #pragma unroll
-      for (int cc = 0; cc < TB; ++cc) prow[cc] = cc > c ? sb[cc] : 0.0;
+    for (int q = 0; q < NQ; ++q) {
+      const bool upd = pos[q] > col;
+      const double l = upd ? x[q][c] * rp : 0.0;
+      x[q][c] = upd ? l : x[q][c];
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        if (pos[q] > col) {
-          const double l = x[q][c] * rp;
-          x[q][c] = l;
-#pragma unroll
-          for (int cc = 0; cc < TB; ++cc)  // (a constant trip count: unrolled before the c loop is)
-            if (cc > c) x[q][cc] = fma(-l, prow[cc], x[q][cc]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) pos[q] = pos[q] == p ? col : (pos[q] == col ? p : pos[q]);
-      if (lane == 0 && S.info == 0 && col < n) S.info = col + 1;  // LAPACK: U(col, col) is exactly zero
+      for (int cc = 0; cc < TB; ++cc)
+        if (cc > c) x[q][cc] = fma(-l, prow[cc], x[q][cc]);
     }
   }
+  if (lane == 0 && zinfo != 0 && S.info == 0) S.info = zinfo;
   LU_PH(8);
   // rows back to S.P at their final positions; the net permutation is read off the positions:
   // the content of row r0 + l + 64 q moved to pos[q] (at most 32 rows move), slots by prefix count
@@ -256,8 +277,8 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, doub
     const uint64_t m = __ballot(moved);
     const int sl = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     if (moved) {  // (after the -1 fill: same wave, LDS order)
-      S.sslot[r] = sl;
-      S.dslot[pos[q]] = sl;
+      S.sslot[slot_idx(r)] = sl;
+      S.dslot[slot_idx(pos[q])] = sl;
     }
     base += __builtin_popcountll(m);
   }
@@ -265,6 +286,19 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, doub
   LU_PH(10);
   l11_inverse<NB>(S, Pp, r0, lane);
   LU_PH(9);
+}
+
+// panel K with the fewest row levels that hold its NP - 16 K rows (wave-uniform choice)
+template <int NB, int NQ>
+__device__ __forceinline__ void panel_factor_lv(LuSmem<NB>& S, double* Pp, int K, int lane, int n LU_PHP) {
+  constexpr int NP = NB * TB;
+  if constexpr (NQ > 1) {
+    if (NP - K * TB <= (NQ - 1) * WAVE) {
+      panel_factor_lv<NB, NQ - 1>(S, Pp, K, lane, n LU_PHA);
+      return;
+    }
+  }
+  panel_factor_reg<NB, NQ>(S, Pp, K, lane, n LU_PHA);
 }
 
 template <int NB>
@@ -309,6 +343,9 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       // out of the K loop and held in registers for the whole factorisation
       int w = w0, lc = lc0, lg = lg0;
       asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg));
+      constexpr bool FEW = LuSmem<NB>::FEW;
+      double* Pk = S.P[FEW ? (K & 1) : 0];
+      double* Ub = FEW ? S.U : S.X;
       // 1. panel tiles (I >= K, K) to LDS
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
@@ -316,7 +353,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         const int I = ti / NB, J = ti % NB;
         if (ti < NB * NB && J == K && I >= K) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) S.P[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+          for (int r = 0; r < 4; ++r) Pk[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
         }
       }
       __syncthreads();
@@ -328,7 +365,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         for (int s = 0; s < NT; ++s)
 #pragma unroll
           for (int r = 0; r < 4; ++r) S.TS[(4 * s + r) * WAVE + lane] = t[s][r];
-        panel_factor_reg<NB>(S, S.P, S.X, K, lane, n LU_PHA);
+        panel_factor_lv<NB, (NB * TB + WAVE - 1) / WAVE>(S, Pk, K, lane, n LU_PHA);
 #pragma unroll
         for (int s = 0; s < NT; ++s)
 #pragma unroll
@@ -345,8 +382,13 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         for (int s = 0; s < NT; ++s) {
           const int ti = w + LU_WAVES * s;
           const int I = min(ti / NB, NB - 1);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) qs[s][r] = S.sslot[I * TB + lg + 4 * r];
+          {
+            const int4 v = *reinterpret_cast<const int4*>(&S.sslot[I * TB + (lg << 2)]);  // rows lg + 4 r
+            qs[s][0] = v.x;
+            qs[s][1] = v.y;
+            qs[s][2] = v.z;
+            qs[s][3] = v.w;
+          }
         }
 #pragma unroll
         for (int s = 0; s < NT; ++s) {
@@ -358,7 +400,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
               if (qs[s][r] >= 0) S.X[qs[s][r] * NP + J * TB + lc] = t[s][r];
           } else if (ti < NB * NB && J == K && I >= K) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) t[s][r] = S.P[(I * TB + lg + 4 * r) * PLD + lc];
+            for (int r = 0; r < 4; ++r) t[s][r] = Pk[(I * TB + lg + 4 * r) * PLD + lc];
           }
         }
         __syncthreads();
@@ -366,8 +408,13 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         for (int s = 0; s < NT; ++s) {
           const int ti = w + LU_WAVES * s;
           const int I = min(ti / NB, NB - 1);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) qs[s][r] = S.dslot[I * TB + lg + 4 * r];
+          {
+            const int4 v = *reinterpret_cast<const int4*>(&S.dslot[I * TB + (lg << 2)]);  // rows lg + 4 r
+            qs[s][0] = v.x;
+            qs[s][1] = v.y;
+            qs[s][2] = v.z;
+            qs[s][3] = v.w;
+          }
         }
 #pragma unroll
         for (int s = 0; s < NT; ++s) {
@@ -380,9 +427,9 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           }
         }
       }
-      __syncthreads();
+      if constexpr (!FEW) __syncthreads();  // (with its own U buffer the U12 step does not overwrite X)
       LU_PH(3);
-      // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (X reused as [16][NP])
+      // 4. U12 = L11^-1 A12 on block row K; U12 to LDS (Ub: U, or X reused as [16][NP])
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
         const int ti = w + LU_WAVES * s;
@@ -393,7 +440,7 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           for (int kk = 0; kk < 4; ++kk) u = mfma16(S.Linv[lc * PLD + 4 * kk + lg], t[s][kk], u);
           t[s] = u;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) S.X[(lg + 4 * r) * NP + J * TB + lc] = u[r];
+          for (int r = 0; r < 4; ++r) Ub[(lg + 4 * r) * NP + J * TB + lc] = u[r];
         }
       }
       __syncthreads();
@@ -406,11 +453,13 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
         if (ti < NB * NB && I > K && J > K) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
-            t[s] = mfma16(-S.P[(I * TB + lc) * PLD + 4 * kk + lg], S.X[(4 * kk + lg) * NP + J * TB + lc], t[s]);
+            t[s] = mfma16(-Pk[(I * TB + lc) * PLD + 4 * kk + lg], Ub[(4 * kk + lg) * NP + J * TB + lc], t[s]);
         }
       }
       if (threadIdx.x < TB && K * TB + threadIdx.x < n) ipiv[(size_t)sys * n + K * TB + threadIdx.x] = S.piv[threadIdx.x];
-      __syncthreads();  // P, X and piv are rewritten by the next panel
+      if constexpr (!FEW) __syncthreads();  // P, X and piv are rewritten by the next panel
+      // (FEW: the next panel's tiles go to the other P buffer, and a wave reaches the next panel's X / U
+      // writes only after the next panel's barriers, which every wave passes after this update)
       LU_PH(5);
     }
     // opaque copies: otherwise the 4 NT store addresses are CSE'd with the load addresses and

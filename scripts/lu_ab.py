@@ -40,10 +40,13 @@ if __name__ == "__main__":
         ref = None
         for p in sys.argv[1:]:
             ms, A, ipiv, info = time_lib(p, newton=newton)
-            same = None
+            same = piv_same = maxdiff = None
             if ref is None:
                 ref = (A, ipiv, info)
             else:
                 same = bool(torch.equal(A, ref[0]) and torch.equal(ipiv, ref[1]) and torch.equal(info, ref[2]))
+                piv_same = bool(torch.equal(ipiv, ref[1]))
+                maxdiff = float(((A - ref[0]).abs().max() / ref[0].abs().max()).item())
             print(json.dumps({"lib": p, "matrices": "newton" if newton else "randn", "ms": ms,
-                              "bitwise_equal_to_first": same}), flush=True)
+                              "bitwise_equal_to_first": same, "pivots_equal": piv_same,
+                              "max_rel_diff": maxdiff}), flush=True)
