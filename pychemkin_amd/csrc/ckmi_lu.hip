@@ -395,6 +395,10 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           const int ti = w + LU_WAVES * s;
           const int I = ti / NB, J = ti % NB;
           if (ti < NB * NB && J != K && I >= K) {
+#ifdef CKMI_LU_SKIP
+            // (a tile none of whose rows move is skipped as a wave: one ballot instead of 4 masked stores)
+            if (__ballot((qs[s][0] & qs[s][1] & qs[s][2] & qs[s][3]) >= 0) != 0)  // some row moves (slots are -1 or >= 0)
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qs[s][r] >= 0) S.X[qs[s][r] * NP + J * TB + lc] = t[s][r];
@@ -421,6 +425,9 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           const int ti = w + LU_WAVES * s;
           const int I = ti / NB, J = ti % NB;
           if (ti < NB * NB && J != K && I >= K) {
+#ifdef CKMI_LU_SKIP
+            if (__ballot((qs[s][0] & qs[s][1] & qs[s][2] & qs[s][3]) >= 0) != 0)  // some row moves (slots are -1 or >= 0)
+#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qs[s][r] >= 0) t[s][r] = S.X[qs[s][r] * NP + J * TB + lc];
