@@ -344,21 +344,38 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       int w = w0, lc = lc0, lg = lg0;
       asm volatile("" : "+s"(w), "+v"(lc), "+v"(lg));
       constexpr bool FEW = LuSmem<NB>::FEW;
+      constexpr bool LA = FEW;  // the trailing update split around the next panel (below)
       double* Pk = S.P[FEW ? (K & 1) : 0];
       double* Ub = FEW ? S.U : S.X;
-      // 1. panel tiles (I >= K, K) to LDS
+      // 1. panel tiles (I >= K, K) to LDS (LA: written by the previous panel's update, except for K = 0)
+      if (!LA || K == 0) {
 #pragma unroll
-      for (int s = 0; s < NT; ++s) {
-        const int ti = w + LU_WAVES * s;
-        const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && J == K && I >= K) {
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w + LU_WAVES * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && J == K && I >= K) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) Pk[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+            for (int r = 0; r < 4; ++r) Pk[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+          }
         }
       }
       __syncthreads();
       LU_PH(1);
-      // 2. factor the panel
+      // 2. factor the panel; LA: meanwhile waves 1..7 finish the previous panel's trailing update (the block
+      // columns beyond this panel; its L21 is in the other P buffer, its U12 still in U)
+      if (LA && w != 0 && K > 0) {
+        const double* Pp = S.P[(K - 1) & 1];
+#pragma unroll
+        for (int s = 0; s < NT; ++s) {
+          const int ti = w + LU_WAVES * s;
+          const int I = ti / NB, J = ti % NB;
+          if (ti < NB * NB && I > K - 1 && J > K) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+              t[s] = mfma16(-Pp[(I * TB + lc) * PLD + 4 * kk + lg], Ub[(4 * kk + lg) * NP + J * TB + lc], t[s]);
+          }
+        }
+      }
       if (w == 0) {
         // park the tiles: the panel's 48 doubles per lane take their registers meanwhile
 #pragma unroll
@@ -395,10 +412,6 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           const int ti = w + LU_WAVES * s;
           const int I = ti / NB, J = ti % NB;
           if (ti < NB * NB && J != K && I >= K) {
-#ifdef CKMI_LU_SKIP
-            // (a tile none of whose rows move is skipped as a wave: one ballot instead of 4 masked stores)
-            if (__ballot((qs[s][0] & qs[s][1] & qs[s][2] & qs[s][3]) >= 0) != 0)  // some row moves (slots are -1 or >= 0)
-#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qs[s][r] >= 0) S.X[qs[s][r] * NP + J * TB + lc] = t[s][r];
@@ -425,9 +438,6 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
           const int ti = w + LU_WAVES * s;
           const int I = ti / NB, J = ti % NB;
           if (ti < NB * NB && J != K && I >= K) {
-#ifdef CKMI_LU_SKIP
-            if (__ballot((qs[s][0] & qs[s][1] & qs[s][2] & qs[s][3]) >= 0) != 0)  // some row moves (slots are -1 or >= 0)
-#endif
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (qs[s][r] >= 0) t[s][r] = S.X[qs[s][r] * NP + J * TB + lc];
@@ -452,15 +462,21 @@ __global__ __launch_bounds__(LU_WAVES* WAVE) void lu_factor_kernel(int nsys, int
       }
       __syncthreads();
       LU_PH(4);
-      // 5. trailing update A22 -= L21 U12
+      // 5. trailing update A22 -= L21 U12 (LA: waves 1..7 only the next panel's block column now, whose
+      // tiles then go to the next P buffer; the rest during the next panel)
 #pragma unroll
       for (int s = 0; s < NT; ++s) {
         const int ti = w + LU_WAVES * s;
         const int I = ti / NB, J = ti % NB;
-        if (ti < NB * NB && I > K && J > K) {
+        if (ti < NB * NB && I > K && J > K && (!LA || w == 0 || J == K + 1)) {
 #pragma unroll
           for (int kk = 0; kk < 4; ++kk)
             t[s] = mfma16(-Pk[(I * TB + lc) * PLD + 4 * kk + lg], Ub[(4 * kk + lg) * NP + J * TB + lc], t[s]);
+          if (LA && J == K + 1) {
+            double* Pn = S.P[(K + 1) & 1];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pn[(I * TB + lg + 4 * r) * PLD + lc] = t[s][r];
+          }
         }
       }
       if (threadIdx.x < TB && K * TB + threadIdx.x < n) ipiv[(size_t)sys * n + K * TB + threadIdx.x] = S.piv[threadIdx.x];
