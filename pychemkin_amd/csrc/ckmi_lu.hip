@@ -151,6 +151,7 @@ __device__ __forceinline__ void l11_inverse(LuSmem<NB>& S, const double* Pp, int
   for (int k = 0; k < 4; ++k) S.Linv[i * PLD + g + 4 * k] = x[k];
 }
 
+
 // exact int min over the wave
 __device__ __forceinline__ int wave_min_i32(int v) {
   v = min(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false));
@@ -187,6 +188,7 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, int 
   }
   LU_PH(7);
   int zinfo = 0;  // first exactly-zero pivot column + 1 of this panel
+  int pivr = 0;
 #pragma unroll
   for (int c = 0; c < TB; ++c) {
     const int col = r0 + c;
@@ -215,7 +217,7 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, int 
       cand = __ballot(best == maxv && bpos == p);
     }
     p = __builtin_amdgcn_readfirstlane(p);
-    if (lane == 0) S.piv[c] = p;
+    pivr = lane == c ? p : pivr;  // lane c keeps the pivot of column c (one LDS store per panel)
     // the pivot row (position p) straight from its lane's registers: its level (wave-uniform after a
     // readlane) picks the register row by a scalar branch, its entries come over by readlane (no LDS
     // round trip); then it takes position col and the row at col takes p
@@ -255,6 +257,7 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, int 
     }
   }
   if (lane == 0 && zinfo != 0 && S.info == 0) S.info = zinfo;
+  if (lane < TB) S.piv[lane] = pivr;
   LU_PH(8);
   // rows back to S.P at their final positions; the net permutation is read off the positions:
   // the content of row r0 + l + 64 q moved to pos[q] (at most 32 rows move), slots by prefix count
