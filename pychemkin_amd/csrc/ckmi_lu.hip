@@ -18,6 +18,11 @@
 //        B operand), written to LDS;
 //     5. A22 -= L21 U12: 4 MFMAs per trailing tile, A from the panel in LDS, B from U12 in LDS.
 //
+// With the LDS for two panel buffers and a U12 buffer of its own (NB <= 11, LuSmem::FEW), step 5 is
+// split around the next panel: every wave first updates its tiles of block column K + 1 and writes them
+// straight to the other panel buffer (step 1 of panel K + 1), and waves 1..7 finish the rest of the
+// update while wave 0 factors panel K + 1; four workgroup barriers per panel instead of six.
+//
 // The result has LAPACK dgetrf semantics (A = P L U, unit-lower L below the diagonal, U on and
 // above, row interchanges applied to the whole rows) with 0-based pivot rows.  This is the
 // factorisation inside the reference's closed KINAll0D_Calculate (batchreactor.py:1158) for a
