@@ -835,6 +835,7 @@ static void adjust_order(bdf* b, int deltaq) {
  * never projected: their drift stays far below rtol), which keeps the integrator's results those of the
  * unconstrained BDF (e.g. the sensitivity golden's finite differences). */
 #define PROJ_RIDGE 1e-8
+#define PROJ_TRACE 1e-6
 #ifndef PROJ_TOL
 #define PROJ_TOL 0.1
 #endif
@@ -870,6 +871,10 @@ static int elem_project(bdf* b) {
     bmax = fmax(bmax, b->eb0[m]);
   }
   if (!(rmax > PROJ_TOL * b->rtol * bmax)) return 0;
+  /* trace elements (initial content at most PROJ_TRACE of the largest) are left out: their Gram entries carry
+   * only trace species, and a multiplier from them would rescale those species by orders of magnitude */
+  for (int m = 0; m < M; ++m)
+    if (!(b->eb0[m] > PROJ_TRACE * bmax)) G[m][m] = 0.0;
   /* LDL^T of the ridged Gram matrix (lower triangle), elements without weight dropped */
   double L[CKO_PROJ_MMAX][CKO_PROJ_MMAX], dg[CKO_PROJ_MMAX], z[CKO_PROJ_MMAX], lam[CKO_PROJ_MMAX];
   int live[CKO_PROJ_MMAX];

@@ -239,8 +239,12 @@ __device__ __forceinline__ void elem_project_big(const MechView& V, Blk& B, int 
   }
   if (tid == 0) {
 #pragma unroll
-    for (int e = 0; e < PROJ_MMAX; ++e)
-      if (e < npe) scr[PROJ_SCR_RES + e] = v[e];
+    for (int e = 0; e < PROJ_MMAX; ++e) {
+      if (e < npe) {
+        scr[PROJ_SCR_RES + e] = v[e];
+        if (!(eb0[e] > PROJ_TRACE * bmax)) scr[e * (e + 1) / 2 + e] = 0.0;  // trace element: left out
+      }
+    }
     proj_solve_lds(scr, npe);
   }
   __syncthreads();

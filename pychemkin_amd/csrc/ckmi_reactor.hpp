@@ -511,6 +511,7 @@ __device__ __forceinline__ double reactor_rhs(const MechView& V, const RunCtx& R
 // of 8 packed pairs.
 constexpr int PROJ_MMAX = CKMI_PROJ_MMAX;
 constexpr double PROJ_RIDGE = 1e-8, PROJ_TOL = 0.1;
+constexpr double PROJ_TRACE = 1e-6;  // elements with at most this share of the largest content are left out
 // scratch layout (doubles): packed lower-triangle Gram [0..35] (m (m + 1) / 2 + l), residual [40..47],
 // multipliers [48..55]
 constexpr int PROJ_SCR_RES = 40, PROJ_SCR_LAM = 48, PROJ_SCR_N = 56;
@@ -602,8 +603,12 @@ __device__ __forceinline__ void elem_project_wave(const MechView& V, int npe, co
   }
   if (lane == 0) {
 #pragma unroll
-    for (int e = 0; e < PROJ_MMAX; ++e)
-      if (e < npe) scr[PROJ_SCR_RES + e] = v[e];
+    for (int e = 0; e < PROJ_MMAX; ++e) {
+      if (e < npe) {
+        scr[PROJ_SCR_RES + e] = v[e];
+        if (!(eb0[e] > PROJ_TRACE * bmax)) scr[e * (e + 1) / 2 + e] = 0.0;  // trace element: left out
+      }
+    }
     proj_solve_lds(scr, npe);
   }
   wave_lds_sync();
