@@ -668,7 +668,11 @@ void cko_lu_factor_batch(int n, int nsys, double* A, int* piv, int* info, int nt
 #define DGMAX 0.3
 #define RDIV 2.0
 #define MSBP 20
-#define MSBJ 50
+/* Jacobian refresh after at most 15 steps (CVODE's msbj, default 51): the stiff ignition runs converge with far
+ * fewer steps, RHS calls and Newton setups on a fresher J; priced by scripts/solver_knobs_oracle.py
+ * (profiles/r06w_solver_knobs_oracle.log: configs[2] -17 %, configs[4] -11 % modelled cycles, tau within 3e-5; 10 saves 2 % more on configs[2] but
+ * stalls one of the 35 tolerance-perturbed FORD runs of tests/test_ford.py) */
+#define MSBJ 15
 #define THRESH 1.5
 #define CORTES 0.1
 #define UROUND 2.220446049250313e-16

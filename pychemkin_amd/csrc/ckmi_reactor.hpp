@@ -27,7 +27,10 @@ constexpr double ETAMX1 = 10000.0, ETAMX2 = 10.0, ETAMX3 = 10.0, ETAMXF = 0.2, E
 constexpr double ADDON = 1e-6, BIAS1 = 6.0, BIAS2 = 6.0, BIAS3 = 10.0, ONEPSM = 1.000001;
 constexpr int SMALL_NST = 10, MXNCF = 10, MXNEF = 7, MXNEF1 = 3, SMALL_NEF = 2, LONG_WAIT = 10, MAXCOR = 3;
 constexpr double CRDOWN = 0.3, DGMAX = 0.3, RDIV = 2.0, THRESH = 1.5, CORTES = 0.1;
-constexpr int MSBP = 20, MSBJ = 50;
+// MSBJ: Jacobian refresh after at most 15 steps (CVODE's msbj, default 51), as oracle/ckoracle.c: on the stiff
+// ignition runs a fresher J saves more steps, RHS calls and Newton setups than its evaluations cost
+// (scripts/solver_knobs_oracle.py, profiles/r06w_solver_knobs_oracle.log)
+constexpr int MSBP = 20, MSBJ = 15;
 constexpr double UROUND = 2.220446049250313e-16, NNEG_TOL = 0.01;
 
 // Per-wave LDS slice (one reactor): concentrations, g/RT, h/RT, production and dwdot/dT
