@@ -23,7 +23,7 @@ import oracle.oracle as oo  # noqa: E402
 TMP = "/tmp/ckoracle_knobs"
 os.makedirs(TMP, exist_ok=True)
 src = open(os.path.join(ROOT, "oracle", "ckoracle.c")).read()
-for k in ("DGMAX", "MSBP", "MSBJ"):
+for k in ("DGMAX", "MSBP", "MSBJ", "MAXCOR", "CRDOWN", "RDIV"):
     src = re.sub(rf"^#define {k} (\S+)$", rf"#ifndef {k}\n#define {k} \1\n#endif", src, flags=re.M)
 open(os.path.join(TMP, "ck.c"), "w").write(src)
 open(os.path.join(TMP, "ckoracle.h"), "w").write(open(os.path.join(ROOT, "oracle", "ckoracle.h")).read())
