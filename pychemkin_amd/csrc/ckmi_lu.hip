@@ -197,6 +197,12 @@ __device__ __forceinline__ void panel_factor_reg(LuSmem<NB>& S, double* Pp, int 
 #pragma unroll
   for (int c = 0; c < TB; ++c) {
     const int col = r0 + c;
+    // identity padding (col >= n): the pivot is row col itself and every multiplier is 0 -- the step changes
+    // nothing, so it is skipped (wave-uniform branch; n = 161: 15 of the 176 column steps)
+    if (col >= n) {
+      pivr = lane == c ? col : pivr;
+      continue;
+    }
     // this lane's best active row: largest |a|, then the smallest position; its reciprocal is
     // taken now, beside the wave reduction, instead of after the pivot row arrives
     double best = -1.0, bval = 1.0;
